@@ -1,0 +1,799 @@
+/*
+ * oracle_index.c -- restatement of the index job (map + shuffle + reduce), its
+ * output bytes, and the query ranking.  TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Record split   XMLRecordReader.next / readUntilMatch
+ *                C/edu/umd/cloud9/collection/XMLInputFormat.java:110-143,173-198
+ * docid          TrecDocument.getDocid  C/edu/umd/cloud9/collection/trec/TrecDocument.java:76-89
+ * docno          TrecDocnoMapping.getDocno (Arrays.binarySearch) / readDocnoData
+ *                C/edu/umd/cloud9/collection/trec/TrecDocnoMapping.java:67-69,137-155
+ * map            TermKGramDocIndexer.MyMapper.map
+ *                C/sa/edu/kaust/indexing/TermKGramDocIndexer.java:84-90,119-160
+ * shuffle        [Hadoop] HashPartitioner on TermDF.hashCode (C/sa/edu/kaust/io/TermDF.java:79-81),
+ *                key order TermDF.compareTo (TermDF.java:64-70)
+ * reduce         TermKGramDocIndexer.MyReducer.reduce  TermKGramDocIndexer.java:168-213,
+ *                PostingWritable.compareTo  C/sa/edu/kaust/io/PostingWritable.java:57-59
+ * bytes          TermDF.write 50-56, ArrayListWritable.write
+ *                C/edu/umd/cloud9/io/array/ArrayListWritable.java:90-105, PostingWritable.write 46-49
+ * query          IntDocVectorsForwardIndex.rank / DocScore
+ *                C/sa/edu/kaust/fwindex/IntDocVectorsForwardIndex.java:192-223,329-371
+ *
+ * This is the "ref-faithful" restatement: every map-output record is
+ * materialised, sorted by string keys with a comparison merge sort, and reduced
+ * with the reference's two list sorts.  It is deliberately not fast.
+ */
+#include <limits.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+/* ------------------------------------------------------------------ */
+/* error reporting                                                      */
+static char g_err[256];
+const char *or_last_error(void) { return g_err; }
+
+/* ------------------------------------------------------------------ */
+/* record reader                                                        */
+
+/* readUntilMatch: advances *pos over bytes [.., n); returns 1 on full match.
+ * withinBlock: bytes are appended to the record (we track the span instead). */
+static int read_until_match(const uint8_t *b, size_t n, size_t *pos, size_t end, const char *m,
+                            int withinBlock) {
+  int ml = (int)strlen(m);
+  int i = 0;
+  for (;;) {
+    if (*pos >= n) {
+      (*pos)++;
+      return 0; /* b == -1: EOF (pos still incremented, as the reference does) */
+    }
+    int c = b[*pos];
+    (*pos)++;
+    if (c == (unsigned char)m[i]) {
+      i++;
+      if (i >= ml) return 1;
+    } else {
+      i = 0;
+    }
+    if (!withinBlock && i == 0 && *pos >= end) return 0;
+  }
+}
+
+typedef struct {
+  size_t off, len;
+} rec;
+
+/* Records of one split [start, end) in the XMLRecordReader order. */
+static int split_records(const uint8_t *b, size_t n, size_t start, size_t end, rec **out,
+                         int *nout) {
+  size_t pos = start;
+  int cap = 16, cnt = 0;
+  rec *r = (rec *)malloc(sizeof(rec) * cap);
+  while (pos < end) {
+    if (!read_until_match(b, n, &pos, end, "<DOC>", 0)) break;
+    size_t rs = pos - 5;
+    if (!read_until_match(b, n, &pos, end, "</DOC>", 1)) break;
+    if (cnt == cap) {
+      cap *= 2;
+      r = (rec *)realloc(r, sizeof(rec) * cap);
+    }
+    r[cnt].off = rs;
+    r[cnt].len = pos - rs;
+    cnt++;
+  }
+  *out = r;
+  *nout = cnt;
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* docno mapping                                                        */
+typedef struct {
+  jstr *ids; /* ids[0] = "" sentinel */
+  int n;     /* entries including sentinel */
+} mapping;
+
+static int read_u16be(const uint8_t *p) { return (p[0] << 8) | p[1]; }
+static int32_t read_i32be(const uint8_t *p) {
+  return (int32_t)(((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]);
+}
+
+/* DataInput.readUTF: modified UTF-8 -> UTF-16 */
+static int read_mutf8(const uint8_t *p, int len, jstr *out) {
+  out->n = 0;
+  int i = 0;
+  while (i < len) {
+    unsigned c = p[i];
+    if (c < 0x80) {
+      js_push(out, (uint16_t)c);
+      i++;
+    } else if ((c & 0xE0) == 0xC0) {
+      if (i + 1 >= len) return -1;
+      js_push(out, (uint16_t)(((c & 0x1F) << 6) | (p[i + 1] & 0x3F)));
+      i += 2;
+    } else if ((c & 0xF0) == 0xE0) {
+      if (i + 2 >= len) return -1;
+      js_push(out, (uint16_t)(((c & 0x0F) << 12) | ((p[i + 1] & 0x3F) << 6) | (p[i + 2] & 0x3F)));
+      i += 3;
+    } else {
+      return -1;
+    }
+  }
+  return 0;
+}
+
+static int load_mapping(const uint8_t *m, size_t n, mapping *mp) {
+  if (n < 4) {
+    snprintf(g_err, sizeof g_err, "mapping file too short");
+    return -1;
+  }
+  int cnt = read_i32be(m);
+  if (cnt < 0) {
+    snprintf(g_err, sizeof g_err, "negative mapping count");
+    return -1;
+  }
+  mp->n = cnt + 1;
+  mp->ids = (jstr *)calloc((size_t)mp->n, sizeof(jstr));
+  size_t p = 4;
+  for (int i = 1; i < mp->n; i++) {
+    if (p + 2 > n) {
+      snprintf(g_err, sizeof g_err, "truncated mapping file");
+      return -1;
+    }
+    int l = read_u16be(m + p);
+    p += 2;
+    if (p + (size_t)l > n) {
+      snprintf(g_err, sizeof g_err, "truncated mapping file");
+      return -1;
+    }
+    js_init(&mp->ids[i]);
+    if (read_mutf8(m + p, l, &mp->ids[i]) < 0) {
+      snprintf(g_err, sizeof g_err, "bad modified UTF-8 in mapping");
+      return -1;
+    }
+    p += (size_t)l;
+  }
+  js_init(&mp->ids[0]);
+  return 0;
+}
+
+/* Arrays.binarySearch(Object[], key) */
+static int get_docno(const mapping *mp, const uint16_t *k, int kn) {
+  int low = 0, high = mp->n - 1;
+  while (low <= high) {
+    int mid = (int)(((unsigned)low + (unsigned)high) >> 1);
+    int c = js_cmp(mp->ids[mid].p, mp->ids[mid].n, k, kn);
+    if (c < 0)
+      low = mid + 1;
+    else if (c > 0)
+      high = mid - 1;
+    else
+      return mid;
+  }
+  return -(low + 1);
+}
+
+/* TrecDocument.getDocid: trim(substring(indexOf("<DOCNO>")+7, indexOf("</DOCNO>", start))) */
+static int get_docid(const jstr *doc, jstr *id) {
+  static const char *o = "<DOCNO>", *c = "</DOCNO>";
+  int start = -1;
+  for (int i = 0; i + 7 <= doc->n && start < 0; i++) {
+    int k = 0;
+    while (k < 7 && doc->p[i + k] == (unsigned char)o[k]) k++;
+    if (k == 7) start = i;
+  }
+  if (start < 0) {
+    id->n = 0;
+    return 0;
+  }
+  int end = -1;
+  for (int i = start; i + 8 <= doc->n && end < 0; i++) {
+    int k = 0;
+    while (k < 8 && doc->p[i + k] == (unsigned char)c[k]) k++;
+    if (k == 8) end = i;
+  }
+  if (end < 0 || end < start + 7) {
+    snprintf(g_err, sizeof g_err, "StringIndexOutOfBoundsException in getDocid (no </DOCNO>)");
+    return -1;
+  }
+  int b = start + 7, e = end;
+  while (b < e && doc->p[b] <= 0x20) b++;
+  while (e > b && doc->p[e - 1] <= 0x20) e--;
+  js_set(id, doc->p + b, e - b);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* map output records                                                   */
+typedef struct {
+  const jstr *gram; /* K strings (points into a doc's token array), or NULL for " " */
+  int docno, tf;
+  int part;
+} mrec;
+
+typedef struct {
+  jstr_list toks; /* stems of one record */
+} docbuf;
+
+static jstr SPACE_KEY; /* " " */
+static int g_K;
+
+static const jstr *gram_at(const mrec *r, int i) { return r->gram ? &r->gram[i] : &SPACE_KEY; }
+static int gram_len(const mrec *r) { return r->gram ? g_K : 1; }
+
+/* TermDF.compareTo */
+static int key_cmp(const mrec *a, const mrec *b) {
+  int al = gram_len(a), bl = gram_len(b);
+  for (int i = 0; i < al && i < bl; i++) {
+    const jstr *x = gram_at(a, i), *y = gram_at(b, i);
+    int r = js_cmp(x->p, x->n, y->p, y->n);
+    if (r) return r;
+  }
+  return al - bl;
+}
+
+/* Arrays.hashCode(Object[]) of the k-gram, HashPartitioner */
+static int partition_of(const mrec *r, int R) {
+  uint32_t h = 1;
+  for (int i = 0; i < gram_len(r); i++) {
+    const jstr *s = gram_at(r, i);
+    h = 31u * h + (uint32_t)js_hash(s->p, s->n);
+  }
+  return (int)(((int32_t)h & 0x7fffffff) % R);
+}
+
+static int mrec_cmp(const mrec *a, const mrec *b) {
+  if (a->part != b->part) return a->part - b->part;
+  return key_cmp(a, b);
+}
+
+/* stable merge sort (the shuffle's order within a key does not matter for the
+ * real terms; for " " we keep emission order, which the tests compare as a multiset) */
+static void msort(mrec *a, mrec *tmp, size_t n) {
+  if (n < 2) return;
+  size_t h = n / 2;
+  msort(a, tmp, h);
+  msort(a + h, tmp, n - h);
+  if (mrec_cmp(&a[h - 1], &a[h]) <= 0) return;
+  size_t i = 0, j = h, k = 0;
+  while (i < h && j < n) tmp[k++] = (mrec_cmp(&a[j], &a[i]) < 0) ? a[j++] : a[i++];
+  while (i < h) tmp[k++] = a[i++];
+  while (j < n) tmp[k++] = a[j++];
+  memcpy(a, tmp, n * sizeof(mrec));
+}
+
+typedef struct {
+  int docno, tf;
+} posting;
+
+/* ------------------------------------------------------------------ */
+/* index                                                                */
+typedef struct {
+  jstr *gram; /* K strings (or 1 for " ") */
+  int k;
+  int df_field;      /* stored TermDF.df */
+  posting *post;     /* reduce output order */
+  int npost;
+  int part;
+} term_rec;
+
+typedef struct or_index {
+  int K, R;
+  int N;             /* df of " " = number of records mapped */
+  term_rec *terms;   /* global key order (" " first) */
+  int nterms;
+  uint8_t **part_bytes;
+  size_t *part_len;
+} or_index;
+
+static void stable_sort_postings(posting *a, posting *tmp, int n, int by_tf) {
+  /* Collections.sort is a stable merge sort; take left while compare(left,right) <= 0.
+   * reducer comparator: o1.docNo - o2.docNo;  PostingWritable.compareTo: o.tf - tf */
+  if (n < 2) return;
+  int h = n / 2;
+  stable_sort_postings(a, tmp, h, by_tf);
+  stable_sort_postings(a + h, tmp, n - h, by_tf);
+  int i = 0, j = h, k = 0;
+  while (i < h && j < n) {
+    int32_t c = by_tf ? (int32_t)((uint32_t)a[j].tf - (uint32_t)a[i].tf)
+                      : (int32_t)((uint32_t)a[i].docno - (uint32_t)a[j].docno);
+    tmp[k++] = (c <= 0) ? a[i++] : a[j++];
+  }
+  while (i < h) tmp[k++] = a[i++];
+  while (j < n) tmp[k++] = a[j++];
+  memcpy(a, tmp, (size_t)n * sizeof(posting));
+}
+
+static void put_i32(uint8_t **p, int32_t v) {
+  uint32_t u = (uint32_t)v;
+  (*p)[0] = (uint8_t)(u >> 24);
+  (*p)[1] = (uint8_t)(u >> 16);
+  (*p)[2] = (uint8_t)(u >> 8);
+  (*p)[3] = (uint8_t)u;
+  *p += 4;
+}
+
+static const char *CLASSNAME = "sa.edu.kaust.io.PostingWritable";
+
+static size_t key_bytes(const term_rec *t) {
+  size_t s = 8;
+  for (int i = 0; i < t->k; i++) s += 2 + (size_t)mutf8_len(t->gram[i].p, t->gram[i].n);
+  return s;
+}
+static size_t val_bytes(const term_rec *t) {
+  return 4 + (t->npost > 0 ? 2 + strlen(CLASSNAME) + 8 * (size_t)t->npost : 0);
+}
+
+/* SequenceFile record framing: int32 recLen(key+value), int32 keyLen, key, value */
+static void serialize(or_index *ix) {
+  ix->part_bytes = (uint8_t **)calloc((size_t)ix->R, sizeof(uint8_t *));
+  ix->part_len = (size_t *)calloc((size_t)ix->R, sizeof(size_t));
+  for (int t = 0; t < ix->nterms; t++) {
+    term_rec *tr = &ix->terms[t];
+    ix->part_len[tr->part] += 8 + key_bytes(tr) + val_bytes(tr);
+  }
+  uint8_t **cur = (uint8_t **)calloc((size_t)ix->R, sizeof(uint8_t *));
+  for (int r = 0; r < ix->R; r++) cur[r] = ix->part_bytes[r] = (uint8_t *)malloc(ix->part_len[r] + 1);
+  for (int t = 0; t < ix->nterms; t++) {
+    term_rec *tr = &ix->terms[t];
+    uint8_t **p = &cur[tr->part];
+    size_t kb = key_bytes(tr), vb = val_bytes(tr);
+    put_i32(p, (int32_t)(kb + vb));
+    put_i32(p, (int32_t)kb);
+    put_i32(p, tr->k);
+    for (int i = 0; i < tr->k; i++) {
+      int l = mutf8_len(tr->gram[i].p, tr->gram[i].n);
+      (*p)[0] = (uint8_t)(l >> 8);
+      (*p)[1] = (uint8_t)l;
+      *p += 2;
+      *p += mutf8_encode(tr->gram[i].p, tr->gram[i].n, *p);
+    }
+    put_i32(p, tr->df_field);
+    put_i32(p, tr->npost);
+    if (tr->npost > 0) {
+      size_t cl = strlen(CLASSNAME);
+      (*p)[0] = (uint8_t)(cl >> 8);
+      (*p)[1] = (uint8_t)cl;
+      *p += 2;
+      memcpy(*p, CLASSNAME, cl);
+      *p += cl;
+      for (int i = 0; i < tr->npost; i++) {
+        put_i32(p, tr->post[i].docno);
+        put_i32(p, tr->post[i].tf);
+      }
+    }
+  }
+  free(cur);
+}
+
+void or_index_free(or_index *ix) {
+  if (!ix) return;
+  for (int t = 0; t < ix->nterms; t++) {
+    for (int i = 0; i < ix->terms[t].k; i++) js_free(&ix->terms[t].gram[i]);
+    free(ix->terms[t].gram);
+    free(ix->terms[t].post);
+  }
+  free(ix->terms);
+  if (ix->part_bytes)
+    for (int r = 0; r < ix->R; r++) free(ix->part_bytes[r]);
+  free(ix->part_bytes);
+  free(ix->part_len);
+  free(ix);
+}
+
+/*
+ * Build the index.  splits: n_splits+1 byte offsets (split i = [s[i], s[i+1]));
+ * NULL means one split over the whole corpus (Hadoop local mode, one map task).
+ */
+or_index *or_build_index(const uint8_t *corpus, size_t n, const uint8_t *map_bytes, size_t map_len,
+                         int K, int R, const uint64_t *splits, int n_splits) {
+  g_err[0] = 0;
+  if (K < 1 || R < 1) {
+    snprintf(g_err, sizeof g_err, "bad K/R");
+    return NULL;
+  }
+  mapping mp;
+  if (load_mapping(map_bytes, map_len, &mp) < 0) return NULL;
+  js_init(&SPACE_KEY);
+  js_set_ascii(&SPACE_KEY, " ");
+  g_K = K;
+
+  uint64_t one_split[2] = {0, (uint64_t)n};
+  if (!splits) {
+    splits = one_split;
+    n_splits = 1;
+  }
+
+  size_t mcap = 1024, mn = 0;
+  mrec *m = (mrec *)malloc(sizeof(mrec) * mcap);
+  size_t dcap = 64, dn = 0;
+  docbuf *docs = (docbuf *)malloc(sizeof(docbuf) * dcap);
+  int N = 0;
+  jstr text, id;
+  js_init(&text);
+  js_init(&id);
+  int fail = 0;
+
+  for (int s = 0; s < n_splits && !fail; s++) {
+    rec *recs;
+    int nrec;
+    split_records(corpus, n, (size_t)splits[s], (size_t)splits[s + 1], &recs, &nrec);
+    posting shared = {0, 0}; /* MyMapper.posting, fresh per map task */
+    for (int r = 0; r < nrec; r++) {
+      utf8_to_utf16(corpus + recs[r].off, recs[r].len, &text);
+      if (get_docid(&text, &id) < 0) {
+        fail = 1;
+        break;
+      }
+      int docno = get_docno(&mp, id.p, id.n);
+      N++;
+      if (mn + 2 > mcap) {
+        mcap *= 2;
+        m = (mrec *)realloc(m, sizeof(mrec) * mcap);
+      }
+      m[mn].gram = NULL;
+      m[mn].docno = shared.docno;
+      m[mn].tf = shared.tf;
+      mn++;
+      if (dn == dcap) {
+        dcap *= 2;
+        docs = (docbuf *)realloc(docs, sizeof(docbuf) * dcap);
+      }
+      jl_init(&docs[dn].toks);
+      or_process_content(text.p, text.n, &docs[dn].toks);
+      shared.docno = docno;
+      shared.tf = 1;
+      int T = docs[dn].toks.n;
+      for (int i = 0; i + K <= T; i++) {
+        if (mn + 1 > mcap) {
+          mcap *= 2;
+          m = (mrec *)realloc(m, sizeof(mrec) * mcap);
+        }
+        m[mn].gram = &docs[dn].toks.v[i]; /* toks.v is final once processContent returned */
+        m[mn].docno = docno;
+        m[mn].tf = 1;
+        mn++;
+      }
+      dn++;
+    }
+    free(recs);
+  }
+  js_free(&text);
+  js_free(&id);
+  if (fail) {
+    for (size_t d = 0; d < dn; d++) jl_free(&docs[d].toks);
+    free(docs);
+    free(m);
+    free(mp.ids);
+    return NULL;
+  }
+  for (size_t i = 0; i < mn; i++) m[i].part = partition_of(&m[i], R);
+
+  mrec *tmp = (mrec *)malloc(sizeof(mrec) * (mn ? mn : 1));
+  msort(m, tmp, mn);
+  free(tmp);
+
+  or_index *ix = (or_index *)calloc(1, sizeof(or_index));
+  ix->K = K;
+  ix->R = R;
+  ix->N = N;
+  /* reduce, per partition, groups of equal keys */
+  size_t tcap = 1024;
+  ix->terms = (term_rec *)malloc(sizeof(term_rec) * tcap);
+  for (size_t i = 0; i < mn;) {
+    size_t j = i + 1;
+    while (j < mn && m[j].part == m[i].part && key_cmp(&m[j], &m[i]) == 0) j++;
+    if ((size_t)ix->nterms == tcap) {
+      tcap *= 2;
+      ix->terms = (term_rec *)realloc(ix->terms, sizeof(term_rec) * tcap);
+    }
+    term_rec *tr = &ix->terms[ix->nterms++];
+    tr->k = gram_len(&m[i]);
+    tr->gram = (jstr *)calloc((size_t)tr->k, sizeof(jstr));
+    for (int g = 0; g < tr->k; g++) js_set(&tr->gram[g], gram_at(&m[i], g)->p, gram_at(&m[i], g)->n);
+    tr->part = m[i].part;
+    int cnt = (int)(j - i);
+    posting *res = (posting *)malloc(sizeof(posting) * (size_t)cnt);
+    for (int q = 0; q < cnt; q++) {
+      res[q].docno = m[i + q].docno;
+      res[q].tf = m[i + q].tf;
+    }
+    if (m[i].gram == NULL) { /* doc counter: term.getK_gram()[0].equals(" ") */
+      tr->df_field = cnt;
+      tr->post = res;
+      tr->npost = cnt;
+    } else {
+      posting *tmpp = (posting *)malloc(sizeof(posting) * (size_t)cnt);
+      stable_sort_postings(res, tmpp, cnt, 0);
+      int w = 0;
+      for (int q = 0; q < cnt; q++) {
+        int sum = res[q].tf;
+        int r = q + 1;
+        while (r < cnt && res[r].docno == res[q].docno) sum += res[r++].tf;
+        res[w].docno = res[q].docno;
+        res[w].tf = sum;
+        w++;
+        q = r - 1;
+      }
+      stable_sort_postings(res, tmpp, w, 1);
+      free(tmpp);
+      tr->df_field = 1; /* T1: reducer never updates df of real terms */
+      tr->post = res;
+      tr->npost = w;
+    }
+    i = j;
+  }
+  free(m);
+  for (size_t d = 0; d < dn; d++) jl_free(&docs[d].toks);
+  free(docs);
+  for (int i = 0; i < mp.n; i++) js_free(&mp.ids[i]);
+  free(mp.ids);
+  serialize(ix);
+  return ix;
+}
+
+/* ---- accessors (ctypes) ---- */
+int or_index_nterms(const or_index *ix) { return ix->nterms; }
+int or_index_N(const or_index *ix) { return ix->N; }
+size_t or_index_part_len(const or_index *ix, int part) { return ix->part_len[part]; }
+const uint8_t *or_index_part_bytes(const or_index *ix, int part) { return ix->part_bytes[part]; }
+int or_index_term_part(const or_index *ix, int t) { return ix->terms[t].part; }
+int or_index_term_npost(const or_index *ix, int t) { return ix->terms[t].npost; }
+int or_index_term_df_field(const or_index *ix, int t) { return ix->terms[t].df_field; }
+int or_index_term_k(const or_index *ix, int t) { return ix->terms[t].k; }
+/* modified-UTF-8 bytes of gram element g into buf (cap bytes); returns length */
+int or_index_term_gram(const or_index *ix, int t, int g, uint8_t *buf, int cap) {
+  const jstr *s = &ix->terms[t].gram[g];
+  int l = mutf8_len(s->p, s->n);
+  if (l > cap) return -l;
+  mutf8_encode(s->p, s->n, buf);
+  return l;
+}
+void or_index_term_postings(const or_index *ix, int t, int32_t *docno, int32_t *tf) {
+  for (int i = 0; i < ix->terms[t].npost; i++) {
+    docno[i] = ix->terms[t].post[i].docno;
+    tf[i] = ix->terms[t].post[i].tf;
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* query: rank()                                                        */
+
+static int find_term(const or_index *ix, const uint16_t *w, int n) {
+  /* IntDocVectorsForwardIndex keys the forward index by k_gram[0] (T11) */
+  for (int t = 0; t < ix->nterms; t++) {
+    const jstr *g = &ix->terms[t].gram[0];
+    if (g->n == n && (n == 0 || memcmp(g->p, w, (size_t)n * 2) == 0)) return t;
+  }
+  return -1;
+}
+
+typedef struct {
+  int docId;
+  double score;
+  int first; /* first-encounter index */
+} docscore;
+
+/* DocScore.compareTo: (int)Math.ceil(o.score - score) */
+static int ds_cmp_ref(const docscore *a, const docscore *b) {
+  double d = ceil(b->score - a->score);
+  if (d != d) return 0;
+  if (d >= 2147483647.0) return INT_MAX;
+  if (d <= -2147483648.0) return INT_MIN;
+  return (int)d;
+}
+
+/* Java 6 Arrays.mergeSort(Object[] src, Object[] dest, low, high, off) */
+static void legacy_merge_sort(docscore *src, docscore *dest, int low, int high, int off) {
+  int length = high - low;
+  if (length < 7) {
+    for (int i = low; i < high; i++)
+      for (int j = i; j > low && ds_cmp_ref(&dest[j - 1], &dest[j]) > 0; j--) {
+        docscore t = dest[j];
+        dest[j] = dest[j - 1];
+        dest[j - 1] = t;
+      }
+    return;
+  }
+  int destLow = low, destHigh = high;
+  low += off;
+  high += off;
+  int mid = (int)(((unsigned)low + (unsigned)high) >> 1);
+  legacy_merge_sort(dest, src, low, mid, -off);
+  legacy_merge_sort(dest, src, mid, high, -off);
+  if (ds_cmp_ref(&src[mid - 1], &src[mid]) <= 0) {
+    memcpy(dest + destLow, src + low, (size_t)length * sizeof(docscore));
+    return;
+  }
+  for (int i = destLow, p = low, q = mid; i < destHigh; i++) {
+    if (q >= high || (p < mid && ds_cmp_ref(&src[p], &src[q]) <= 0))
+      dest[i] = src[p++];
+    else
+      dest[i] = src[q++];
+  }
+}
+
+static int ds_cmp_docno(const void *x, const void *y) {
+  const docscore *a = (const docscore *)x, *b = (const docscore *)y;
+  if (a->score > b->score) return -1;
+  if (a->score < b->score) return 1;
+  return (a->docId > b->docId) - (a->docId < b->docId);
+}
+static int ds_cmp_first(const void *x, const void *y) {
+  const docscore *a = (const docscore *)x, *b = (const docscore *)y;
+  if (a->score > b->score) return -1;
+  if (a->score < b->score) return 1;
+  return a->first - b->first;
+}
+
+/*
+ * Score one query (terms as UTF-16 strings already tokenized, in token order).
+ * idf_mode: 0 = reference (stored key df, T1/T2), 1 = true df (postings length), int division both.
+ * order: 0 = score desc / docno asc (north-star tie-break),
+ *        1 = Java 6 Collections.sort with the reference DocScore comparator,
+ *        2 = score desc / first-encounter (stable exact ties).
+ * Returns number of results written (<= k); scores/docnos out.
+ */
+int or_query(const or_index *ix, const uint16_t *const *terms, const int *lens, int nterms, int k,
+             int idf_mode, int order, int32_t *out_docno, double *out_score) {
+  int cap = 1024, n = 0;
+  docscore *sc = (docscore *)malloc(sizeof(docscore) * cap);
+  int N = ix->N;
+  for (int qi = 0; qi < nterms; qi++) {
+    int t = find_term(ix, terms[qi], lens[qi]);
+    if (t < 0) continue; /* getValue: unknown term silently skipped */
+    const term_rec *tr = &ix->terms[t];
+    int df = idf_mode == 0 ? tr->df_field : tr->npost;
+    double idf = log10((double)(N / df));
+    for (int p = 0; p < tr->npost; p++) {
+      int d = tr->post[p].docno;
+      int idx = -1;
+      for (int s = 0; s < n; s++) /* scores.indexOf (T6) */
+        if (sc[s].docId == d) {
+          idx = s;
+          break;
+        }
+      if (idx < 0) {
+        if (n == cap) {
+          cap *= 2;
+          sc = (docscore *)realloc(sc, sizeof(docscore) * cap);
+        }
+        sc[n].docId = d;
+        sc[n].score = 0.0;
+        sc[n].first = n;
+        idx = n++;
+      }
+      double w = (1.0 + log((double)tr->post[p].tf)) * idf;
+      sc[idx].score += w;
+    }
+  }
+  if (order == 1) {
+    docscore *aux = (docscore *)malloc(sizeof(docscore) * (n ? n : 1));
+    memcpy(aux, sc, sizeof(docscore) * n);
+    legacy_merge_sort(aux, sc, 0, n, 0);
+    free(aux);
+  } else {
+    qsort(sc, (size_t)n, sizeof(docscore), order == 2 ? ds_cmp_first : ds_cmp_docno);
+  }
+  int r = n < k ? n : k;
+  for (int i = 0; i < r; i++) {
+    out_docno[i] = sc[i].docId;
+    out_score[i] = sc[i].score;
+  }
+  free(sc);
+  return r;
+}
+
+/* ---- tokenizer / stemmer entry points on UTF-8 (ctypes) ---- */
+/* processContent on UTF-8 text; tokens written as modified UTF-8, each prefixed by u16 length. */
+int or_process_content_utf8(const uint8_t *b, size_t n, uint8_t *out, size_t cap, int *ntok) {
+  jstr t;
+  js_init(&t);
+  utf8_to_utf16(b, n, &t);
+  jstr_list l;
+  jl_init(&l);
+  or_process_content(t.p, t.n, &l);
+  size_t k = 0;
+  for (int i = 0; i < l.n; i++) {
+    int ml = mutf8_len(l.v[i].p, l.v[i].n);
+    if (k + 2 + (size_t)ml > cap) {
+      jl_free(&l);
+      js_free(&t);
+      return -1;
+    }
+    out[k] = (uint8_t)(ml >> 8);
+    out[k + 1] = (uint8_t)ml;
+    mutf8_encode(l.v[i].p, l.v[i].n, out + k + 2);
+    k += 2 + (size_t)ml;
+  }
+  *ntok = l.n;
+  jl_free(&l);
+  js_free(&t);
+  return (int)k;
+}
+
+/* TagTokenizer terms only (before stopwords/stemming). Same output format. */
+int or_tag_tokenize_utf8(const uint8_t *b, size_t n, uint8_t *out, size_t cap, int *ntok) {
+  jstr t;
+  js_init(&t);
+  utf8_to_utf16(b, n, &t);
+  jstr_list l;
+  jl_init(&l);
+  or_tag_tokenize(t.p, t.n, &l);
+  size_t k = 0;
+  for (int i = 0; i < l.n; i++) {
+    int ml = mutf8_len(l.v[i].p, l.v[i].n);
+    if (k + 2 + (size_t)ml > cap) {
+      jl_free(&l);
+      js_free(&t);
+      return -1;
+    }
+    out[k] = (uint8_t)(ml >> 8);
+    out[k + 1] = (uint8_t)ml;
+    mutf8_encode(l.v[i].p, l.v[i].n, out + k + 2);
+    k += 2 + (size_t)ml;
+  }
+  *ntok = l.n;
+  jl_free(&l);
+  js_free(&t);
+  return (int)k;
+}
+
+/* stem an ASCII/UTF-8 word; result as modified UTF-8 */
+int or_stem_utf8(const uint8_t *b, size_t n, uint8_t *out, size_t cap) {
+  jstr w, s;
+  js_init(&w);
+  js_init(&s);
+  utf8_to_utf16(b, n, &w);
+  or_stem_js(w.p, w.n, &s);
+  int ml = mutf8_len(s.p, s.n);
+  if ((size_t)ml > cap) return -1;
+  mutf8_encode(s.p, s.n, out);
+  js_free(&w);
+  js_free(&s);
+  return ml;
+}
+
+int or_is_stopword_utf8(const uint8_t *b, size_t n) {
+  jstr w;
+  js_init(&w);
+  utf8_to_utf16(b, n, &w);
+  int r = or_is_stopword(w.p, w.n);
+  js_free(&w);
+  return r;
+}
+
+/* query from UTF-8 strings of (already processed) terms, NUL-separated list */
+int or_query_utf8(const or_index *ix, const uint8_t *terms_blob, const int *offs, int nterms, int k,
+                  int idf_mode, int order, int32_t *out_docno, double *out_score) {
+  uint16_t **tp = (uint16_t **)malloc(sizeof(uint16_t *) * (nterms ? nterms : 1));
+  int *tl = (int *)malloc(sizeof(int) * (nterms ? nterms : 1));
+  jstr *tmp = (jstr *)calloc((size_t)(nterms ? nterms : 1), sizeof(jstr));
+  for (int i = 0; i < nterms; i++) {
+    utf8_to_utf16(terms_blob + offs[i], (size_t)(offs[i + 1] - offs[i]), &tmp[i]);
+    tp[i] = tmp[i].p;
+    tl[i] = tmp[i].n;
+  }
+  int r = or_query(ix, (const uint16_t *const *)tp, tl, nterms, k, idf_mode, order, out_docno,
+                   out_score);
+  for (int i = 0; i < nterms; i++) js_free(&tmp[i]);
+  free(tmp);
+  free(tp);
+  free(tl);
+  return r;
+}
+
+/* record split only: returns count; offsets/lengths into caller arrays (cap entries) */
+int or_split_records(const uint8_t *b, size_t n, uint64_t *off, uint64_t *len, int cap) {
+  rec *r;
+  int nr;
+  split_records(b, n, 0, n, &r, &nr);
+  for (int i = 0; i < nr && i < cap; i++) {
+    off[i] = r[i].off;
+    len[i] = r[i].len;
+  }
+  free(r);
+  return nr;
+}

@@ -1,0 +1,165 @@
+"""ctypes binding of the CPU oracle (oracle/build/liboracle.so).
+
+Test infrastructure only: the oracle is the checker, never the product.
+"""
+import ctypes as C
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        L = C.CDLL(LIB_PATH)
+        L.or_process_content_utf8.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_int)]
+        L.or_tag_tokenize_utf8.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_int)]
+        L.or_stem_utf8.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        L.or_is_stopword_utf8.argtypes = [C.c_char_p, C.c_size_t]
+        L.or_build_index.restype = C.c_void_p
+        L.or_build_index.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_int, C.c_int,
+                                     C.c_void_p, C.c_int]
+        L.or_index_free.argtypes = [C.c_void_p]
+        L.or_index_nterms.argtypes = [C.c_void_p]
+        L.or_index_N.argtypes = [C.c_void_p]
+        L.or_index_part_len.argtypes = [C.c_void_p, C.c_int]
+        L.or_index_part_len.restype = C.c_size_t
+        L.or_index_part_bytes.argtypes = [C.c_void_p, C.c_int]
+        L.or_index_part_bytes.restype = C.c_void_p
+        for f in ("or_index_term_part", "or_index_term_npost", "or_index_term_df_field", "or_index_term_k"):
+            getattr(L, f).argtypes = [C.c_void_p, C.c_int]
+        L.or_index_term_gram.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int]
+        L.or_index_term_postings.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.or_query_utf8.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.c_void_p, C.c_void_p]
+        L.or_last_error.restype = C.c_char_p
+        L.or_split_records.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]
+        _lib = L
+    return _lib
+
+
+def _decode_toks(buf, n, ntok):
+    out, k = [], 0
+    for _ in range(ntok):
+        ln = (buf[k] << 8) | buf[k + 1]
+        out.append(bytes(buf[k + 2:k + 2 + ln]).decode("utf-8", "surrogatepass"))
+        k += 2 + ln
+    return out
+
+
+def _tok_call(fn, text):
+    b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+    cap = 8 * len(b) + 64
+    buf = (C.c_ubyte * cap)()
+    nt = C.c_int(0)
+    r = fn(b, len(b), buf, cap, C.byref(nt))
+    assert r >= 0
+    return _decode_toks(buf, r, nt.value)
+
+
+def process_content(text):
+    """GalagoTokenizer.processContent"""
+    return _tok_call(lib().or_process_content_utf8, text)
+
+
+def tag_tokenize(text):
+    """TagTokenizer.tokenize(text).terms"""
+    return _tok_call(lib().or_tag_tokenize_utf8, text)
+
+
+def stem(word):
+    b = word.encode("utf-8")
+    buf = (C.c_ubyte * (4 * len(b) + 16))()
+    r = lib().or_stem_utf8(b, len(b), buf, len(buf))
+    return bytes(buf[:r]).decode("utf-8")
+
+
+def is_stopword(word):
+    b = word.encode("utf-8")
+    return bool(lib().or_is_stopword_utf8(b, len(b)))
+
+
+def split_records(corpus):
+    cap = corpus.count(b"<DOC>") + 1
+    off = (C.c_uint64 * cap)()
+    ln = (C.c_uint64 * cap)()
+    n = lib().or_split_records(corpus, len(corpus), off, ln, cap)
+    return [(off[i], ln[i]) for i in range(n)]
+
+
+class OracleIndex:
+    """Result of the ref-faithful index job (terms in (partition, key) order)."""
+
+    def __init__(self, corpus, mapping, K=1, R=1, splits=None):
+        L = lib()
+        sp = None
+        nsp = 0
+        if splits is not None:
+            arr = (C.c_uint64 * len(splits))(*splits)
+            sp, nsp = arr, len(splits) - 1
+        self._h = L.or_build_index(corpus, len(corpus), mapping, len(mapping), K, R, sp, nsp)
+        if not self._h:
+            raise RuntimeError(L.or_last_error().decode())
+        self.K, self.R = K, R
+        self.N = L.or_index_N(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().or_index_free(self._h)
+            self._h = None
+
+    def partition_bytes(self, part):
+        L = lib()
+        n = L.or_index_part_len(self._h, part)
+        p = L.or_index_part_bytes(self._h, part)
+        return C.string_at(p, n) if n else b""
+
+    def terms(self):
+        """list of (gram tuple, part, df_field, [(docno, tf), ...])"""
+        L = lib()
+        out = []
+        buf = (C.c_ubyte * 70000)()
+        for t in range(L.or_index_nterms(self._h)):
+            k = L.or_index_term_k(self._h, t)
+            gram = []
+            for g in range(k):
+                ln = L.or_index_term_gram(self._h, t, g, buf, len(buf))
+                gram.append(bytes(buf[:ln]).decode("utf-8", "surrogatepass"))
+            n = L.or_index_term_npost(self._h, t)
+            d = (C.c_int32 * max(n, 1))()
+            f = (C.c_int32 * max(n, 1))()
+            L.or_index_term_postings(self._h, t, d, f)
+            out.append((tuple(gram), L.or_index_term_part(self._h, t), L.or_index_term_df_field(self._h, t),
+                        [(d[i], f[i]) for i in range(n)]))
+        return out
+
+    def query(self, terms, k=10, idf_mode=0, order=0):
+        """rank() over already-processed query terms; order 0 docno tie-break,
+        1 Java-6 Collections.sort with DocScore comparator, 2 first-encounter."""
+        bs = [t.encode("utf-8") for t in terms]
+        blob = b"".join(bs)
+        offs = [0]
+        for b in bs:
+            offs.append(offs[-1] + len(b))
+        o = (C.c_int * len(offs))(*offs)
+        dn = (C.c_int32 * max(k, 1))()
+        sc = (C.c_double * max(k, 1))()
+        r = lib().or_query_utf8(self._h, blob, o, len(terms), k, idf_mode, order, dn, sc)
+        return [dn[i] for i in range(r)], [sc[i] for i in range(r)]
+
+
+def write_mapping(docids):
+    """TrecDocnoMapping.writeDocnoData format: int32 N, N x writeUTF (sorted docids)."""
+    import struct
+    out = [struct.pack(">i", len(docids))]
+    for d in docids:
+        b = d.encode("utf-8")
+        out.append(struct.pack(">H", len(b)) + b)
+    return b"".join(out)
