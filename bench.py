@@ -1,0 +1,255 @@
+"""bench.py -- index build GB/s (+ top-10 QPS) on MI355X, BASELINE.json configs.
+
+Workload (N=1): configs[1] "Synthetic Zipfian corpus 1M docs x ~500 tokens, 1
+MI355X: index build + TF-IDF" (N=1e6, doc length U[400,600],
+V_w=2^20, Zipf s=1, seed 42).  One step = one full index build + TF-IDF weight
+pass over the HBM-resident corpus (sme_build_index_device): record split, docno
+lookup, tokenize/stop/stem, per-record tf aggregation, term sort, weights, and
+the reduce-order (tf desc, docno asc) postings.  The corpus is generated on the
+device before the timed region.  After the timed build steps, the c3 query batch
+(100k queries, 2-8 terms drawn by df, top-10) is timed the same way and reported
+in "query".
+
+Multi-GPU (torchrun, one rank per GPU, RCCL): weak scaling -- every rank owns a
+contiguous shard of N docs (docids offset by rank), builds its local index, and
+the global document count is all-reduced in every step (reference-mode idf =
+log10(N_global)).  Queries are run on every shard and the per-shard top-k lists
+are all-gathered and merged.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes as C
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "simple-mapreduce-search-engine-information-retrieval-_amd"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--docs", type=int, default=1_000_000, help="docs per GPU")
+    p.add_argument("--vocab", type=int, default=1 << 20)
+    p.add_argument("--queries", type=int, default=100_000)
+    p.add_argument("--cpu-docs", type=int, default=8000, help="docs in the CPU-baseline sample (0 = skip)")
+    p.add_argument("--no-query", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    sme = importlib.import_module(PKG)
+    synth = importlib.import_module(PKG + ".synth")
+    L = sme.lib()
+
+    # ---- corpus shard in HBM (untimed) ----
+    seed = 42
+    blob, voff = synth.make_vocab(a.vocab, seed)
+    cdf = synth.zipf_cdf(a.vocab, 1.0)
+    L.sme_synth_corpus.argtypes = [C.c_int, C.c_char_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int64,
+                                   C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    L.sme_synth_free.argtypes = [C.c_void_p]
+    d_corpus, nbytes = C.c_void_p(), C.c_size_t()
+    d0 = rank * a.docs
+    rc = L.sme_synth_corpus(local, blob, voff.ctypes.data, a.vocab, cdf.ctypes.data, a.docs, d0, seed, 400, 600,
+                            C.byref(d_corpus), C.byref(nbytes))
+    assert rc == 0, rc
+    nbytes = nbytes.value
+    # every rank loads the global mapping (all world*docs docids), so docnos are global
+    mapping = synth.mapping_bytes(a.docs * world)
+    ctx = sme.Context(k=1, num_partitions=1, device=local)
+    ctx.load_docno_mapping(mapping)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    n_tensor = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+    def step():
+        ix = ctx.build_device(d_corpus.value, nbytes, stream)
+        if dist is not None:
+            n_tensor.fill_(ix.N)
+            dist.all_reduce(n_tensor)
+            ix.reweight(int(n_tensor.item()), None, stream)  # idf = log10(N_global)
+        return ix
+
+    ix = None
+    for _ in range(a.warmup):
+        if ix is not None:
+            ix.close()
+        ix = step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        if ix is not None:
+            ix.close()
+        ix = step()
+    barrier()
+    dt = (time.perf_counter() - t0) / a.steps
+    prof = ctx.last_build_profile()
+    N, V, P = ix.N, ix.V, ix.P
+    t_max = dt
+    tot_bytes = nbytes
+    if dist is not None:
+        tt = torch.tensor([dt, float(nbytes), float(N), float(V), float(P)], dtype=torch.float64, device="cuda")
+        ts = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(ts, tt)
+        ts = torch.stack(ts).cpu().numpy()
+        t_max = float(ts[:, 0].max())
+        tot_bytes = float(ts[:, 1].sum())
+    gbs = tot_bytes / t_max / 1e9
+    alg_bytes = nbytes + 8 * P + 8 * (V + 1)  # A_build = B + 8P + 8(V+1) per GPU
+    achieved = alg_bytes / dt / 1e9
+
+    # ---- queries (c3) ----
+    query = None
+    if not a.no_query and a.queries > 0:
+        query = run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier)
+
+    result = {
+        "metric": "index build GB/s of text (top-10 queries/sec in 'query')",
+        "value": round(gbs, 4),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(t_max * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8 text / int32 postings / f64 weights",
+        "data": "synthetic (device-generated Zipfian TREC corpus, seed 42)",
+        "config": {"workload": "c2: %d docs/GPU x U[400,600] tokens, V_w=%d, Zipf s=1, K=1 index + TF-IDF"
+                               % (a.docs, a.vocab), "docs_per_gpu": a.docs, "text_bytes_per_gpu": nbytes,
+                   "N": N, "V": V, "P": P, "parallelism": "doc-sharded x%d" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "what": "whole build step: algorithmic bytes B + 8P + 8(V+1) per GPU / step time"},
+        "stage_ms": prof,
+    }
+    if query is not None:
+        result["query"] = query
+    if rank == 0 and a.cpu_docs > 0:
+        result["cpu_baseline"] = cpu_baseline(synth, a.cpu_docs, a.vocab)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ix.close()
+    ctx.close()
+    L.sme_synth_free(d_corpus)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
+    k = 10
+    _, _, _, df = ix.csr()
+    terms, qoff = synth.queries_by_df(df, a.queries, seed=7)
+    if dist is not None:
+        # queries are defined by term strings (rank 0's draw); every shard maps them to its own ids
+        uniq = np.unique(terms)
+        obj = [[ix.term(int(t)) for t in uniq], uniq, qoff] if rank == 0 else [None, None, None]
+        dist.broadcast_object_list(obj, src=0)
+        strs, uniq, qoff = obj
+        if rank == 0:
+            pos = np.searchsorted(uniq, terms)
+        else:
+            terms = None
+        loc = ix.lookup(strs)
+        obj2 = [pos if rank == 0 else None]
+        dist.broadcast_object_list(obj2, src=0)
+        terms = loc[obj2[0]].astype(np.int32)
+    d_terms = torch.from_numpy(terms).cuda()
+    d_qoff = torch.from_numpy(qoff).cuda()
+    out_d = torch.empty((a.queries, k), dtype=torch.int32, device="cuda")
+    out_s = torch.empty((a.queries, k), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def qstep():
+        ix.query_topk_device(d_terms.data_ptr(), d_qoff.data_ptr(), a.queries, k, out_d.data_ptr(), out_s.data_ptr(),
+                             stream)
+        if dist is not None:
+            # merge per-shard top-k: all-gather (score, docno) lists, keep the best k per query
+            gs = [torch.empty_like(out_s) for _ in range(world)]
+            gd = [torch.empty_like(out_d) for _ in range(world)]
+            dist.all_gather(gs, out_s)
+            dist.all_gather(gd, out_d)
+            s = torch.cat(gs, 1)
+            d = torch.cat(gd, 1).to(torch.int64)
+            valid = d >= 0
+            s = torch.where(valid, s, torch.full_like(s, -float("inf")))
+            d = torch.where(valid, d, torch.full_like(d, 1 << 40))
+            # (score desc, docno asc): stable sort by docno, then stable sort by -score
+            i1 = torch.argsort(d, dim=1, stable=True)
+            s1, d1 = torch.gather(s, 1, i1), torch.gather(d, 1, i1)
+            i2 = torch.argsort(-s1, dim=1, stable=True)[:, :k]
+            return torch.gather(d1, 1, i2), torch.gather(s1, 1, i2)
+        return out_d
+
+    qstep()
+    barrier()
+    steps = max(1, a.steps // 2)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        qstep()
+    barrier()
+    dt = (time.perf_counter() - t0) / steps
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    qps = a.queries / dt
+    nt = np.diff(qoff)
+    # algorithmic bytes: postings of distinct batch terms read once (docno + weight = 12 B here)
+    tv = terms[terms >= 0]
+    uniq = np.unique(tv)
+    alg = 12 * int(df[uniq].sum()) + 4 * int(nt.sum()) + 12 * k * a.queries
+    touched = 12 * int(df[tv].sum())
+    return {"metric": "top-10 queries/sec", "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
+            "terms_per_query": "U{2..8} drawn by df (seed 7)", "ms_per_batch": round(dt * 1e3, 3),
+            "roofline": {"bound": "hbm", "achieved": round(alg / dt / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(alg / dt / 1e9 / HBM_PEAK_GBS, 6),
+                         "what": "A_q = 12*sum(df of distinct batch terms) + 4*sum|q| + 12*k*Q"},
+            "postings_touched_GBps": round(touched / dt / 1e9, 2)}
+
+
+def cpu_baseline(synth, n_docs, V):
+    """The oracle (ref-faithful CPU restatement, single thread) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    corpus = synth.gen_corpus(n_docs, V=V, seed=42, len_lo=400, len_hi=600)
+    mapping = synth.mapping_bytes(n_docs)
+    t0 = time.perf_counter()
+    ix = O.OracleIndex(corpus, mapping, 1, 1)
+    dt = time.perf_counter() - t0
+    del ix
+    return {"value": round(len(corpus) / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "%d docs (%d bytes) of the c2 distribution, ref-faithful oracle (per-token emit, "
+                      "string-key merge sort, reduce sorts), %.1f s" % (n_docs, len(corpus), dt)}
+
+
+if __name__ == "__main__":
+    main()

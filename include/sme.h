@@ -1,0 +1,153 @@
+/*
+ * sme.h -- C-ABI of the MI355X-native index-build / TF-IDF / query hot path.
+ *
+ * "sme" = Simple MapReduce Engine.  This library replaces, as one batch call,
+ * the reference's whole TermKGramDocIndexer job (map -> shuffle/sort ->
+ * combine/reduce) and IntDocVectorsForwardIndex.rank():
+ *
+ *   sme_build_index*      <- TermKGramDocIndexer.run / MyMapper.map / MyReducer.reduce
+ *                            C/sa/edu/kaust/indexing/TermKGramDocIndexer.java:119-160,168-213,227-283
+ *   sme_load_docno_mapping<- MyMapper.configure -> TrecDocnoMapping.loadMapping/readDocnoData
+ *                            TermKGramDocIndexer.java:93-117; C/edu/umd/cloud9/collection/trec/TrecDocnoMapping.java:75-77,137-155
+ *   sme_index_partition_records <- SequenceFileOutputFormat part-NNNNN record stream
+ *                            (TermDF.write TermDF.java:50-56, ArrayListWritable.write ArrayListWritable.java:90-105)
+ *   sme_tokenize          <- GalagoTokenizer.processContent  C/ivory/tokenize/GalagoTokenizer.java:139-183
+ *   sme_lookup_terms      <- IntDocVectorsForwardIndex.getValue(String[]) term lookup
+ *                            C/sa/edu/kaust/fwindex/IntDocVectorsForwardIndex.java:131-184
+ *   sme_query_topk        <- IntDocVectorsForwardIndex.rank()  IntDocVectorsForwardIndex.java:192-223
+ * (C/ = ABDURRAHMAN-PA2-3-code/src/ of the reference; U+2010 hyphens in the real path.)
+ *
+ * Conventions: every int-returning function returns 0 (SME_OK) on success and
+ * a negative SME_E* code on failure; sme_last_error() returns a thread-local
+ * message for the last failure.  Inputs are borrowed for the duration of the
+ * call; outputs returned through pointers are owned by the library until the
+ * owning object is freed.  One sme_ctx per device; calls on one context must
+ * be serialized by the caller (the reference's query class is not thread-safe
+ * either: IntDocVectorsForwardIndex.java:63-65).
+ */
+#ifndef SME_H
+#define SME_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SME_OK 0
+#define SME_EINVAL -1    /* bad argument */
+#define SME_EHIP -2      /* HIP runtime error */
+#define SME_ENOMEM -3    /* device allocation failed */
+#define SME_EPARSE -4    /* input the reference rejects (e.g. <DOCNO> without </DOCNO>: getDocid throws) */
+#define SME_ENOMAP -5    /* no docno mapping loaded */
+#define SME_ELIMIT -6    /* an implementation limit was hit (message says which) */
+#define SME_ENOTIMPL -7  /* feature not built yet (message says which) */
+
+/* idf_mode */
+#define SME_IDF_REFERENCE 0 /* log10(N / stored_df); stored df of every real term is 1 */
+#define SME_IDF_TRUE_DF 1   /* log10(N / df) with df = postings length, int division as the reference */
+
+/* tiebreak */
+#define SME_TIE_DOCNO 0 /* score desc, then docno asc (north-star contract) */
+
+typedef struct sme_ctx sme_ctx;
+typedef struct sme_index sme_index;
+
+typedef struct {
+  int k;              /* K of the K-gram index (TermKGramDocIndexer args[0]); 1 = term index */
+  int num_partitions; /* R reducers (conf.setNumReduceTasks(10) on the cluster, 1 in local mode) */
+  int idf_mode;       /* SME_IDF_* used by the TF-IDF weight pass and sme_query_topk */
+  int tiebreak;       /* SME_TIE_* */
+  int device;         /* HIP device ordinal */
+  int reserved[11];   /* must be zero */
+} sme_config;
+
+const char *sme_last_error(void);
+const char *sme_version(void);
+
+int sme_create(const sme_config *cfg, sme_ctx **out);
+void sme_destroy(sme_ctx *ctx);
+
+/* Docno mapping file bytes: int32 N, then N x writeUTF(docid), docids sorted
+ * (TrecDocnoMapping.writeDocnoData format).  Uploaded once; docno lookup is
+ * Arrays.binarySearch over {"", docids...} on the device. */
+int sme_load_docno_mapping(sme_ctx *ctx, const uint8_t *mapping_file, size_t n);
+
+/* Build from a host corpus (TREC <DOC>..</DOC> records, one split). Copies to HBM. */
+int sme_build_index(sme_ctx *ctx, const uint8_t *corpus, size_t nbytes, sme_index **out);
+
+/* Build from a corpus already resident in device memory (d_corpus on ctx's
+ * device, nbytes long); stream may be NULL (default stream).  No host copies
+ * of the corpus are made; this is the timed path of bench.py. */
+int sme_build_index_device(sme_ctx *ctx, const void *d_corpus, size_t nbytes, void *stream,
+                           sme_index **out);
+
+void sme_index_free(sme_index *ix);
+
+/* N = records mapped (= df of the " " doc-counter key), V = distinct terms
+ * (K-grams) excluding the doc counter, P = postings (distinct (term, docno)). */
+int sme_index_stats(const sme_index *ix, uint64_t *N, uint64_t *V, uint64_t *P);
+
+/* Serialized records of reduce partition `part` in key order, framed as in a
+ * SequenceFile body: int32 recLen(key+value), int32 keyLen, TermDF bytes,
+ * ArrayListWritable<PostingWritable> bytes (all big-endian).  The buffer lives
+ * on the host and is owned by ix. */
+int sme_index_partition_records(sme_index *ix, int part, const uint8_t **buf, size_t *n);
+
+/* Host copies of the CSR in reduce-output order (tf desc, docno asc) over
+ * terms in TermDF key order.  offsets has V+1 entries; true_df has V. */
+int sme_index_csr(sme_index *ix, const int64_t **offsets, const int32_t **docno,
+                  const int32_t **tf, const int32_t **true_df);
+
+/* Device pointers of the query-side arrays (docno-ascending postings per term
+ * and their fp64 TF-IDF weights), for callers that keep data in HBM. */
+int sme_index_device_arrays(sme_index *ix, const int64_t **d_offsets, const int32_t **d_docno,
+                            const double **d_weight);
+
+/* Term string of term id t (modified-UTF-8 bytes as written by writeUTF). */
+int sme_index_term(sme_index *ix, int64_t t, const uint8_t **utf8, size_t *n);
+
+/* GalagoTokenizer.processContent on one UTF-8 string, run through the same
+ * device kernels as the build.  Tokens (modified UTF-8) are written back to back
+ * into buf; offs[i]..offs[i+1] delimits token i (offs has cap_tok+1 entries). */
+int sme_tokenize(sme_ctx *ctx, const uint8_t *utf8, size_t n, uint8_t *buf, size_t cap,
+                 int64_t *offs, int cap_tok, int *ntok);
+
+/* Map processed terms (UTF-8, offs delimits n terms) to term ids; -1 if absent
+ * (getValue skips unknown terms silently). */
+int sme_lookup_terms(sme_index *ix, const uint8_t *terms, const int64_t *offs, int n,
+                     int32_t *term_ids);
+
+/* Batched rank(): query q has term ids term_ids[q_offsets[q] .. q_offsets[q+1])
+ * in query-token order (duplicates count twice, -1 entries are skipped).
+ * Writes k docnos / scores per query (score desc, docno asc), padded with
+ * docno -1 / score 0 when fewer than k documents match. */
+int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq,
+                   int k, int32_t *out_docno, double *out_score);
+
+/* Same with all arrays already in device memory (timed path). */
+int sme_query_topk_device(sme_index *ix, const int32_t *d_term_ids, const int64_t *d_q_offsets,
+                          int nq, int k, int32_t *d_out_docno, double *d_out_score, void *stream);
+
+/* Recompute the fp64 TF-IDF weights of a doc-sharded index with global
+ * statistics: n_global = records over all shards (all-reduced doc counter),
+ * d_df_global = per local term the all-reduced df (device int64[V]) or NULL to
+ * keep the shard's own df (SME_IDF_TRUE_DF only; reference mode uses stored df 1). */
+int sme_index_reweight(sme_index *ix, int64_t n_global, const int64_t *d_df_global, void *stream);
+
+/* Synthetic Zipfian TREC corpus generated directly in HBM (bench / tests; same
+ * bytes as synth.py).  vocab/vocab_off/cdf are host arrays (V words, V+1
+ * offsets, V cumulative probabilities).  *d_corpus is freed with sme_synth_free. */
+int sme_synth_corpus(int device, const uint8_t *vocab, const int64_t *vocab_off, int64_t V, const double *cdf,
+                     int64_t n_docs, int64_t d0, uint64_t seed, int len_lo, int len_hi, void **d_corpus,
+                     size_t *nbytes);
+void sme_synth_free(void *d_corpus);
+
+/* Timing of the last build, per stage, in milliseconds (device events). */
+int sme_last_build_profile(const sme_ctx *ctx, const char **json);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,293 @@
+"""sme -- MI355X-native drop-in for the reference's index/TF-IDF/query hot path.
+
+Host-side mirror of the reference operator surface (names follow the Java
+classes; see include/sme.h for the C-ABI each call goes through):
+
+  TermKGramDocIndexer    C/sa/edu/kaust/indexing/TermKGramDocIndexer.java:227-283 (run)
+  TrecDocnoMapping       C/edu/umd/cloud9/collection/trec/TrecDocnoMapping.java:92-155
+  GalagoTokenizer        C/ivory/tokenize/GalagoTokenizer.java:139-183 (processContent)
+  IntDocVectorsForwardIndex  C/sa/edu/kaust/fwindex/IntDocVectorsForwardIndex.java:131-223
+                         (getValue / rank), batched as Index.query_topk
+
+Everything computes on the GPU through libsme.so.  There is no CPU fallback:
+if the HIP library is missing or no GPU is visible, calls raise SmeError.
+"""
+import ctypes as C
+import os
+import struct
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsme.so")
+
+SME_IDF_REFERENCE = 0
+SME_IDF_TRUE_DF = 1
+
+
+class SmeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("sme error %d: %s" % (code, msg))
+        self.code = code
+
+
+class _Config(C.Structure):
+    _fields_ = [("k", C.c_int), ("num_partitions", C.c_int), ("idf_mode", C.c_int), ("tiebreak", C.c_int),
+                ("device", C.c_int), ("reserved", C.c_int * 11)]
+
+
+_lib = None
+
+EXPORTS = [
+    "sme_last_error", "sme_version", "sme_create", "sme_destroy", "sme_load_docno_mapping", "sme_build_index",
+    "sme_build_index_device", "sme_index_free", "sme_index_stats", "sme_index_partition_records", "sme_index_csr",
+    "sme_index_device_arrays", "sme_index_term", "sme_tokenize", "sme_lookup_terms", "sme_query_topk",
+    "sme_query_topk_device", "sme_last_build_profile", "sme_index_reweight",
+]
+
+
+def lib():
+    """Load libsme.so (fails loudly: the product has no CPU path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SmeError(-2, "libsme.so not built (run __graft_entry__.build() or make -C %s)" % _HERE)
+    L = C.CDLL(LIB_PATH)
+    vp, sz, i64p, i32p = C.c_void_p, C.c_size_t, C.POINTER(C.c_int64), C.POINTER(C.c_int32)
+    L.sme_last_error.restype = C.c_char_p
+    L.sme_version.restype = C.c_char_p
+    L.sme_create.argtypes = [C.POINTER(_Config), C.POINTER(vp)]
+    L.sme_destroy.argtypes = [vp]
+    L.sme_destroy.restype = None
+    L.sme_load_docno_mapping.argtypes = [vp, C.c_char_p, sz]
+    L.sme_build_index.argtypes = [vp, C.c_char_p, sz, C.POINTER(vp)]
+    L.sme_build_index_device.argtypes = [vp, vp, sz, vp, C.POINTER(vp)]
+    L.sme_index_free.argtypes = [vp]
+    L.sme_index_free.restype = None
+    L.sme_index_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.sme_index_partition_records.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
+    L.sme_index_csr.argtypes = [vp, C.POINTER(i64p), C.POINTER(i32p), C.POINTER(i32p), C.POINTER(i32p)]
+    L.sme_index_device_arrays.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
+    L.sme_index_term.argtypes = [vp, C.c_int64, C.POINTER(vp), C.POINTER(sz)]
+    L.sme_tokenize.argtypes = [vp, C.c_char_p, sz, vp, sz, i64p, C.c_int, C.POINTER(C.c_int)]
+    L.sme_lookup_terms.argtypes = [vp, C.c_char_p, i64p, C.c_int, i32p]
+    L.sme_query_topk.argtypes = [vp, i32p, i64p, C.c_int, C.c_int, i32p, C.POINTER(C.c_double)]
+    L.sme_query_topk_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp]
+    L.sme_last_build_profile.argtypes = [vp, C.POINTER(C.c_char_p)]
+    L.sme_index_reweight.argtypes = [vp, C.c_int64, vp, vp]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise SmeError(rc, lib().sme_last_error().decode("utf-8", "replace"))
+
+
+def _mutf8_decode(b):
+    """DataInput.readUTF body -> str (surrogates kept)."""
+    out, i = [], 0
+    while i < len(b):
+        c = b[i]
+        if c < 0x80:
+            out.append(c)
+            i += 1
+        elif c & 0xE0 == 0xC0:
+            out.append(((c & 0x1F) << 6) | (b[i + 1] & 0x3F))
+            i += 2
+        else:
+            out.append(((c & 0x0F) << 12) | ((b[i + 1] & 0x3F) << 6) | (b[i + 2] & 0x3F))
+            i += 3
+    raw = b"".join(u.to_bytes(2, "little") for u in out)
+    return raw.decode("utf-16-le", "surrogatepass")
+
+
+# ---------------------------------------------------------------------------
+class TrecDocnoMapping:
+    """Docno mapping file: int32 N, N x writeUTF(docid), docids sorted (writeDocnoData)."""
+
+    @staticmethod
+    def write(docids):
+        out = [struct.pack(">i", len(docids))]
+        for d in docids:
+            b = d.encode("utf-8")
+            out.append(struct.pack(">H", len(b)) + b)
+        return b"".join(out)
+
+
+class Context:
+    """One device context (sme_ctx): config + docno mapping + reusable HBM workspace."""
+
+    def __init__(self, k=1, num_partitions=1, idf_mode=SME_IDF_REFERENCE, device=0):
+        cfg = _Config(k, num_partitions, idf_mode, 0, device)
+        h = C.c_void_p()
+        _check(lib().sme_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.k, self.num_partitions, self.idf_mode, self.device = k, num_partitions, idf_mode, device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().sme_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def load_docno_mapping(self, mapping_bytes):
+        _check(lib().sme_load_docno_mapping(self._h, mapping_bytes, len(mapping_bytes)))
+
+    def build(self, corpus):
+        """Build from host bytes (copied to HBM)."""
+        h = C.c_void_p()
+        _check(lib().sme_build_index(self._h, corpus, len(corpus), C.byref(h)))
+        return Index(h, self)
+
+    def build_device(self, d_ptr, nbytes, stream=None):
+        """Build from a corpus already in HBM (e.g. a torch uint8 tensor's data_ptr())."""
+        h = C.c_void_p()
+        _check(lib().sme_build_index_device(self._h, C.c_void_p(d_ptr), nbytes, C.c_void_p(stream or 0),
+                                            C.byref(h)))
+        return Index(h, self)
+
+    def last_build_profile(self):
+        import json
+        p = C.c_char_p()
+        _check(lib().sme_last_build_profile(self._h, C.byref(p)))
+        return json.loads(p.value.decode())
+
+    def process_content(self, text):
+        """GalagoTokenizer.processContent on the device."""
+        b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        cap_tok = len(b) + 4
+        buf = (C.c_ubyte * (3 * len(b) + 16))()
+        offs = (C.c_int64 * (cap_tok + 1))()
+        nt = C.c_int(0)
+        _check(lib().sme_tokenize(self._h, b, len(b), buf, len(buf), offs, cap_tok, C.byref(nt)))
+        raw = bytes(buf)
+        return [_mutf8_decode(raw[offs[i]:offs[i + 1]]) for i in range(nt.value)]
+
+
+class Index:
+    """A built index (sme_index): reduce output + query-side CSR, resident in HBM."""
+
+    def __init__(self, h, ctx):
+        self._h, self.ctx = h, ctx
+        n, v, p = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib().sme_index_stats(h, C.byref(n), C.byref(v), C.byref(p)))
+        self.N, self.V, self.P = n.value, v.value, p.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().sme_index_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def partition_records(self, part):
+        p, n = C.c_void_p(), C.c_size_t()
+        _check(lib().sme_index_partition_records(self._h, part, C.byref(p), C.byref(n)))
+        return C.string_at(p, n.value) if n.value else b""
+
+    def csr(self):
+        """(offsets[V+1], docno[P], tf[P], true_df[V]) in reduce-output order (tf desc, docno asc)."""
+        o, d, t, f = C.POINTER(C.c_int64)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)()
+        _check(lib().sme_index_csr(self._h, C.byref(o), C.byref(d), C.byref(t), C.byref(f)))
+        V, P = self.V, self.P
+        return (np.ctypeslib.as_array(o, (V + 1,)).copy(), np.ctypeslib.as_array(d, (max(P, 1),))[:P].copy(),
+                np.ctypeslib.as_array(t, (max(P, 1),))[:P].copy(), np.ctypeslib.as_array(f, (max(V, 1),))[:V].copy())
+
+    def device_arrays(self):
+        o, d, w = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        _check(lib().sme_index_device_arrays(self._h, C.byref(o), C.byref(d), C.byref(w)))
+        return o.value, d.value, w.value
+
+    def term(self, t):
+        p, n = C.c_void_p(), C.c_size_t()
+        _check(lib().sme_index_term(self._h, t, C.byref(p), C.byref(n)))
+        return _mutf8_decode(C.string_at(p, n.value))
+
+    def terms(self):
+        return [self.term(t) for t in range(self.V)]
+
+    def lookup(self, terms):
+        bs = [t.encode("utf-8", "surrogatepass") for t in terms]
+        offs = np.zeros(len(bs) + 1, dtype=np.int64)
+        offs[1:] = np.cumsum([len(b) for b in bs]) if bs else []
+        ids = np.zeros(max(len(bs), 1), dtype=np.int32)
+        _check(lib().sme_lookup_terms(self._h, b"".join(bs), offs.ctypes.data_as(C.POINTER(C.c_int64)), len(bs),
+                                      ids.ctypes.data_as(C.POINTER(C.c_int32))))
+        return ids[:len(bs)]
+
+    def query_topk(self, term_ids, q_offsets, k=10):
+        """Batched rank(): returns (docno[nq,k], score[nq,k]); docno -1 pads."""
+        term_ids = np.ascontiguousarray(term_ids, dtype=np.int32)
+        q_offsets = np.ascontiguousarray(q_offsets, dtype=np.int64)
+        nq = len(q_offsets) - 1
+        dn = np.zeros((max(nq, 1), k), dtype=np.int32)
+        sc = np.zeros((max(nq, 1), k), dtype=np.float64)
+        _check(lib().sme_query_topk(self._h, term_ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    q_offsets.ctypes.data_as(C.POINTER(C.c_int64)), nq, k,
+                                    dn.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    sc.ctypes.data_as(C.POINTER(C.c_double))))
+        return dn[:nq], sc[:nq]
+
+    def reweight(self, n_global, d_df_global=None, stream=None):
+        """TF-IDF weights with all-reduced N (and df) of a doc-sharded index."""
+        _check(lib().sme_index_reweight(self._h, n_global, C.c_void_p(d_df_global or 0), C.c_void_p(stream or 0)))
+
+    def query_topk_device(self, d_terms, d_qoff, nq, k, d_out_docno, d_out_score, stream=None):
+        _check(lib().sme_query_topk_device(self._h, C.c_void_p(d_terms), C.c_void_p(d_qoff), nq, k,
+                                           C.c_void_p(d_out_docno), C.c_void_p(d_out_score), C.c_void_p(stream or 0)))
+
+
+# ---------------------------------------------------------------------------
+# reference-shaped facades
+class GalagoTokenizer:
+    """GalagoTokenizer.processContent, evaluated by the device tokenizer."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx or Context()
+
+    def processContent(self, text):  # noqa: N802 (reference name)
+        return self.ctx.process_content(text)
+
+
+class TermKGramDocIndexer:
+    """TermKGramDocIndexer.run(K, input, output, mapping) as one device call.
+
+    run() returns the Index; if output_dir is given, the reduce partitions are
+    written as part-NNNNN files (SequenceFile v6 container, see seqfile.py).
+    """
+
+    def __init__(self, k=1, num_reduce_tasks=10, idf_mode=SME_IDF_REFERENCE, device=0):
+        self.ctx = Context(k, num_reduce_tasks, idf_mode, device)
+
+    def run(self, corpus, mapping, output_dir=None):
+        corpus = open(corpus, "rb").read() if isinstance(corpus, str) else corpus
+        mapping = open(mapping, "rb").read() if isinstance(mapping, str) else mapping
+        self.ctx.load_docno_mapping(mapping)
+        ix = self.ctx.build(corpus)
+        if output_dir is not None:
+            from . import seqfile
+            seqfile.write_index_dir(ix, output_dir)
+        return ix
+
+
+class IntDocVectorsForwardIndex:
+    """Query side: getValue(terms) then rank() -> up to 10 docnos (score desc, docno asc)."""
+
+    def __init__(self, index):
+        self.index = index
+        self._terms = []
+
+    def getValue(self, terms):  # noqa: N802
+        ids = self.index.lookup(list(terms))
+        self._terms = [int(t) for t in ids if t >= 0]  # unknown terms are skipped silently
+
+    def rank(self, k=10):
+        if not self._terms:
+            return []
+        dn, _ = self.index.query_topk(np.array(self._terms, np.int32), np.array([0, len(self._terms)], np.int64), k)
+        return [int(d) for d in dn[0] if d >= 0]

@@ -1,0 +1,391 @@
+// sme_api.hip -- the C-ABI (include/sme.h).  Every entry point converts
+// sme::Error / std::exception into a negative status and a thread-local message.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "sme_internal.hpp"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+template <typename F>
+int guard(F &&f) {
+  try {
+    f();
+    g_err.clear();
+    return SME_OK;
+  } catch (const sme::Error &e) {
+    return fail(e.code, e.what());
+  } catch (const std::bad_alloc &) {
+    return fail(SME_ENOMEM, "host allocation failed");
+  } catch (const std::exception &e) {
+    return fail(SME_EINVAL, e.what());
+  }
+}
+
+hipStream_t stream_of(sme_ctx *cx, void *s) { return s ? (hipStream_t)s : cx->own_stream; }
+
+void set_device(sme_ctx *cx) { SME_HIP(hipSetDevice(cx->device)); }
+
+// DataInput.readUTF body -> UTF-16
+bool read_mutf8(const uint8_t *p, size_t len, std::vector<uint16_t> &out) {
+  size_t i = 0;
+  while (i < len) {
+    unsigned c = p[i];
+    if (c < 0x80) {
+      out.push_back((uint16_t)c);
+      i++;
+    } else if ((c & 0xE0) == 0xC0) {
+      if (i + 1 >= len) return false;
+      out.push_back((uint16_t)(((c & 0x1F) << 6) | (p[i + 1] & 0x3F)));
+      i += 2;
+    } else if ((c & 0xF0) == 0xE0) {
+      if (i + 2 >= len) return false;
+      out.push_back((uint16_t)(((c & 0x0F) << 12) | ((p[i + 1] & 0x3F) << 6) | (p[i + 2] & 0x3F)));
+      i += 3;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+// standard UTF-8 -> UTF-16 (API inputs of already-processed terms)
+std::vector<uint16_t> utf8_to_u16(const uint8_t *p, size_t n) {
+  std::vector<uint16_t> o;
+  size_t i = 0;
+  while (i < n) {
+    unsigned c = p[i];
+    unsigned cp;
+    int extra;
+    if (c < 0x80) {
+      cp = c;
+      extra = 0;
+    } else if ((c & 0xE0) == 0xC0) {
+      cp = c & 0x1F;
+      extra = 1;
+    } else if ((c & 0xF0) == 0xE0) {
+      cp = c & 0x0F;
+      extra = 2;
+    } else {
+      cp = c & 0x07;
+      extra = 3;
+    }
+    i++;
+    for (int k = 0; k < extra && i < n; k++, i++) cp = (cp << 6) | (p[i] & 0x3F);
+    if (cp >= 0x10000) {
+      cp -= 0x10000;
+      o.push_back((uint16_t)(0xD800 + (cp >> 10)));
+      o.push_back((uint16_t)(0xDC00 + (cp & 0x3FF)));
+    } else {
+      o.push_back((uint16_t)cp);
+    }
+  }
+  return o;
+}
+
+// DataOutput.writeUTF body of UTF-16 units
+void u16_to_mutf8(const uint16_t *u, size_t n, std::vector<uint8_t> &o) {
+  for (size_t i = 0; i < n; i++) {
+    uint16_t c = u[i];
+    if (c >= 1 && c <= 0x7F) {
+      o.push_back((uint8_t)c);
+    } else if (c > 0x7FF) {
+      o.push_back((uint8_t)(0xE0 | ((c >> 12) & 0x0F)));
+      o.push_back((uint8_t)(0x80 | ((c >> 6) & 0x3F)));
+      o.push_back((uint8_t)(0x80 | (c & 0x3F)));
+    } else {
+      o.push_back((uint8_t)(0xC0 | ((c >> 6) & 0x1F)));
+      o.push_back((uint8_t)(0x80 | (c & 0x3F)));
+    }
+  }
+}
+
+void ensure_host_terms(sme_index *ix) {
+  if (ix->h_terms_ready) return;
+  ix->h_term_off.resize(ix->V + 1);
+  SME_HIP(hipMemcpy(ix->h_term_off.data(), ix->d_term_off.p, (ix->V + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+  ix->h_term_chars.resize(ix->h_term_off[ix->V] + 1);
+  if (ix->h_term_off[ix->V] > 0)
+    SME_HIP(hipMemcpy(ix->h_term_chars.data(), ix->d_term_chars.p, ix->h_term_off[ix->V] * sizeof(uint16_t),
+                      hipMemcpyDeviceToHost));
+  ix->h_terms_ready = true;
+}
+}  // namespace
+
+extern "C" {
+
+const char *sme_last_error(void) { return g_err.c_str(); }
+const char *sme_version(void) { return "sme 0.1 (gfx950)"; }
+
+int sme_create(const sme_config *cfg, sme_ctx **out) {
+  return guard([&] {
+    if (!cfg || !out) throw sme::Error(SME_EINVAL, "null argument");
+    if (cfg->k < 1) throw sme::Error(SME_EINVAL, "k must be >= 1");
+    if (cfg->num_partitions < 1) throw sme::Error(SME_EINVAL, "num_partitions must be >= 1");
+    if (cfg->idf_mode != SME_IDF_REFERENCE && cfg->idf_mode != SME_IDF_TRUE_DF)
+      throw sme::Error(SME_EINVAL, "bad idf_mode");
+    if (cfg->tiebreak != SME_TIE_DOCNO) throw sme::Error(SME_EINVAL, "bad tiebreak");
+    int ndev = 0;
+    SME_HIP(hipGetDeviceCount(&ndev));
+    if (cfg->device < 0 || cfg->device >= ndev) throw sme::Error(SME_EINVAL, "bad device ordinal");
+    sme_ctx *cx = new sme_ctx();
+    cx->cfg = *cfg;
+    cx->device = cfg->device;
+    try {
+      set_device(cx);
+      SME_HIP(hipStreamCreateWithFlags(&cx->own_stream, hipStreamNonBlocking));
+    } catch (...) {
+      delete cx;
+      throw;
+    }
+    *out = cx;
+  });
+}
+
+void sme_destroy(sme_ctx *cx) {
+  if (!cx) return;
+  (void)hipSetDevice(cx->device);
+  (void)hipDeviceSynchronize();
+  if (cx->own_stream) (void)hipStreamDestroy(cx->own_stream);
+  delete cx;
+}
+
+int sme_load_docno_mapping(sme_ctx *cx, const uint8_t *m, size_t n) {
+  return guard([&] {
+    if (!cx || (!m && n)) throw sme::Error(SME_EINVAL, "null argument");
+    set_device(cx);
+    if (n < 4) throw sme::Error(SME_EINVAL, "mapping file shorter than its int32 count");
+    int32_t cnt = (int32_t)(((uint32_t)m[0] << 24) | ((uint32_t)m[1] << 16) | ((uint32_t)m[2] << 8) | m[3]);
+    if (cnt < 0) throw sme::Error(SME_EINVAL, "negative mapping count");
+    std::vector<uint16_t> chars;
+    std::vector<int64_t> off;
+    off.push_back(0);
+    off.push_back(0);  // "" sentinel at index 0 (readDocnoData)
+    size_t p = 4;
+    for (int32_t i = 0; i < cnt; i++) {
+      if (p + 2 > n) throw sme::Error(SME_EINVAL, "truncated mapping file");
+      size_t l = ((size_t)m[p] << 8) | m[p + 1];
+      p += 2;
+      if (p + l > n) throw sme::Error(SME_EINVAL, "truncated mapping file");
+      if (!read_mutf8(m + p, l, chars)) throw sme::Error(SME_EINVAL, "bad modified UTF-8 in mapping file");
+      p += l;
+      off.push_back((int64_t)chars.size());
+    }
+    chars.push_back(0);
+    hipStream_t st = cx->own_stream;
+    uint16_t *dc = cx->map_chars.as<uint16_t>(chars.size());
+    int64_t *doff = cx->map_off.as<int64_t>(off.size());
+    SME_HIP(hipMemcpyAsync(dc, chars.data(), chars.size() * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+    SME_HIP(hipMemcpyAsync(doff, off.data(), off.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    SME_HIP(hipStreamSynchronize(st));
+    cx->map_n = (int64_t)off.size() - 1;
+    cx->has_map = true;
+  });
+}
+
+int sme_build_index_device(sme_ctx *cx, const void *d_corpus, size_t nbytes, void *stream, sme_index **out) {
+  return guard([&] {
+    if (!cx || !out || (!d_corpus && nbytes)) throw sme::Error(SME_EINVAL, "null argument");
+    set_device(cx);
+    hipStream_t st = stream_of(cx, stream);
+    sme_index *ix = sme::build_index(cx, (const uint8_t *)d_corpus, nbytes, st);
+    cx->last_profile = ix->profile;
+    *out = ix;
+  });
+}
+
+int sme_build_index(sme_ctx *cx, const uint8_t *corpus, size_t nbytes, sme_index **out) {
+  return guard([&] {
+    if (!cx || !out || (!corpus && nbytes)) throw sme::Error(SME_EINVAL, "null argument");
+    set_device(cx);
+    hipStream_t st = cx->own_stream;
+    sme::DevBuf buf;
+    uint8_t *d = buf.as<uint8_t>(nbytes + 16);
+    if (nbytes) SME_HIP(hipMemcpyAsync(d, corpus, nbytes, hipMemcpyHostToDevice, st));
+    sme_index *ix = sme::build_index(cx, d, nbytes, st);
+    SME_HIP(hipStreamSynchronize(st));
+    cx->last_profile = ix->profile;
+    *out = ix;
+  });
+}
+
+void sme_index_free(sme_index *ix) {
+  if (!ix) return;
+  (void)hipSetDevice(ix->ctx->device);
+  (void)hipDeviceSynchronize();
+  delete ix;
+}
+
+int sme_index_stats(const sme_index *ix, uint64_t *N, uint64_t *V, uint64_t *P) {
+  return guard([&] {
+    if (!ix) throw sme::Error(SME_EINVAL, "null index");
+    if (N) *N = (uint64_t)ix->N;
+    if (V) *V = (uint64_t)ix->V;
+    if (P) *P = (uint64_t)ix->P;
+  });
+}
+
+int sme_index_partition_records(sme_index *ix, int part, const uint8_t **buf, size_t *n) {
+  return guard([&] {
+    if (!ix || !buf || !n) throw sme::Error(SME_EINVAL, "null argument");
+    if (part < 0 || part >= ix->R) throw sme::Error(SME_EINVAL, "partition out of range");
+    set_device(ix->ctx);
+    hipStream_t st = ix->ctx->own_stream;
+    sme::serialize_index(ix, st);
+    if (!ix->h_parts_ready[part]) {
+      const int64_t a = ix->part_start[part], b = ix->part_start[part + 1];
+      ix->h_parts[part].resize((size_t)(b - a));
+      if (b > a)
+        SME_HIP(hipMemcpy(ix->h_parts[part].data(), (const uint8_t *)ix->d_ser.p + a, (size_t)(b - a),
+                          hipMemcpyDeviceToHost));
+      ix->h_parts_ready[part] = 1;
+    }
+    *buf = ix->h_parts[part].data();
+    *n = ix->h_parts[part].size();
+  });
+}
+
+int sme_index_csr(sme_index *ix, const int64_t **offsets, const int32_t **docno, const int32_t **tf,
+                  const int32_t **true_df) {
+  return guard([&] {
+    if (!ix) throw sme::Error(SME_EINVAL, "null index");
+    set_device(ix->ctx);
+    if (!ix->h_csr_ready) {
+      ix->h_off.resize(ix->V + 1);
+      ix->h_docno.resize(ix->P);
+      ix->h_tf.resize(ix->P);
+      ix->h_df.resize(ix->V);
+      SME_HIP(hipMemcpy(ix->h_off.data(), ix->d_off.p, (ix->V + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+      if (ix->P) {
+        SME_HIP(hipMemcpy(ix->h_docno.data(), ix->d_docno_o.p, ix->P * sizeof(int32_t), hipMemcpyDeviceToHost));
+        SME_HIP(hipMemcpy(ix->h_tf.data(), ix->d_tf_o.p, ix->P * sizeof(int32_t), hipMemcpyDeviceToHost));
+      }
+      for (int64_t t = 0; t < ix->V; t++) ix->h_df[t] = (int32_t)(ix->h_off[t + 1] - ix->h_off[t]);
+      ix->h_csr_ready = true;
+    }
+    if (offsets) *offsets = ix->h_off.data();
+    if (docno) *docno = ix->h_docno.data();
+    if (tf) *tf = ix->h_tf.data();
+    if (true_df) *true_df = ix->h_df.data();
+  });
+}
+
+int sme_index_device_arrays(sme_index *ix, const int64_t **d_offsets, const int32_t **d_docno,
+                            const double **d_weight) {
+  return guard([&] {
+    if (!ix) throw sme::Error(SME_EINVAL, "null index");
+    if (d_offsets) *d_offsets = (const int64_t *)ix->d_off.p;
+    if (d_docno) *d_docno = (const int32_t *)ix->d_docno_d.p;
+    if (d_weight) *d_weight = (const double *)ix->d_w.p;
+  });
+}
+
+int sme_index_term(sme_index *ix, int64_t t, const uint8_t **utf8, size_t *n) {
+  return guard([&] {
+    if (!ix || !utf8 || !n) throw sme::Error(SME_EINVAL, "null argument");
+    if (t < 0 || t >= ix->V) throw sme::Error(SME_EINVAL, "term id out of range");
+    set_device(ix->ctx);
+    ensure_host_terms(ix);
+    ix->h_term_tmp.clear();
+    u16_to_mutf8(ix->h_term_chars.data() + ix->h_term_off[t], (size_t)(ix->h_term_off[t + 1] - ix->h_term_off[t]),
+                 ix->h_term_tmp);
+    *utf8 = ix->h_term_tmp.data();
+    *n = ix->h_term_tmp.size();
+  });
+}
+
+int sme_tokenize(sme_ctx *cx, const uint8_t *utf8, size_t n, uint8_t *buf, size_t cap, int64_t *offs, int cap_tok,
+                 int *ntok) {
+  return guard([&] {
+    if (!cx || !buf || !offs || !ntok || (!utf8 && n)) throw sme::Error(SME_EINVAL, "null argument");
+    set_device(cx);
+    std::vector<std::vector<uint16_t>> toks;
+    sme::tokenize_string(cx, utf8, n, toks, cx->own_stream);
+    if ((int)toks.size() > cap_tok) throw sme::Error(SME_ELIMIT, "more tokens than cap_tok");
+    std::vector<uint8_t> o;
+    offs[0] = 0;
+    for (size_t i = 0; i < toks.size(); i++) {
+      u16_to_mutf8(toks[i].data(), toks[i].size(), o);
+      offs[i + 1] = (int64_t)o.size();
+    }
+    if (o.size() > cap) throw sme::Error(SME_ELIMIT, "token buffer too small");
+    if (!o.empty()) memcpy(buf, o.data(), o.size());
+    *ntok = (int)toks.size();
+  });
+}
+
+int sme_lookup_terms(sme_index *ix, const uint8_t *terms, const int64_t *offs, int n, int32_t *term_ids) {
+  return guard([&] {
+    if (!ix || !offs || !term_ids || n < 0) throw sme::Error(SME_EINVAL, "null argument");
+    set_device(ix->ctx);
+    std::vector<std::vector<uint16_t>> q(n);
+    for (int i = 0; i < n; i++) q[i] = utf8_to_u16(terms + offs[i], (size_t)(offs[i + 1] - offs[i]));
+    sme::lookup_terms(ix, q, term_ids, ix->ctx->own_stream);
+  });
+}
+
+int sme_query_topk_device(sme_index *ix, const int32_t *d_term_ids, const int64_t *d_q_offsets, int nq, int k,
+                          int32_t *d_out_docno, double *d_out_score, void *stream) {
+  return guard([&] {
+    if (!ix || (nq > 0 && (!d_term_ids || !d_q_offsets || !d_out_docno || !d_out_score)))
+      throw sme::Error(SME_EINVAL, "null argument");
+    set_device(ix->ctx);
+    sme::query_topk(ix, d_term_ids, d_q_offsets, nq, k, d_out_docno, d_out_score, stream_of(ix->ctx, stream));
+  });
+}
+
+int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq, int k,
+                   int32_t *out_docno, double *out_score) {
+  return guard([&] {
+    if (!ix || (nq > 0 && (!term_ids || !q_offsets || !out_docno || !out_score)))
+      throw sme::Error(SME_EINVAL, "null argument");
+    if (nq <= 0) return;
+    set_device(ix->ctx);
+    hipStream_t st = ix->ctx->own_stream;
+    const int64_t nt = q_offsets[nq];
+    sme::DevBuf a, b, c, d;
+    int32_t *dt = a.as<int32_t>(nt + 1);
+    int64_t *dq = b.as<int64_t>(nq + 1);
+    int32_t *dd = c.as<int32_t>((size_t)nq * k);
+    double *ds = d.as<double>((size_t)nq * k);
+    if (nt) SME_HIP(hipMemcpyAsync(dt, term_ids, nt * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    SME_HIP(hipMemcpyAsync(dq, q_offsets, (nq + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    sme::query_topk(ix, dt, dq, nq, k, dd, ds, st);
+    SME_HIP(hipMemcpyAsync(out_docno, dd, (size_t)nq * k * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipMemcpyAsync(out_score, ds, (size_t)nq * k * sizeof(double), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+  });
+}
+
+int sme_index_reweight(sme_index *ix, int64_t n_global, const int64_t *d_df_global, void *stream) {
+  return guard([&] {
+    if (!ix || n_global < 0) throw sme::Error(SME_EINVAL, "bad argument");
+    set_device(ix->ctx);
+    sme::reweight_index(ix, n_global, d_df_global, stream_of(ix->ctx, stream));
+  });
+}
+
+int sme_last_build_profile(const sme_ctx *cx, const char **json) {
+  return guard([&] {
+    if (!cx || !json) throw sme::Error(SME_EINVAL, "null argument");
+    std::ostringstream os;
+    os << "{";
+    for (size_t i = 0; i < cx->last_profile.size(); i++)
+      os << (i ? "," : "") << "\"" << cx->last_profile[i].first << "\":" << cx->last_profile[i].second;
+    os << "}";
+    const_cast<sme_ctx *>(cx)->profile_json = os.str();
+    *json = cx->profile_json.c_str();
+  });
+}
+
+}  // extern "C"

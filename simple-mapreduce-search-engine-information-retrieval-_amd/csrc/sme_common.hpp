@@ -1,0 +1,151 @@
+// sme_common.hpp -- host/device plumbing shared by the sme kernels:
+// error propagation, a reusable device workspace, and wave64 / block scans.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/sme.h"
+
+namespace sme {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define SME_HIP(x)                                                                      \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess)                                                               \
+      throw ::sme::Error(e_ == hipErrorOutOfMemory ? SME_ENOMEM : SME_EHIP,             \
+                         std::string(#x) + ": " + hipGetErrorString(e_) + " @" __FILE__ \
+                         ":" + std::to_string(__LINE__));                               \
+  } while (0)
+
+#define SME_CHECK_LAUNCH() SME_HIP(hipGetLastError())
+
+// A device buffer that grows on demand and is kept across builds, so the
+// timed path does no hipMalloc once warmed up.
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  void *get(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes > cap) {
+      if (p) {
+        SME_HIP(hipDeviceSynchronize());  // in-flight kernels may still use the old block
+        SME_HIP(hipFree(p));
+      }
+      p = nullptr;
+      size_t nc = bytes + bytes / 8;
+      SME_HIP(hipMalloc(&p, nc));
+      cap = nc;
+    }
+    return p;
+  }
+  template <typename T>
+  T *as(size_t n) {
+    return reinterpret_cast<T *>(get(n * sizeof(T)));
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  ~DevBuf() { release(); }
+};
+
+__host__ __device__ inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+inline uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// ---- device scans ---------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_sum(T v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T u = __shfl_up(v, o, 64);
+    if (l >= o) v += u;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_incl_max(T v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T u = __shfl_up(v, o, 64);
+    if (l >= o) v = v > u ? v : u;
+  }
+  return v;
+}
+
+// Block-wide exclusive sum for blockDim.x == NT (multiple of 64); scratch >= NT/64+1.
+template <int NT, typename T>
+__device__ __forceinline__ T block_excl_sum(T v, T *scratch, T *total) {
+  const int w = threadIdx.x >> 6, l = lane_id();
+  T inc = wave_incl_sum(v);
+  if (l == 63) scratch[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T run = 0;
+    for (int i = 0; i < NT / 64; i++) {
+      T t = scratch[i];
+      scratch[i] = run;
+      run += t;
+    }
+    scratch[NT / 64] = run;
+  }
+  __syncthreads();
+  T r = scratch[w] + inc - v;
+  *total = scratch[NT / 64];
+  __syncthreads();
+  return r;
+}
+// Block-wide exclusive max (identity `lo`).
+template <int NT, typename T>
+__device__ __forceinline__ T block_excl_max(T v, T lo, T *scratch, T *total) {
+  const int w = threadIdx.x >> 6, l = lane_id();
+  T inc = wave_incl_max(v);
+  T exc = __shfl_up(inc, 1, 64);
+  if (l == 0) exc = lo;
+  if (l == 63) scratch[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T run = lo;
+    for (int i = 0; i < NT / 64; i++) {
+      T t = scratch[i];
+      scratch[i] = run;
+      run = run > t ? run : t;
+    }
+    scratch[NT / 64] = run;
+  }
+  __syncthreads();
+  T pre = scratch[w];
+  T r = pre > exc ? pre : exc;
+  *total = scratch[NT / 64];
+  __syncthreads();
+  return r;
+}
+
+// 64-bit token hash (FNV-1a + murmur3 fmix); 0 is reserved for "empty".
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+}  // namespace sme

@@ -1,0 +1,72 @@
+// sme_internal.hpp -- context and index objects behind the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "sme_common.hpp"
+
+struct sme_ctx {
+  sme_config cfg{};
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  // docno mapping: {"", docids...} as UTF-16 (TrecDocnoMapping.readDocnoData)
+  sme::DevBuf map_chars, map_off;
+  int64_t map_n = 0;  // entries including the "" sentinel
+  bool has_map = false;
+  // build workspace, reused across builds (see DevBuf)
+  sme::DevBuf ws[64];  // 0..47 build, 48..63 query / serializer / tokenizer
+  sme::DevBuf cub_tmp;
+  std::string profile_json;
+  std::vector<std::pair<std::string, float>> last_profile;
+};
+
+struct sme_index {
+  sme_ctx *ctx = nullptr;
+  int K = 1, R = 1, idf_mode = 0;
+  int64_t N = 0, V = 0, P = 0;
+  int32_t max_tf = 0;
+  // sorted vocabulary (rank order): UTF-16 units
+  sme::DevBuf d_term_off;    // int64 [V+1]
+  sme::DevBuf d_term_chars;  // uint16
+  // query-side CSR: postings per term in docno-ascending order, fp64 TF-IDF weights
+  sme::DevBuf d_off;      // int64 [V+1]
+  sme::DevBuf d_docno_d;  // int32 [P]
+  sme::DevBuf d_tf_d;     // int32 [P]
+  sme::DevBuf d_w;        // double [P]
+  // reduce-output CSR: (tf desc, docno asc) per term (MyReducer.reduce order)
+  sme::DevBuf d_docno_o;  // int32 [P]
+  sme::DevBuf d_tf_o;     // int32 [P]
+  // docno of every record in input order (for the " " doc-counter postings)
+  sme::DevBuf d_rec_docno;  // int32 [N]
+  // serialized partitions (lazily built)
+  sme::DevBuf d_ser;
+  std::vector<int64_t> part_start;  // R+1
+  bool ser_ready = false;
+  std::vector<std::vector<uint8_t>> h_parts;
+  std::vector<char> h_parts_ready;
+  // host copies (lazily)
+  std::vector<int64_t> h_off;
+  std::vector<int32_t> h_docno, h_tf, h_df;
+  bool h_csr_ready = false;
+  std::vector<int64_t> h_term_off;
+  std::vector<uint16_t> h_term_chars;
+  std::vector<uint8_t> h_term_tmp;
+  bool h_terms_ready = false;
+  // stage timings of the build that produced this index (ms)
+  std::vector<std::pair<std::string, float>> profile;
+};
+
+namespace sme {
+sme_index *build_index(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st);
+void serialize_index(sme_index *ix, hipStream_t st);
+void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t st);
+void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k,
+                int32_t *d_out_docno, double *d_out_score, hipStream_t st);
+void tokenize_string(sme_ctx *cx, const uint8_t *h_utf8, size_t n, std::vector<std::vector<uint16_t>> &out,
+                     hipStream_t st);
+void lookup_terms(sme_index *ix, const std::vector<std::vector<uint16_t>> &terms, int32_t *ids,
+                  hipStream_t st);
+}  // namespace sme

@@ -1,0 +1,199 @@
+// sme_serial.hip -- the reduce output as the reference writes it: per reducer
+// partition, records in key order, framed as in a SequenceFile body
+// (int32 recLen, int32 keyLen, key bytes, value bytes; big-endian).
+//
+//   partition  HashPartitioner: (TermDF.hashCode & MAX_VALUE) % R, TermDF.hashCode =
+//              Arrays.hashCode(k_gram)                       C/sa/edu/kaust/io/TermDF.java:79-81
+//   key        TermDF.write: int32 k, k x writeUTF, int32 df TermDF.java:50-56 (df = 1 for real
+//              terms, N for " ": TermKGramDocIndexer.java:116,175-183)
+//   value      ArrayListWritable.write: int32 n, writeUTF(class name), n x PostingWritable
+//              C/edu/umd/cloud9/io/array/ArrayListWritable.java:90-105, PostingWritable.java:46-49
+//   " " record postings: (0,0) then the previous record's (docno,1) for every later record
+//              (the mapper's shared posting object, TermKGramDocIndexer.java:84-90,126,132-133)
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+#include "sme_internal.hpp"
+
+namespace sme {
+
+constexpr int kClassLen = 31;
+
+__device__ __forceinline__ int mutf8_unit_len(uint16_t c) { return (c >= 1 && c <= 0x7F) ? 1 : (c > 0x7FF ? 3 : 2); }
+
+__device__ __forceinline__ void put_be32(uint8_t *p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 24);
+  p[1] = (uint8_t)(v >> 16);
+  p[2] = (uint8_t)(v >> 8);
+  p[3] = (uint8_t)v;
+}
+
+__global__ void k_ser_sizes(const int64_t *toff, const uint16_t *tch, const int64_t *off, int64_t V, int R,
+                            int64_t *rec_bytes, uint32_t *part, uint32_t *idx, unsigned long long *psum) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
+    const uint16_t *u = tch + toff[t];
+    const int64_t l = toff[t + 1] - toff[t];
+    int64_t ul = 0;
+    uint32_t h = 0;
+    for (int64_t i = 0; i < l; i++) {
+      ul += mutf8_unit_len(u[i]);
+      h = 31u * h + u[i];
+    }
+    const int64_t df = off[t + 1] - off[t];
+    const int64_t key = 4 + 2 + ul + 4;
+    const int64_t val = 4 + (df > 0 ? 2 + kClassLen + 8 * df : 0);
+    rec_bytes[t] = 8 + key + val;
+    const uint32_t ah = 31u * 1u + h;  // Arrays.hashCode: 31 * 1 + hash(k_gram[0])
+    const uint32_t p = (uint32_t)((int32_t)(ah & 0x7fffffffu) % R);
+    part[t] = p;
+    idx[t] = (uint32_t)t;
+    atomicAdd(&psum[p], (unsigned long long)(8 + key + val));
+  }
+}
+
+__global__ void k_ser_offsets(const uint32_t *grp_term, const int64_t *scan, int64_t V, const uint32_t *part,
+                              uint32_t part_sp, int64_t sp_bytes, int64_t *rec_off) {
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < V; g += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t t = grp_term[g];
+    rec_off[t] = scan[g] + (part[t] >= part_sp ? sp_bytes : 0);
+  }
+}
+
+// one wave per term
+__global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int64_t *off, const int32_t *docno_o,
+                            const int32_t *tf_o, int64_t V, const int64_t *rec_off, uint8_t *out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wpb = blockDim.x / 64;
+  for (int64_t t = blockIdx.x * wpb + (threadIdx.x >> 6); t < V; t += (int64_t)gridDim.x * wpb) {
+    const uint16_t *u = tch + toff[t];
+    const int64_t l = toff[t + 1] - toff[t];
+    const int64_t p0 = off[t], df = off[t + 1] - off[t];
+    uint8_t *o = out + rec_off[t];
+    int64_t ul = 0;
+    for (int64_t i = 0; i < l; i++) ul += mutf8_unit_len(u[i]);
+    const int64_t key = 10 + ul, val = 4 + (df > 0 ? 2 + kClassLen + 8 * df : 0);
+    uint8_t *post = o + 8 + key + 4 + 2 + kClassLen;
+    if (lane == 0) {
+      put_be32(o, (uint32_t)(key + val));
+      put_be32(o + 4, (uint32_t)key);
+      put_be32(o + 8, 1u);
+      o[12] = (uint8_t)(ul >> 8);
+      o[13] = (uint8_t)ul;
+      uint8_t *q = o + 14;
+      for (int64_t i = 0; i < l; i++) {
+        uint16_t c = u[i];
+        if (c >= 1 && c <= 0x7F) {
+          *q++ = (uint8_t)c;
+        } else if (c > 0x7FF) {
+          *q++ = (uint8_t)(0xE0 | ((c >> 12) & 0x0F));
+          *q++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
+          *q++ = (uint8_t)(0x80 | (c & 0x3F));
+        } else {
+          *q++ = (uint8_t)(0xC0 | ((c >> 6) & 0x1F));
+          *q++ = (uint8_t)(0x80 | (c & 0x3F));
+        }
+      }
+      put_be32(q, 1u);  // stored df of a real term (T1)
+      put_be32(q + 4, (uint32_t)df);
+      if (df > 0) {
+        q[8] = 0;
+        q[9] = (uint8_t)kClassLen;
+        for (int i = 0; i < kClassLen; i++) q[10 + i] = (uint8_t)"sa.edu.kaust.io.PostingWritable"[i];
+      }
+    }
+    for (int64_t i = lane; i < df; i += 64) {
+      put_be32(post + 8 * i, (uint32_t)docno_o[p0 + i]);
+      put_be32(post + 8 * i + 4, (uint32_t)tf_o[p0 + i]);
+    }
+  }
+}
+
+__global__ void k_ser_space(const int32_t *rec_docno, int64_t N, uint8_t *o) {
+  // key: k=1, writeUTF(" "), df = N ; value: n = N, class, postings
+  const int64_t key = 11, val = 4 + 2 + kClassLen + 8 * N;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    put_be32(o, (uint32_t)(key + val));
+    put_be32(o + 4, (uint32_t)key);
+    put_be32(o + 8, 1u);
+    o[12] = 0;
+    o[13] = 1;
+    o[14] = ' ';
+    put_be32(o + 15, (uint32_t)N);
+    put_be32(o + 19, (uint32_t)N);
+    o[23] = 0;
+    o[24] = (uint8_t)kClassLen;
+    for (int i = 0; i < kClassLen; i++) o[25 + i] = (uint8_t)"sa.edu.kaust.io.PostingWritable"[i];
+  }
+  uint8_t *post = o + 25 + kClassLen;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t d = i == 0 ? 0u : (uint32_t)rec_docno[i - 1];
+    put_be32(post + 8 * i, d);
+    put_be32(post + 8 * i + 4, i == 0 ? 0u : 1u);
+  }
+}
+
+__global__ void k_gather_bytes(const uint32_t *g, const int64_t *rb, int64_t n, int64_t *gb) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    gb[i] = rb[g[i]];
+}
+
+void serialize_index(sme_index *ix, hipStream_t st) {
+  if (ix->ser_ready) return;
+  auto &W = ix->ctx->ws;
+  const int64_t V = ix->V, N = ix->N;
+  const int R = ix->R;
+  int64_t *rec_bytes = W[48].as<int64_t>(V + 1);
+  uint32_t *part = W[49].as<uint32_t>(V + 1), *idx = W[50].as<uint32_t>(V + 1);
+  uint32_t *part2 = W[51].as<uint32_t>(V + 1), *idx2 = W[52].as<uint32_t>(V + 1);
+  int64_t *grp_bytes = W[53].as<int64_t>(V + 1), *scan = W[54].as<int64_t>(V + 1);
+  unsigned long long *psum = W[55].as<unsigned long long>(R + 1);
+  SME_HIP(hipMemsetAsync(psum, 0, (R + 1) * sizeof(unsigned long long), st));
+  const int G = (int)std::min<int64_t>(std::max<int64_t>((V + 255) / 256, 1), 8192);
+  if (V > 0)
+    hipLaunchKernelGGL(k_ser_sizes, dim3(G), dim3(256), 0, st, (const int64_t *)ix->d_term_off.p,
+                       (const uint16_t *)ix->d_term_chars.p, (const int64_t *)ix->d_off.p, V, R, rec_bytes, part, idx,
+                       psum);
+  SME_CHECK_LAUNCH();
+  std::vector<unsigned long long> hps(R + 1);
+  SME_HIP(hipMemcpyAsync(hps.data(), psum, (R + 1) * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  SME_HIP(hipStreamSynchronize(st));
+  const uint32_t part_sp = (uint32_t)((31 + 32) % R);  // Arrays.hashCode({" "}) = 31 + 32
+  const int64_t sp_bytes = N > 0 ? 8 + 11 + 4 + 2 + kClassLen + 8 * N : 0;
+  ix->part_start.assign(R + 1, 0);
+  for (int p = 0; p < R; p++) {
+    ix->part_start[p + 1] = ix->part_start[p] + (int64_t)hps[p] + (p == (int)part_sp ? sp_bytes : 0);
+  }
+  const int64_t total = ix->part_start[R];
+  uint8_t *out = ix->d_ser.as<uint8_t>(total + 16);
+  if (V > 0) {
+    int bits = 1;
+    while ((1 << bits) < R) bits++;
+    size_t tb = 0;
+    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, part, part2, idx, idx2, (int)V, 0, bits, st));
+    SME_HIP(hipcub::DeviceRadixSort::SortPairs(ix->ctx->cub_tmp.get(tb), tb, part, part2, idx, idx2, (int)V, 0, bits,
+                                               st));
+    hipLaunchKernelGGL(k_gather_bytes, dim3(G), dim3(256), 0, st, idx2, rec_bytes, V, grp_bytes);
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, grp_bytes, scan, (int)V, st));
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tb), tb, grp_bytes, scan, (int)V, st));
+    int64_t *rec_off = grp_bytes;  // reuse after scan
+    hipLaunchKernelGGL(k_ser_offsets, dim3(G), dim3(256), 0, st, idx2, scan, V, part, part_sp, sp_bytes, rec_off);
+    hipLaunchKernelGGL(k_ser_write, dim3((unsigned)std::min<int64_t>((V + 3) / 4, 65536)), dim3(256), 0, st,
+                       (const int64_t *)ix->d_term_off.p, (const uint16_t *)ix->d_term_chars.p,
+                       (const int64_t *)ix->d_off.p, (const int32_t *)ix->d_docno_o.p, (const int32_t *)ix->d_tf_o.p,
+                       V, rec_off, out);
+    SME_CHECK_LAUNCH();
+  }
+  if (N > 0) {
+    hipLaunchKernelGGL(k_ser_space, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 8192)), dim3(256), 0, st,
+                       (const int32_t *)ix->d_rec_docno.p, N, out + ix->part_start[part_sp]);
+    SME_CHECK_LAUNCH();
+  }
+  SME_HIP(hipStreamSynchronize(st));
+  ix->ser_ready = true;
+  ix->h_parts.assign(R, {});
+  ix->h_parts_ready.assign(R, 0);
+}
+
+}  // namespace sme

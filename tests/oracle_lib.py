@@ -45,11 +45,29 @@ def lib():
     return _lib
 
 
+def mutf8_decode(b):
+    """DataInput.readUTF body -> str; surrogate pairs are combined like Java strings."""
+    units, i = [], 0
+    while i < len(b):
+        c = b[i]
+        if c < 0x80:
+            units.append(c)
+            i += 1
+        elif c & 0xE0 == 0xC0:
+            units.append(((c & 0x1F) << 6) | (b[i + 1] & 0x3F))
+            i += 2
+        else:
+            units.append(((c & 0x0F) << 12) | ((b[i + 1] & 0x3F) << 6) | (b[i + 2] & 0x3F))
+            i += 3
+    raw = b"".join(u.to_bytes(2, "little") for u in units)
+    return raw.decode("utf-16-le", "surrogatepass")
+
+
 def _decode_toks(buf, n, ntok):
     out, k = [], 0
     for _ in range(ntok):
         ln = (buf[k] << 8) | buf[k + 1]
-        out.append(bytes(buf[k + 2:k + 2 + ln]).decode("utf-8", "surrogatepass"))
+        out.append(mutf8_decode(bytes(buf[k + 2:k + 2 + ln])))
         k += 2 + ln
     return out
 
@@ -78,7 +96,7 @@ def stem(word):
     b = word.encode("utf-8")
     buf = (C.c_ubyte * (4 * len(b) + 16))()
     r = lib().or_stem_utf8(b, len(b), buf, len(buf))
-    return bytes(buf[:r]).decode("utf-8")
+    return mutf8_decode(bytes(buf[:r]))
 
 
 def is_stopword(word):
@@ -131,7 +149,7 @@ class OracleIndex:
             gram = []
             for g in range(k):
                 ln = L.or_index_term_gram(self._h, t, g, buf, len(buf))
-                gram.append(bytes(buf[:ln]).decode("utf-8", "surrogatepass"))
+                gram.append(mutf8_decode(bytes(buf[:ln])))
             n = L.or_index_term_npost(self._h, t)
             d = (C.c_int32 * max(n, 1))()
             f = (C.c_int32 * max(n, 1))()

@@ -1,0 +1,138 @@
+"""Device path (libsme.so on gfx950) against the CPU oracle: tokenizer, index
+records (bit-exact), CSR, and query top-k."""
+import json
+import os
+import random
+
+import common
+import numpy as np
+import oracle_lib as O
+import pytest
+
+pytestmark = pytest.mark.gpu
+KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kat_appendix_b.json")))
+
+
+@pytest.fixture(scope="module")
+def ctx(sme):
+    return sme.Context(1, 1)
+
+
+@pytest.mark.parametrize("text,expected", KAT["process_content"])
+def test_device_process_content_kat(ctx, text, expected):
+    assert ctx.process_content(text) == expected
+
+
+@pytest.mark.parametrize("word,expected", KAT["stem"])
+def test_device_stem_kat(ctx, word, expected):
+    assert ctx.process_content(word) == ([] if O.is_stopword(word) else [expected])
+
+
+def test_device_process_content_fuzz(ctx):
+    rng = random.Random(1234)
+    for i in range(300):
+        doc = common.fuzz_doc(rng, "X%d" % i, rng.randint(1, 40))
+        assert ctx.process_content(doc) == O.process_content(doc), doc
+
+
+def _check_build(sme, corpus, mapping_ids, R=1, idf_mode=0):
+    mb = O.write_mapping(mapping_ids)
+    ref = O.OracleIndex(corpus, mb, 1, R)
+    ctx = sme.Context(1, R, idf_mode)
+    ctx.load_docno_mapping(mb)
+    ix = ctx.build(corpus)
+    assert ix.N == ref.N
+    for p in range(R):
+        common.compare_partitions(ix.partition_records(p), ref.partition_bytes(p))
+    # CSR view equals the oracle's reduce output
+    off, dn, tf, df = ix.csr()
+    rterms = sorted([t for t in ref.terms() if t[0] != (" ",)], key=lambda t: t[0][0].encode("utf-16-be", "surrogatepass"))
+    assert ix.V == len(rterms)
+    assert ix.P == sum(len(t[3]) for t in rterms)
+    for i, t in enumerate(rterms):
+        assert ix.term(i) == t[0][0]
+        got = list(zip(dn[off[i]:off[i + 1]].tolist(), tf[off[i]:off[i + 1]].tolist()))
+        assert got == [tuple(p) for p in t[3]]
+    return ix, ref
+
+
+def test_build_kat(sme):
+    _check_build(sme, KAT["index_corpus"].encode(), KAT["index_mapping"], R=1)
+    _check_build(sme, KAT["index_corpus"].encode(), KAT["index_mapping"], R=10)
+
+
+def test_build_synthetic(sme, synth):
+    n = 400
+    c = synth.gen_corpus(n, V=5000, seed=1, len_lo=50, len_hi=150)
+    _check_build(sme, c, synth.docids(n), R=1)
+    _check_build(sme, c, synth.docids(n), R=10)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_build_fuzz(sme, seed):
+    corpus, ids = common.fuzz_corpus(seed, 120)
+    _check_build(sme, corpus, ids, R=1)
+    _check_build(sme, corpus, ids, R=7)
+
+
+def test_build_invalid_utf8_and_big_record(sme):
+    rng = random.Random(7)
+    docs = []
+    for i in range(20):
+        body = bytes(rng.choice([0x41, 0x62, 0x20, 0xC3, 0xA9, 0xE2, 0x82, 0xFF, 0xF0, 0x9F, 0x98, 0x80, 0x2E, 0x27])
+                     for _ in range(rng.randint(0, 300)))
+        docs.append(b"<DOC><DOCNO>U%02d</DOCNO>" % i + body + b" </DOC>\n")
+    # one record with many distinct terms (global-table aggregation path)
+    big = " ".join("t%05d" % i for i in range(5000)).encode()
+    docs.append(b"<DOC><DOCNO>BIG</DOCNO>" + big + b"</DOC>")
+    _check_build(sme, b"".join(docs), sorted(["U%02d" % i for i in range(20)] + ["BIG"]), R=3)
+
+
+def test_build_empty_and_no_records(sme):
+    with pytest.raises(sme.SmeError):
+        ctx = sme.Context(1, 1)
+        ctx.load_docno_mapping(O.write_mapping(["A"]))
+        ctx.build(b"<DOC><DOCNO>A x </DOC>")  # getDocid throws in the reference
+    ctx = sme.Context(1, 1)
+    ctx.load_docno_mapping(O.write_mapping(["A"]))
+    ix = ctx.build(b"no records here")
+    assert (ix.N, ix.V, ix.P) == (0, 0, 0)
+
+
+@pytest.mark.parametrize("idf_mode", [0, 1])
+def test_queries_vs_oracle(sme, synth, idf_mode):
+    n = 300
+    c = synth.gen_corpus(n, V=3000, seed=11, len_lo=40, len_hi=120)
+    ix, ref = _check_build(sme, c, synth.docids(n), R=1, idf_mode=idf_mode)
+    _, _, _, df = ix.csr()
+    terms, qoff = synth.queries_by_df(df, 200, seed=7)
+    terms[::17] = -1  # unknown terms are skipped
+    dn, sc = ix.query_topk(terms, qoff, 10)
+    names = [ix.term(i) for i in range(ix.V)]
+    for q in range(len(qoff) - 1):
+        tl = [names[t] for t in terms[qoff[q]:qoff[q + 1]] if t >= 0]
+        rd, rs = ref.query(tl, 10, idf_mode, 0)
+        k = len(rd)
+        assert dn[q, :k].tolist() == rd, q
+        assert np.array_equal(sc[q, :k], np.array(rs)), q  # fp64 bit-exact (same op order)
+        assert (dn[q, k:] == -1).all()
+
+
+def test_single_term_queries_match_reference_sort(sme, synth):
+    """For single-term queries the reference's Collections.sort on DocScore
+    leaves the stored (tf desc, docno asc) order: equal to the docno tie-break."""
+    n = 200
+    c = synth.gen_corpus(n, V=2000, seed=12, len_lo=40, len_hi=80)
+    ix, ref = _check_build(sme, c, synth.docids(n), R=1)
+    for t in range(0, ix.V, max(1, ix.V // 50)):
+        dn, sc = ix.query_topk(np.array([t], np.int32), np.array([0, 1], np.int64), 10)
+        rd, rs = ref.query([ix.term(t)], 10, 0, 1)
+        assert dn[0, :len(rd)].tolist() == rd
+
+
+def test_forward_index_facade(sme):
+    indexer = sme.TermKGramDocIndexer(k=1, num_reduce_tasks=1)
+    ix = indexer.run(KAT["index_corpus"].encode(), O.write_mapping(KAT["index_mapping"]))
+    fw = sme.IntDocVectorsForwardIndex(ix)
+    fw.getValue(["cat", "dog", "unknownterm"])
+    assert fw.rank() == [1, 2]
