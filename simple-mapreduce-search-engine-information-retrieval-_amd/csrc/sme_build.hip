@@ -134,29 +134,48 @@ struct ScanOut {
   unsigned long long *cnt;  // [3]
 };
 
+__device__ __forceinline__ void scan_lt(const uint8_t *__restrict__ t, int64_t n, int64_t p, const ScanOut &o) {
+  if (p + 5 <= n && t[p + 1] == 'D' && t[p + 2] == 'O' && t[p + 3] == 'C' && t[p + 4] == '>') {
+    if (doc_tag_valid(t, p, "<DOC>", 5)) {
+      unsigned long long i = atomicAdd(&o.cnt[0], 1ull);
+      if (i < o.capS) o.S[i] = (uint64_t)p;
+    }
+  } else if (p + 6 <= n && t[p + 1] == '/' && t[p + 2] == 'D' && t[p + 3] == 'O' && t[p + 4] == 'C' &&
+             t[p + 5] == '>') {
+    if (doc_tag_valid(t, p, "</DOC>", 6)) {
+      unsigned long long i = atomicAdd(&o.cnt[1], 1ull);
+      if (i < o.capE) o.E[i] = (uint64_t)p;
+    }
+  }
+  if (!lt_simple(t, n, p)) {
+    unsigned long long i = atomicAdd(&o.cnt[2], 1ull);
+    if (i < o.capC) o.C[i] = (uint64_t)p;
+  }
+}
+
+__device__ __forceinline__ uint32_t has_lt(uint32_t w) {  // bytes equal to '<' (0x3C)
+  uint32_t x = w ^ 0x3C3C3C3Cu;
+  return (x - 0x01010101u) & ~x & 0x80808080u;
+}
+
+// One pass over the text with coalesced 16-byte loads: consecutive lanes read
+// consecutive 16-byte words; only words containing '<' are looked at bytewise.
 __global__ void k_scan_tags(const uint8_t *__restrict__ t, int64_t n, ScanOut o) {
-  const int64_t nseg = (n + 63) / 64;
-  for (int64_t seg = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; seg < nseg;
-       seg += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b0 = seg * 64;
-    const int64_t b1 = b0 + 64 < n ? b0 + 64 : n;
-    for (int64_t p = b0; p < b1; p++) {
-      if (t[p] != '<') continue;
-      if (p + 5 <= n && t[p + 1] == 'D' && t[p + 2] == 'O' && t[p + 3] == 'C' && t[p + 4] == '>') {
-        if (doc_tag_valid(t, p, "<DOC>", 5)) {
-          unsigned long long i = atomicAdd(&o.cnt[0], 1ull);
-          if (i < o.capS) o.S[i] = (uint64_t)p;
-        }
-      } else if (p + 6 <= n && t[p + 1] == '/' && t[p + 2] == 'D' && t[p + 3] == 'O' && t[p + 4] == 'C' &&
-                 t[p + 5] == '>') {
-        if (doc_tag_valid(t, p, "</DOC>", 6)) {
-          unsigned long long i = atomicAdd(&o.cnt[1], 1ull);
-          if (i < o.capE) o.E[i] = (uint64_t)p;
-        }
-      }
-      if (!lt_simple(t, n, p)) {
-        unsigned long long i = atomicAdd(&o.cnt[2], 1ull);
-        if (i < o.capC) o.C[i] = (uint64_t)p;
+  const uintptr_t mis = (uintptr_t)t & 15;
+  const uint4 *a = reinterpret_cast<const uint4 *>(t - mis);
+  const int64_t nv = (int64_t)((n + mis + 15) >> 4);
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 q = a[v];
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (!has_lt(w[k])) continue;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (((w[k] >> (8 * j)) & 0xFF) != '<') continue;
+        const int64_t p = 16 * v + 4 * k + j - (int64_t)mis;
+        if (p < 0 || p >= n) continue;
+        scan_lt(t, n, p, o);
       }
     }
   }
@@ -306,55 +325,83 @@ __global__ void k_mark_slow(const uint64_t *rs, const uint64_t *re, int64_t nR, 
 }
 
 // ============================================================================
-// raw-token vocabulary (open addressing, exact: verified against the bytes)
+// raw-token vocabulary (open addressing, exact)
 // ============================================================================
+// One 32-byte slot per distinct raw token: hash, (byte offset << 24 | length) of
+// a representative occurrence, and the first 16 bytes of the token inline, so a
+// lookup of a token of <= 16 bytes is decided from the slot's cache line alone.
+// Slots are written once (0 -> value).  A plain read may return a stale 0 from
+// another XCD's L2; "found" is only concluded from non-zero final values, and a
+// mismatch is re-checked with coherent (RMW) reads before probing on.
+struct RawSlot {
+  unsigned long long key, rep, w0, w1;
+};
 struct RawTable {
-  unsigned long long *keys;  // 0 = empty
-  unsigned long long *reps;  // (byte offset << 24) | len, 0 = not yet published
+  RawSlot *slots;
   uint64_t mask;
   const uint8_t *text;
   unsigned int *overflow;
+  unsigned long long *count;  // distinct raw tokens inserted
 };
 
-__device__ __forceinline__ uint64_t hash_bytes(const uint8_t *p, int64_t len) {
-  uint64_t h = 0xcbf29ce484222325ull;
-  for (int64_t i = 0; i < len; i++) {
-    h ^= p[i];
-    h *= 0x100000001b3ull;
-  }
-  h = fmix64(h ^ (uint64_t)len);
-  return h ? h : 1;
+struct TokSig {
+  uint64_t h, w0, w1;
+};
+__device__ __forceinline__ void sig_add(TokSig &g, uint8_t b, int64_t i) {
+  g.h ^= b;
+  g.h *= 0x100000001b3ull;
+  if (i < 8)
+    g.w0 |= (uint64_t)b << (8 * i);
+  else if (i < 16)
+    g.w1 |= (uint64_t)b << (8 * (i - 8));
+}
+__device__ __forceinline__ void sig_end(TokSig &g, int64_t len) {
+  g.h = fmix64(g.h ^ (uint64_t)len);
+  g.h = g.h ? g.h : 1;
+}
+__device__ __forceinline__ TokSig sig_bytes(const uint8_t *p, int64_t len) {
+  TokSig g{0xcbf29ce484222325ull, 0, 0};
+  for (int64_t i = 0; i < len; i++) sig_add(g, p[i], i);
+  sig_end(g, len);
+  return g;
 }
 
-__device__ uint32_t raw_insert(const RawTable &tb, uint64_t h, uint64_t off, uint64_t len) {
+__device__ uint32_t raw_insert(const RawTable &tb, const TokSig &g, uint64_t off, uint64_t len) {
   if (len >= (1ull << 24)) {
     atomicOr(tb.overflow, 2u);
     return 0xFFFFFFFFu;
   }
   const uint64_t rep_me = (off << 24) | len;
-  uint64_t slot = h & tb.mask;
+  uint64_t slot = g.h & tb.mask;
   for (uint64_t probe = 0; probe <= tb.mask; probe++) {
-    unsigned long long k = tb.keys[slot];
+    RawSlot *s = &tb.slots[slot];
+    unsigned long long k = s->key;
     if (k == 0) {
-      unsigned long long old = atomicCAS(&tb.keys[slot], 0ull, (unsigned long long)h);
+      unsigned long long old = atomicCAS(&s->key, 0ull, (unsigned long long)g.h);
       if (old == 0) {
-        atomicExch(&tb.reps[slot], (unsigned long long)rep_me);
+        atomicExch(&s->w0, (unsigned long long)g.w0);
+        atomicExch(&s->w1, (unsigned long long)g.w1);
+        __threadfence();
+        atomicExch(&s->rep, (unsigned long long)rep_me);
+        atomicAdd(tb.count, 1ull);
         return (uint32_t)slot;
       }
       k = old;
     }
-    if (k == h) {
-      unsigned long long r = tb.reps[slot];
-      for (int spin = 0; r == 0 && spin < (1 << 22); spin++) r = atomicOr(&tb.reps[slot], 0ull);
+    if (k == g.h) {
+      unsigned long long r = s->rep;
+      for (int spin = 0; r == 0 && spin < (1 << 22); spin++) r = atomicOr(&s->rep, 0ull);
       if (r == 0) {
         atomicOr(tb.overflow, 4u);
         return 0xFFFFFFFFu;
       }
-      uint64_t ro = r >> 24, rl = r & 0xFFFFFFull;
-      if (rl == len) {
-        if (ro == off) return (uint32_t)slot;
-        bool eq = true;
-        for (uint64_t i = 0; i < len && eq; i++) eq = tb.text[ro + i] == tb.text[off + i];
+      if ((r & 0xFFFFFFull) == len) {
+        bool eq = s->w0 == g.w0 && s->w1 == g.w1;
+        if (!eq) eq = atomicOr(&s->w0, 0ull) == g.w0 && atomicOr(&s->w1, 0ull) == g.w1;
+        if (eq && len > 16) {
+          const uint64_t ro = r >> 24;
+          for (uint64_t i = 16; i < len && eq; i++) eq = tb.text[ro + i] == tb.text[off + i];
+        }
         if (eq) return (uint32_t)slot;
       }
     }
@@ -369,80 +416,129 @@ __device__ uint32_t raw_insert(const RawTable &tb, uint64_t h, uint64_t off, uin
 // ============================================================================
 constexpr int kTokNT = 256;
 constexpr int kTokBytes = 16;
+constexpr int kChunk = kTokNT * kTokBytes;  // 4 KiB of text per block iteration
+constexpr int kStageV = kTokNT + 64;         // staged 16-byte words: chunk + 1 KiB lookahead
 
 // entity span end: '&' [a-z0-9#]* ';'  (TagTokenizer.onAmpersand 644-662); p if none
-__device__ __forceinline__ int64_t amp_span_end(const uint8_t *t, int64_t e, int64_t p) {
+template <typename B>
+__device__ __forceinline__ int64_t amp_span_end_f(B &&byte, int64_t e, int64_t p) {
   for (int64_t i = p + 1; i < e; i++) {
-    uint8_t d = t[i];
+    uint8_t d = byte(i);
     if ((d >= 'a' && d <= 'z') || (d >= '0' && d <= '9') || d == '#') continue;
     return d == ';' ? i : p;
   }
   return p;
 }
+// markup span end for '<' at p in a simple record (see lt_simple)
+template <typename B>
+__device__ __forceinline__ int64_t lt_span_end_f(B &&byte, int64_t n, int64_t p) {
+  if (p + 1 >= n) return n;
+  uint8_t c = byte(p + 1);
+  if (c == '!' && p + 3 < n && byte(p + 2) == '-' && byte(p + 3) == '-') {
+    for (int64_t i = p + 1; i + 2 < n; i++)
+      if (byte(i) == '-' && byte(i + 1) == '-' && byte(i + 2) == '>') return i + 2;
+    return n;
+  }
+  if (c == '?') {
+    for (int64_t i = p + 1; i + 1 < n; i++)
+      if (byte(i) == '?' && byte(i + 1) == '>') return i + 1;
+    return n;
+  }
+  for (int64_t i = p + (c == '/' ? 2 : 1); i < n; i++)
+    if (byte(i) == '>') return i;
+  return n;
+}
 
-__global__ __launch_bounds__(kTokNT) void k_tok_fast(const uint8_t *__restrict__ t, const uint64_t *rs,
+// Byte-parallel TagTokenizer for records whose markup is simple: a raw token is
+// a maximal run of non-split bytes whose first byte lies outside every tag /
+// comment / PI / entity span (spans begin and end on split characters, so a run
+// is either wholly inside a span or wholly outside).  The block walks the record
+// in 4 KiB chunks: coalesced 16-byte loads into LDS, per-lane split classes over
+// 16 bytes, span coverage by a block max-scan, token order by a block sum-scan.
+__global__ __launch_bounds__(kTokNT) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n, const uint64_t *rs,
                                                      const uint64_t *re, int64_t nR, const uint8_t *slow,
                                                      uint32_t *tokstream, int32_t *ntok, RawTable tb) {
+  __shared__ uint4 st4[kStageV];
   __shared__ int64_t sc64[kTokNT / 64 + 1];
   __shared__ int32_t sc32[kTokNT / 64 + 1];
+  const int64_t mis = (int64_t)((uintptr_t)t & 15);
+  const uint4 *a4 = reinterpret_cast<const uint4 *>(t - mis);
+  const int64_t nq = n + mis;  // aligned address space: position p lives at q = p + mis
+  const uint8_t *stg = reinterpret_cast<const uint8_t *>(st4);
+  const int tid = threadIdx.x;
   for (int64_t r = blockIdx.x; r < nR; r += gridDim.x) {
     if (slow[r]) continue;
     const int64_t s = (int64_t)rs[r], e = (int64_t)re[r];
     uint32_t *out = tokstream + (s >> 1);
-    int64_t mask_carry = -1;  // max span end of markup that started before this chunk
+    int64_t mask_carry = -1;  // furthest span end of markup that started in earlier chunks
     int32_t tok_carry = 0;
-    for (int64_t c0 = s; c0 < e; c0 += (int64_t)kTokNT * kTokBytes) {
-      const int64_t p0 = c0 + (int64_t)threadIdx.x * kTokBytes;
-      // pass 1: candidates (non-split byte after a split byte) and in-lane masking
+    uint8_t last_prev = ' ';  // byte before the chunk (record start counts as a split)
+    for (int64_t Q = (s + mis) & ~(int64_t)15; Q < e + mis; Q += kChunk) {
+      for (int i = tid; i < kStageV; i += kTokNT) {
+        const int64_t q = Q + 16 * (int64_t)i;
+        st4[i] = q < nq ? a4[q >> 4] : make_uint4(0, 0, 0, 0);
+      }
+      __syncthreads();
+      auto byte_at = [&](int64_t p) -> uint8_t {
+        const int64_t o = p + mis - Q;
+        return (o >= 0 && o < kStageV * 16) ? stg[o] : t[p];
+      };
+      const int64_t p0 = Q + 16 * (int64_t)tid - mis;
+      // pass 1: token-start candidates and spans over this lane's 16 bytes
       uint32_t cand = 0;
       int64_t lane_max = -1;
-      uint8_t prev = (p0 > s && p0 - 1 < e) ? t[p0 - 1] : (uint8_t)' ';
+      uint8_t prev = tid == 0 ? last_prev : stg[16 * tid - 1];
+      if (p0 - 1 < s) prev = ' ';
+      const uint4 v = st4[tid];
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
       for (int i = 0; i < kTokBytes; i++) {
-        int64_t p = p0 + i;
-        if (p >= e) break;
-        uint8_t b = t[p];
-        bool sp = is_split_byte(b);
-        if (!sp && is_split_byte(prev) && lane_max < p) cand |= 1u << i;
-        if (b == '<') {
-          int64_t q = lt_span_end(t, e, p);
-          lane_max = q > lane_max ? q : lane_max;
-        } else if (b == '&') {
-          int64_t q = amp_span_end(t, e, p);
-          lane_max = q > lane_max ? q : lane_max;
+        const int64_t p = p0 + i;
+        const uint8_t b = (uint8_t)(wv[i >> 2] >> (8 * (i & 3)));
+        if (p >= s && p < e) {
+          const bool sp = is_split_byte(b);
+          if (!sp && is_split_byte(prev) && lane_max < p) cand |= 1u << i;
+          if (b == '<') {
+            int64_t q = lt_span_end_f(byte_at, e, p);
+            lane_max = q > lane_max ? q : lane_max;
+          } else if (b == '&') {
+            int64_t q = amp_span_end_f(byte_at, e, p);
+            lane_max = q > lane_max ? q : lane_max;
+          }
         }
-        prev = b;
+        prev = p < s ? (uint8_t)' ' : b;
       }
       int64_t blk_max;
       int64_t before = block_excl_max<kTokNT, int64_t>(lane_max, (int64_t)-1, sc64, &blk_max);
       before = before > mask_carry ? before : mask_carry;
-      // drop candidates covered by markup that started in an earlier lane / chunk
       uint32_t keep = 0;
+#pragma unroll
       for (int i = 0; i < kTokBytes; i++)
         if (((cand >> i) & 1u) && p0 + i > before) keep |= 1u << i;
-      int32_t cnt = __popc(keep);
       int32_t blk_cnt;
-      int32_t idx = block_excl_sum<kTokNT, int32_t>(cnt, sc32, &blk_cnt) + tok_carry;
-      // pass 2: hash each kept token [x, first split byte) and insert
+      int32_t idx = block_excl_sum<kTokNT, int32_t>(__popc(keep), sc32, &blk_cnt) + tok_carry;
+      // pass 2: hash each kept token [x, first split byte) and insert it
       while (keep) {
-        int i = __ffs(keep) - 1;
+        const int i = __ffs(keep) - 1;
         keep &= keep - 1;
-        int64_t x = p0 + i, y = x;
-        uint64_t h = 0xcbf29ce484222325ull;
+        const int64_t x = p0 + i;
+        int64_t y = x;
+        TokSig g{0xcbf29ce484222325ull, 0, 0};
         while (y < e) {
-          uint8_t b = t[y];
+          const uint8_t b = byte_at(y);
           if (is_split_byte(b)) break;
-          h ^= b;
-          h *= 0x100000001b3ull;
+          sig_add(g, b, y - x);
           y++;
         }
-        h = fmix64(h ^ (uint64_t)(y - x));
-        h = h ? h : 1;
-        out[idx++] = raw_insert(tb, h, (uint64_t)x, (uint64_t)(y - x));
+        sig_end(g, y - x);
+        out[idx++] = raw_insert(tb, g, (uint64_t)x, (uint64_t)(y - x));
       }
       mask_carry = blk_max > mask_carry ? blk_max : mask_carry;
       tok_carry += blk_cnt;
+      last_prev = stg[kChunk - 1];
+      __syncthreads();  // stage is overwritten by the next chunk
     }
-    if (threadIdx.x == 0) ntok[r] = tok_carry;
+    if (tid == 0) ntok[r] = tok_carry;
   }
 }
 
@@ -475,8 +571,7 @@ __global__ void k_tok_slow(const uint8_t *__restrict__ t, const uint64_t *rs, co
     sc.n = (int)nu;
     sc.run([&](int u0, int u1) {
       uint64_t x = (uint64_t)s + bo[u0], len = bo[u1] - bo[u0];
-      uint64_t h = hash_bytes(t + x, (int64_t)len);
-      out[cnt++] = raw_insert(tb, h, x, len);
+      out[cnt++] = raw_insert(tb, sig_bytes(t + x, (int64_t)len), x, len);
     });
     ntok[r] = cnt;
   }
@@ -494,6 +589,7 @@ struct CandOut {
   unsigned long long *ncand;
   uint64_t cand_cap;
   int32_t *raw_nout;
+  int32_t *max_nout;
 };
 
 __device__ void emit_final(const CandOut &co, uint32_t slot, uint32_t ordinal, const uint16_t *w, int l) {
@@ -522,6 +618,28 @@ __device__ void vocab_one(const CandOut &co, uint32_t slot, const uint16_t *unit
     ord++;
   });
   co.raw_nout[slot] = (int32_t)ord;
+  if (ord > 1) atomicMax(co.max_nout, (int32_t)ord);
+}
+
+// Fast path for the common raw token: only [a-z0-9] (checkTokenStatus == Clean), so
+// normalization is the identity and the token goes straight to stop list + stemmer.
+__device__ bool vocab_clean(const CandOut &co, uint32_t slot, const uint8_t *p, uint64_t len) {
+  if (len > 48) return false;
+  StemmerT<64> st;
+  for (uint64_t i = 0; i < len; i++) {
+    uint8_t c = p[i];
+    if (!((c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'))) return false;
+    st.b[i] = c;
+  }
+  uint32_t ord = 0;
+  if (!(len > 100 / 6 && len >= 100) && !is_stopword(st.b, (int)len)) {
+    st.len = (int)len;
+    st.run();
+    emit_final(co, slot, 0, st.b, st.len);
+    ord = 1;
+  }
+  co.raw_nout[slot] = (int32_t)ord;
+  return true;
 }
 
 constexpr int kShortRaw = 200;
@@ -530,9 +648,10 @@ __global__ void k_vocab(const RawTable tb, CandOut co, int64_t *long_list, unsig
                         uint64_t long_cap) {
   for (uint64_t slot = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; slot <= tb.mask;
        slot += (uint64_t)gridDim.x * blockDim.x) {
-    if (tb.keys[slot] == 0) continue;
-    uint64_t r = tb.reps[slot];
+    if (tb.slots[slot].key == 0) continue;
+    uint64_t r = tb.slots[slot].rep;
     uint64_t off = r >> 24, len = r & 0xFFFFFFull;
+    if (vocab_clean(co, (uint32_t)slot, tb.text + off, len)) continue;
     if (len > kShortRaw) {
       unsigned long long i = atomicAdd(nlong, 1ull);
       if (i < long_cap) long_list[i] = (int64_t)slot;
@@ -556,7 +675,7 @@ __global__ void k_vocab_long(const RawTable tb, CandOut co, const int64_t *long_
                              const int64_t *scr_off, uint16_t *scr) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nlong; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t slot = (uint64_t)long_list[i];
-    uint64_t r = tb.reps[slot];
+    uint64_t r = tb.slots[slot].rep;
     uint64_t off = r >> 24, len = r & 0xFFFFFFull;
     uint16_t *units = scr + scr_off[i];
     int nu = 0;
@@ -626,23 +745,29 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
   }
 }
 
-// compact occupied final slots; build 128-bit big-endian prefix keys
+// compact occupied final slots; longest term (in units) for the LSD sort depth
 __global__ void k_final_compact(const unsigned long long *fkeys, const unsigned long long *freps, uint64_t fmask,
-                                const uint64_t *cand_str, const uint16_t *pool, unsigned long long *nV,
-                                uint32_t *vslot, uint64_t *khi, uint64_t *klo, uint32_t *vidx) {
+                                const uint64_t *cand_str, unsigned long long *nV, uint32_t *vslot, uint32_t *vidx,
+                                int32_t *maxlen) {
   for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s <= fmask; s += (uint64_t)gridDim.x * blockDim.x) {
     if (fkeys[s] == 0) continue;
     unsigned long long i = atomicAdd(nV, 1ull);
     vslot[i] = (uint32_t)s;
-    uint64_t cs = cand_str[freps[s] - 1];
-    const uint16_t *w = pool + (cs >> 16);
-    int l = (int)(cs & 0xFFFF);
-    uint64_t hi = 0, lo = 0;
-    for (int k = 0; k < 4; k++) hi = (hi << 16) | (k < l ? w[k] : 0);
-    for (int k = 4; k < 8; k++) lo = (lo << 16) | (k < l ? w[k] : 0);
-    khi[i] = hi;
-    klo[i] = lo;
     vidx[i] = (uint32_t)i;
+    atomicMax(maxlen, (int32_t)(cand_str[freps[s] - 1] & 0xFFFF));
+  }
+}
+
+// key word w (units 4w..4w+3, big-endian, zero padded) of the term at each order position
+__global__ void k_term_word(const uint32_t *order, int64_t V, const uint32_t *vslot, const unsigned long long *freps,
+                            const uint64_t *cand_str, const uint16_t *pool, int w, uint64_t *key) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t cs = cand_str[freps[vslot[order[i]]] - 1];
+    const uint16_t *u = pool + (cs >> 16);
+    int l = (int)(cs & 0xFFFF);
+    uint64_t k = 0;
+    for (int j = 4 * w; j < 4 * w + 4; j++) k = (k << 16) | (j < l ? u[j] : 0);
+    key[i] = k;
   }
 }
 
@@ -655,15 +780,26 @@ __device__ int cmp_pool(const uint16_t *pool, uint64_t a, uint64_t b) {
   return xl - yl;
 }
 
-// order[] sorted by (hi, lo) prefix; fix runs of equal prefixes by full comparison
-__global__ void k_final_fixup(const uint64_t *khi_s, const uint64_t *klo_s, uint32_t *order, int64_t V,
-                              const uint32_t *vslot, const unsigned long long *freps, const uint64_t *cand_str,
-                              const uint16_t *pool) {
+__device__ bool same_prefix32(const uint16_t *pool, uint64_t a, uint64_t b) {
+  const uint16_t *x = pool + (a >> 16), *y = pool + (b >> 16);
+  int xl = (int)(a & 0xFFFF), yl = (int)(b & 0xFFFF);
+  for (int i = 0; i < 32; i++) {
+    uint16_t cx = i < xl ? x[i] : 0, cy = i < yl ? y[i] : 0;
+    if (cx != cy) return false;
+  }
+  return true;
+}
+
+// order[] is sorted by the 32-unit prefix; runs of equal prefixes (terms longer than
+// 32 units) are finished by full String.compareTo comparison
+__global__ void k_final_fixup(uint32_t *order, int64_t V, const uint32_t *vslot, const unsigned long long *freps,
+                              const uint64_t *cand_str, const uint16_t *pool) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
-    bool start = i == 0 || khi_s[i] != khi_s[i - 1] || klo_s[i] != klo_s[i - 1];
+    auto str = [&](int64_t pos) { return cand_str[freps[vslot[order[pos]]] - 1]; };
+    bool start = i == 0 || !same_prefix32(pool, str(i), str(i - 1));
     if (!start) continue;
     int64_t j = i + 1;
-    while (j < V && khi_s[j] == khi_s[i] && klo_s[j] == klo_s[i]) j++;
+    while (j < V && same_prefix32(pool, str(j), str(i))) j++;
     if (j - i < 2) continue;
     for (int64_t a = i + 1; a < j; a++) {  // insertion sort (runs are tiny)
       uint32_t v = order[a];
@@ -942,9 +1078,9 @@ __global__ void k_compact_flags(const uint8_t *flag, int64_t n, int64_t *list, u
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     if (flag[i]) list[atomicAdd(cnt, 1ull)] = i;
 }
-__global__ void k_long_lens(const int64_t *list, int64_t n, const unsigned long long *reps, int64_t *lens) {
+__global__ void k_long_lens(const int64_t *list, int64_t n, const RawSlot *slots, int64_t *lens) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    lens[i] = 5 * (int64_t)(reps[list[i]] & 0xFFFFFFull) + 32;
+    lens[i] = 5 * (int64_t)(slots[list[i]].rep & 0xFFFFFFull) + 32;
 }
 __global__ void k_big_list(const int32_t *prec, int64_t n, int64_t *list, unsigned long long *cnt) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -953,15 +1089,11 @@ __global__ void k_big_list(const int32_t *prec, int64_t n, int64_t *list, unsign
 __global__ void k_big_caps(const int64_t *list, int64_t nbig, const int64_t *perm, const int32_t *ntok,
                            const int32_t *max_nout, int64_t *caps) {
   for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nbig; b += (int64_t)gridDim.x * blockDim.x) {
-    int64_t need = (int64_t)ntok[perm[list[b]]] * (int64_t)(*max_nout) * 2 + 64;
+    int64_t need = (int64_t)ntok[perm[list[b]]] * (int64_t)max(*max_nout, 1) * 2 + 64;
     int64_t c = 1;
     while (c < need) c <<= 1;
     caps[b] = c;
   }
-}
-__global__ void k_max_nout(const int32_t *nout, const unsigned long long *keys, uint64_t cap, int32_t *mx) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x)
-    if (keys[i]) atomicMax(mx, nout[i]);
 }
 
 __global__ void k_gather_u64(const uint64_t *src, const uint32_t *idx, int64_t nn, uint64_t *dst) {
@@ -1057,7 +1189,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     so.capC = (uint32_t)std::min<uint64_t>(capC, 0xFFFFFFFFu);
     so.cnt = cnt;
     SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_scan_tags, dim3(grid_for((int64_t)ceil_div(n, 64), 256, 16384)), dim3(256), 0, st, t,
+    hipLaunchKernelGGL(k_scan_tags, dim3(grid_for((int64_t)ceil_div(n, 16), 256, 8192)), dim3(256), 0, st, t,
                        (int64_t)n, so);
     SME_CHECK_LAUNCH();
     SME_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof h_cnt, hipMemcpyDeviceToHost, st));
@@ -1150,17 +1282,17 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   RawTable tb;
   unsigned int *ovf = reinterpret_cast<unsigned int *>(cnt + 8);
   for (int attempt = 0;; attempt++) {
-    tb.keys = W[W_RKEYS].as<unsigned long long>(rcap);
-    tb.reps = W[W_RREPS].as<unsigned long long>(rcap);
+    tb.slots = W[W_RKEYS].as<RawSlot>(rcap);
     tb.mask = rcap - 1;
     tb.text = t;
     tb.overflow = ovf;
-    SME_HIP(hipMemsetAsync(tb.keys, 0, rcap * 8, st));
-    SME_HIP(hipMemsetAsync(tb.reps, 0, rcap * 8, st));
+    tb.count = W[W_MAXNOUT].as<unsigned long long>(4) + 1;
+    SME_HIP(hipMemsetAsync(tb.slots, 0, rcap * sizeof(RawSlot), st));
+    SME_HIP(hipMemsetAsync(tb.count, 0, 8, st));
     SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
     if (nR > 0) {
-      hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)std::min<int64_t>(nR, 65536)), dim3(kTokNT), 0, st, t, rs, re,
-                         nR, slow, tok, ntok, tb);
+      hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)std::min<int64_t>(nR, 65536)), dim3(kTokNT), 0, st, t,
+                         (int64_t)n, rs, re, nR, slow, tok, ntok, tb);
       SME_CHECK_LAUNCH();
     }
     if (nslow > 0) {
@@ -1189,10 +1321,14 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
 
   // ---------------- K4 vocabulary ----------------
   CandOut co;
-  uint64_t pool_cap = 1 << 22, cand_cap = 1 << 20;
+  const uint64_t nraw = d2h(tb.count, st);
+  uint64_t cand_cap = std::max<uint64_t>(cx->vocab_cand_cap, nraw + nraw / 8 + 1024);
+  uint64_t pool_cap = std::max<uint64_t>(cx->vocab_pool_cap, 12 * cand_cap);
   co.raw_nout = W[W_NOUT].as<int32_t>(rcap);
+  int32_t *max_nout = W[W_MAXNOUT].as<int32_t>(4);  // must survive the counter resets below
+  co.max_nout = max_nout;
   int64_t *long_list = nullptr;
-  uint64_t long_cap = 4096;
+  uint64_t long_cap = std::max<uint64_t>(cx->vocab_long_cap, 4096);
   int64_t ncand = 0, nlong = 0;
   for (int attempt = 0;; attempt++) {
     co.pool = W[W_POOL].as<uint16_t>(pool_cap);
@@ -1204,7 +1340,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     co.ncand = cnt + 4;
     long_list = W[W_LONG].as<int64_t>(long_cap);
     SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
-    SME_HIP(hipMemsetAsync(co.raw_nout, 0, rcap * sizeof(int32_t), st));
+    SME_HIP(hipMemsetAsync(max_nout, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(k_vocab, dim3(grid_for((int64_t)rcap, 256, 16384)), dim3(256), 0, st, tb, co, long_list,
                        cnt + 5, long_cap);
     SME_CHECK_LAUNCH();
@@ -1215,7 +1351,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     }
     if (nlong > 0) {
       int64_t *lens = W[W_T0].as<int64_t>(nlong + 1), *soff = W[W_T1].as<int64_t>(nlong + 1);
-      hipLaunchKernelGGL(k_long_lens, dim3(grid_for(nlong)), dim3(256), 0, st, long_list, nlong, tb.reps, lens);
+      hipLaunchKernelGGL(k_long_lens, dim3(grid_for(nlong)), dim3(256), 0, st, long_list, nlong, tb.slots, lens);
       SME_HIP(hipMemsetAsync(lens + nlong, 0, sizeof(int64_t), st));
       size_t tbb = 0;
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, lens, soff, (int)nlong + 1, st));
@@ -1231,6 +1367,9 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     SME_HIP(hipStreamSynchronize(st));
     if (hc[0] <= pool_cap && hc[1] <= cand_cap) {
       ncand = (int64_t)hc[1];
+      cx->vocab_cand_cap = cand_cap;
+      cx->vocab_pool_cap = pool_cap;
+      cx->vocab_long_cap = long_cap;
       break;
     }
     if (attempt > 3) throw Error(SME_ELIMIT, "vocabulary pool");
@@ -1249,16 +1388,17 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     hipLaunchKernelGGL(k_final_insert, dim3(grid_for(ncand)), dim3(256), 0, st, co.pool, co.cand_str, ncand, fkeys,
                        freps, fcap - 1, cand_final, ovf);
   uint32_t *vslot = W[W_VSLOT].as<uint32_t>(ncand + 1);
-  uint64_t *khi = W[W_KHI].as<uint64_t>(ncand + 1), *klo = W[W_KLO].as<uint64_t>(ncand + 1);
   uint32_t *vidx = W[W_VIDX].as<uint32_t>(ncand + 1);
+  int32_t *maxlen = reinterpret_cast<int32_t *>(cnt + 12);
   hipLaunchKernelGGL(k_final_compact, dim3(grid_for((int64_t)fcap)), dim3(256), 0, st, fkeys, freps, fcap - 1,
-                     co.cand_str, co.pool, cnt + 1, vslot, khi, klo, vidx);
+                     co.cand_str, cnt + 1, vslot, vidx, maxlen);
   SME_CHECK_LAUNCH();
-  unsigned long long hv[2];
+  unsigned long long hv[13];
   SME_HIP(hipMemcpyAsync(hv, cnt, sizeof hv, hipMemcpyDeviceToHost, st));
   SME_HIP(hipStreamSynchronize(st));
   if (d2h(ovf, st)) throw Error(SME_ELIMIT, "final term table overflow");
   const int64_t V = (int64_t)hv[1];
+  const int term_maxlen = (int)(int32_t)(uint32_t)hv[12];
 
   sme_index *ix = new sme_index();
   ix->ctx = cx;
@@ -1272,23 +1412,25 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   uint32_t *order = W[W_T2].as<uint32_t>(V + 1);
   int64_t *term_off = ix->d_term_off.as<int64_t>(V + 1);
   if (V > 0) {
-    uint64_t *khi2 = W[W_T0].as<uint64_t>(V), *klo2 = W[W_T1].as<uint64_t>(V);
-    uint32_t *vidx2 = W[W_RAWTERM].as<uint32_t>(V);  // temporary
+    // LSD radix sort of the vocabulary in String.compareTo order: 4 UTF-16 units per
+    // 64-bit key word, least significant word first, stable; terms are at most
+    // 99 units and all words below the longest term's length are sorted.
+    const int nwords = std::min(8, (std::max(term_maxlen, 1) + 3) / 4);
+    uint64_t *kw = W[W_KHI].as<uint64_t>(V), *kw2 = W[W_KLO].as<uint64_t>(V);
+    uint32_t *ord_a = vidx, *ord_b = order;
     size_t tbb = 0;
-    // LSD over the 128-bit prefix: lo then hi (stable)
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, klo, klo2, vidx, vidx2, (int)V, 0, 64, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, klo, klo2, vidx, vidx2, (int)V, 0, 64, st));
-    // permute hi by vidx2 then sort by hi
-    uint64_t *khi_p = W[W_MULTI].as<uint64_t>(V);
-    hipLaunchKernelGGL(k_gather_u64, dim3(grid_for(V)), dim3(256), 0, st, khi, vidx2, V, khi_p);
-    hipLaunchKernelGGL(k_gather_u64, dim3(grid_for(V)), dim3(256), 0, st, klo, vidx2, V, klo2);
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, khi_p, khi2, vidx2, order, (int)V, 0, 64, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, khi_p, khi2, vidx2, order, (int)V, 0, 64, st));
-    // sorted lo in final order: lo_s[i] = klo[order[i]]
-    uint64_t *klo_s = W[W_MULTI].as<uint64_t>(V);
-    hipLaunchKernelGGL(k_gather_u64, dim3(grid_for(V)), dim3(256), 0, st, klo, order, V, klo_s);
-    hipLaunchKernelGGL(k_final_fixup, dim3(grid_for(V)), dim3(256), 0, st, khi2, klo_s, order, V, vslot, freps,
-                       co.cand_str, co.pool);
+    for (int w = nwords - 1; w >= 0; w--) {
+      hipLaunchKernelGGL(k_term_word, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V, vslot, freps, co.cand_str,
+                         co.pool, w, kw);
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, kw, kw2, ord_a, ord_b, (int)V, 0, 64, st));
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, kw, kw2, ord_a, ord_b, (int)V, 0, 64, st));
+      std::swap(ord_a, ord_b);
+    }
+    if (ord_a != order)
+      SME_HIP(hipMemcpyAsync(order, ord_a, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    if (term_maxlen > 32)
+      hipLaunchKernelGGL(k_final_fixup, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, freps, co.cand_str,
+                         co.pool);
     int64_t *tlen = W[W_T0].as<int64_t>(V + 1);
     hipLaunchKernelGGL(k_final_rank, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, freps, co.cand_str,
                        rank_of_slot, tlen);
@@ -1319,10 +1461,6 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
                        rank_of_slot, co.raw_nout, raw_term, multi);
     SME_CHECK_LAUNCH();
   }
-  int32_t *max_nout = W[W_MAXNOUT].as<int32_t>(4);  // must survive the counter resets below
-  SME_HIP(hipMemsetAsync(max_nout, 0, sizeof(int32_t), st));
-  hipLaunchKernelGGL(k_max_nout, dim3(grid_for((int64_t)rcap, 256, 16384)), dim3(256), 0, st, co.raw_nout, tb.keys,
-                     rcap, max_nout);
   prof.mark("vocabulary");
 
   // ---------------- K5 aggregation ----------------

@@ -19,6 +19,7 @@ struct sme_ctx {
   // build workspace, reused across builds (see DevBuf)
   sme::DevBuf ws[64];  // 0..47 build, 48..63 query / serializer / tokenizer
   sme::DevBuf cub_tmp;
+  uint64_t vocab_cand_cap = 0, vocab_pool_cap = 0, vocab_long_cap = 0;  // learned across builds
   std::string profile_json;
   std::vector<std::pair<std::string, float>> last_profile;
 };

@@ -75,8 +75,9 @@ __device__ __forceinline__ bool g_valid_li(uint32_t c) {  // c d e g h k m n r t
   return c >= 99 && c <= 116 && ((0x28D37u >> (c - 99)) & 1u);
 }
 
-struct Stemmer {
-  uint16_t b[kStemCap];
+template <int CAP>
+struct StemmerT {
+  uint16_t b[CAP];
   int len;
   int c, lim, lb, bra, ket;
   int p1, p2;
@@ -562,5 +563,7 @@ struct Stemmer {
     postlude();
   }
 };
+
+using Stemmer = StemmerT<kStemCap>;
 
 }  // namespace sme
