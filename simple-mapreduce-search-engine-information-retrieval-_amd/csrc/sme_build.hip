@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <chrono>
@@ -134,23 +135,60 @@ struct ScanOut {
   unsigned long long *cnt;  // [3]
 };
 
-__device__ __forceinline__ void scan_lt(const uint8_t *__restrict__ t, int64_t n, int64_t p, const ScanOut &o) {
+// Candidates are collected per workgroup in LDS and flushed with ONE global
+// atomic per list per flush: a same-address global atomic per tag (one lane per
+// wave, ~6 tags per record) serialises at the memory side (~14 ns each).
+constexpr int kScanNT = 256;
+constexpr int kScanBuf = 1024;  // per list; one 4 KiB block step adds at most 4096 '<'
+
+struct ScanLds {
+  uint64_t buf[3][kScanBuf];
+  unsigned cnt[3];
+  unsigned long long base[3];
+};
+
+__device__ __forceinline__ void scan_push(ScanLds &L, const ScanOut &o, int list, uint64_t p) {
+  unsigned i = atomicAdd(&L.cnt[list], 1u);
+  if (i < (unsigned)kScanBuf) {
+    L.buf[list][i] = p;
+  } else {  // rare: more '<' in one step than the buffer holds
+    uint64_t *dst = list == 0 ? o.S : list == 1 ? o.E : o.C;
+    const uint32_t cap = list == 0 ? o.capS : list == 1 ? o.capE : o.capC;
+    unsigned long long g = atomicAdd(&o.cnt[list], 1ull);
+    if (g < cap) dst[g] = p;
+  }
+}
+
+__device__ __forceinline__ void scan_lt(const uint8_t *__restrict__ t, int64_t n, int64_t p, const ScanOut &o,
+                                        ScanLds &L) {
   if (p + 5 <= n && t[p + 1] == 'D' && t[p + 2] == 'O' && t[p + 3] == 'C' && t[p + 4] == '>') {
-    if (doc_tag_valid(t, p, "<DOC>", 5)) {
-      unsigned long long i = atomicAdd(&o.cnt[0], 1ull);
-      if (i < o.capS) o.S[i] = (uint64_t)p;
-    }
+    if (doc_tag_valid(t, p, "<DOC>", 5)) scan_push(L, o, 0, (uint64_t)p);
   } else if (p + 6 <= n && t[p + 1] == '/' && t[p + 2] == 'D' && t[p + 3] == 'O' && t[p + 4] == 'C' &&
              t[p + 5] == '>') {
-    if (doc_tag_valid(t, p, "</DOC>", 6)) {
-      unsigned long long i = atomicAdd(&o.cnt[1], 1ull);
-      if (i < o.capE) o.E[i] = (uint64_t)p;
-    }
+    if (doc_tag_valid(t, p, "</DOC>", 6)) scan_push(L, o, 1, (uint64_t)p);
   }
-  if (!lt_simple(t, n, p)) {
-    unsigned long long i = atomicAdd(&o.cnt[2], 1ull);
-    if (i < o.capC) o.C[i] = (uint64_t)p;
+  if (!lt_simple(t, n, p)) scan_push(L, o, 2, (uint64_t)p);
+}
+
+// flush the LDS lists (all threads of the block call this)
+__device__ void scan_flush(ScanLds &L, const ScanOut &o) {
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const unsigned c = min(L.cnt[threadIdx.x], (unsigned)kScanBuf);
+    L.base[threadIdx.x] = c ? atomicAdd(&o.cnt[threadIdx.x], (unsigned long long)c) : 0ull;
   }
+  __syncthreads();
+#pragma unroll
+  for (int list = 0; list < 3; list++) {
+    const unsigned c = min(L.cnt[list], (unsigned)kScanBuf);
+    uint64_t *dst = list == 0 ? o.S : list == 1 ? o.E : o.C;
+    const uint64_t cap = list == 0 ? o.capS : list == 1 ? o.capE : o.capC;
+    for (unsigned i = threadIdx.x; i < c; i += blockDim.x)
+      if (L.base[list] + i < cap) dst[L.base[list] + i] = L.buf[list][i];
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) L.cnt[threadIdx.x] = 0;
+  __syncthreads();
 }
 
 __device__ __forceinline__ uint32_t has_lt(uint32_t w) {  // bytes equal to '<' (0x3C)
@@ -160,25 +198,40 @@ __device__ __forceinline__ uint32_t has_lt(uint32_t w) {  // bytes equal to '<' 
 
 // One pass over the text with coalesced 16-byte loads: consecutive lanes read
 // consecutive 16-byte words; only words containing '<' are looked at bytewise.
-__global__ void k_scan_tags(const uint8_t *__restrict__ t, int64_t n, ScanOut o) {
+__global__ __launch_bounds__(kScanNT) void k_scan_tags(const uint8_t *__restrict__ t, int64_t n, ScanOut o) {
+  __shared__ ScanLds L;
+  if (threadIdx.x < 3) L.cnt[threadIdx.x] = 0;
+  __syncthreads();
   const uintptr_t mis = (uintptr_t)t & 15;
   const uint4 *a = reinterpret_cast<const uint4 *>(t - mis);
   const int64_t nv = (int64_t)((n + mis + 15) >> 4);
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
-    const uint4 q = a[v];
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  const int64_t stride = (int64_t)gridDim.x * kScanNT;
+  for (int64_t v0 = blockIdx.x * (int64_t)kScanNT; v0 < nv; v0 += stride) {
+    const int64_t v = v0 + threadIdx.x;
+    if (v < nv) {
+      const uint4 q = a[v];
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+      uint32_t lts = 0;  // '<' bytes of the 16-byte word; examined out of the unrolled loop
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (!has_lt(w[k])) continue;
+      for (int k = 0; k < 4; k++) {
+        if (!has_lt(w[k])) continue;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (((w[k] >> (8 * j)) & 0xFF) != '<') continue;
-        const int64_t p = 16 * v + 4 * k + j - (int64_t)mis;
+        for (int j = 0; j < 4; j++)
+          if (((w[k] >> (8 * j)) & 0xFF) == '<') lts |= 1u << (4 * k + j);
+      }
+      while (lts) {
+        const int b = __ffs(lts) - 1;
+        lts &= lts - 1;
+        const int64_t p = 16 * v + b - (int64_t)mis;
         if (p < 0 || p >= n) continue;
-        scan_lt(t, n, p, o);
+        scan_lt(t, n, p, o, L);
       }
     }
+    __syncthreads();
+    const bool full = L.cnt[0] >= kScanBuf / 2 || L.cnt[1] >= kScanBuf / 2 || L.cnt[2] >= kScanBuf / 2;
+    if (full) scan_flush(L, o);  // block-uniform condition (read after the barrier)
   }
+  scan_flush(L, o);
 }
 
 __device__ __forceinline__ int64_t lower_bound_u64(const uint64_t *a, int64_t n, uint64_t v) {
@@ -314,11 +367,15 @@ __global__ void k_docno(const uint8_t *t, const uint64_t *rs, const uint64_t *re
 }
 
 // mark records that contain a complex '<' (sorted complex list)
+constexpr int64_t kMinFastRec = 48;
+
 __global__ void k_mark_slow(const uint64_t *rs, const uint64_t *re, int64_t nR, const uint64_t *C, int64_t nC,
                             uint8_t *slow, unsigned long long *nslow) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nR; r += (int64_t)gridDim.x * blockDim.x) {
     int64_t i = lower_bound_u64(C, nC, rs[r]);
-    bool s = i < nC && C[i] < re[r];
+    // complex markup, or a record too short for the stream tokenizer's window
+    // (at most kChunk / kMinFastRec + 2 records overlap one chunk)
+    bool s = (i < nC && C[i] < re[r]) || re[r] - rs[r] < kMinFastRec;
     slow[r] = s;
     if (s) atomicAdd(nslow, 1ull);
   }
@@ -341,63 +398,113 @@ struct RawTable {
   uint64_t mask;
   const uint8_t *text;
   unsigned int *overflow;
-  unsigned long long *count;  // distinct raw tokens inserted
 };
 
+// Raw-token signature: w0/w1 = the first 16 bytes (little-endian, zero padded),
+// h = a word-wise mix of (len, w0, w1, further 8-byte words).  (w0, w1, len)
+// identify tokens of <= 16 bytes exactly; longer ones are compared byte-wise.
 struct TokSig {
   uint64_t h, w0, w1;
 };
-__device__ __forceinline__ void sig_add(TokSig &g, uint8_t b, int64_t i) {
-  g.h ^= b;
-  g.h *= 0x100000001b3ull;
-  if (i < 8)
-    g.w0 |= (uint64_t)b << (8 * i);
-  else if (i < 16)
-    g.w1 |= (uint64_t)b << (8 * (i - 8));
+__device__ __forceinline__ uint64_t sig_mix(uint64_t h, uint64_t w) { return fmix64(h ^ (w * 0x9E3779B97F4A7C15ull)); }
+__device__ __forceinline__ uint64_t sig_head(uint64_t len, uint64_t w0, uint64_t w1) {
+  return sig_mix(sig_mix(0xC2B2AE3D27D4EB4Full ^ len, w0), w1);
 }
-__device__ __forceinline__ void sig_end(TokSig &g, int64_t len) {
-  g.h = fmix64(g.h ^ (uint64_t)len);
-  g.h = g.h ? g.h : 1;
+__device__ __forceinline__ uint64_t sig_fin(uint64_t h) { return h ? h : 1; }
+__device__ __forceinline__ uint64_t load_word_bytes(const uint8_t *p, int64_t n) {  // n in [0, 8]
+  uint64_t w = 0;
+  for (int64_t i = 0; i < n; i++) w |= (uint64_t)p[i] << (8 * i);
+  return w;
 }
 __device__ __forceinline__ TokSig sig_bytes(const uint8_t *p, int64_t len) {
-  TokSig g{0xcbf29ce484222325ull, 0, 0};
-  for (int64_t i = 0; i < len; i++) sig_add(g, p[i], i);
-  sig_end(g, len);
+  TokSig g;
+  g.w0 = load_word_bytes(p, len < 8 ? len : 8);
+  g.w1 = len > 8 ? load_word_bytes(p + 8, len < 16 ? len - 8 : 8) : 0;
+  uint64_t h = sig_head((uint64_t)len, g.w0, g.w1);
+  for (int64_t o = 16; o < len; o += 8) h = sig_mix(h, load_word_bytes(p + o, len - o < 8 ? len - o : 8));
+  g.h = sig_fin(h);
   return g;
 }
 
-__device__ uint32_t raw_insert(const RawTable &tb, const TokSig &g, uint64_t off, uint64_t len) {
+constexpr uint64_t kMaxProbe = 4096;  // longer runs mean the table is too full: retry with 4x slots
+
+// Slot words are read with agent-scope relaxed loads (global_load ... sc1): a
+// plain load may hit a line this XCD's L2 cached before another XCD filled the
+// slot, and would then see a stale 0 on every later lookup of that token.
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The four words of a slot, as independent loads (one round trip).  Slots are
+// written once, so a plain (L2-cacheable) read is either current or shows the
+// slot (partly) empty; only then are the words re-read agent-coherently.
+struct SlotVal {
+  unsigned long long key, rep, w0, w1;
+};
+__device__ __forceinline__ SlotVal ld_slot(const RawSlot *s) {
+  SlotVal v;
+  v.key = ld_agent(&s->key);
+  v.rep = ld_agent(&s->rep);
+  v.w0 = ld_agent(&s->w0);
+  v.w1 = ld_agent(&s->w1);
+  return v;
+}
+__device__ __forceinline__ SlotVal ld_slot_plain(const RawSlot *s) {
+  SlotVal v;
+  v.key = s->key;
+  v.rep = s->rep;
+  v.w0 = s->w0;
+  v.w1 = s->w1;
+  return v;
+}
+
+// Find-or-insert the raw token (signature g, text[off, off+len)); v holds the
+// plainly loaded words of its home slot (g.h & mask).  Returns the slot index.
+__device__ __noinline__ uint32_t raw_insert(const RawTable &tb, const TokSig &g, uint64_t off, uint64_t len, SlotVal v) {
   if (len >= (1ull << 24)) {
     atomicOr(tb.overflow, 2u);
     return 0xFFFFFFFFu;
   }
   const uint64_t rep_me = (off << 24) | len;
   uint64_t slot = g.h & tb.mask;
-  for (uint64_t probe = 0; probe <= tb.mask; probe++) {
+  const uint64_t max_probe = tb.mask < kMaxProbe ? tb.mask : kMaxProbe;
+  for (uint64_t probe = 0; probe <= max_probe; probe++) {
     RawSlot *s = &tb.slots[slot];
-    unsigned long long k = s->key;
+    if (probe > 0) v = ld_slot_plain(s);
+    if (v.key == 0 || (v.key == g.h && v.rep == 0)) v = ld_slot(s);  // maybe stale: re-read coherently
+    unsigned long long k = v.key;
     if (k == 0) {
       unsigned long long old = atomicCAS(&s->key, 0ull, (unsigned long long)g.h);
       if (old == 0) {
+        // w0/w1 must be performed before rep (readers trust w0/w1 once rep != 0).
+        // The atomics execute at the memory side; waiting for their completion
+        // orders them without __threadfence(), whose agent-scope release is an
+        // L2 writeback + invalidate (buffer_wbl2 / buffer_inv sc1) per insert.
         atomicExch(&s->w0, (unsigned long long)g.w0);
         atomicExch(&s->w1, (unsigned long long)g.w1);
-        __threadfence();
+        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
         atomicExch(&s->rep, (unsigned long long)rep_me);
-        atomicAdd(tb.count, 1ull);
         return (uint32_t)slot;
       }
       k = old;
+      v.rep = 0;  // written after key: reload below
     }
     if (k == g.h) {
-      unsigned long long r = s->rep;
-      for (int spin = 0; r == 0 && spin < (1 << 22); spin++) r = atomicOr(&s->rep, 0ull);
-      if (r == 0) {
-        atomicOr(tb.overflow, 4u);
-        return 0xFFFFFFFFu;
+      unsigned long long r = v.rep;
+      if (r == 0) {  // slot being filled by another lane: wait for rep (written last, after w0/w1)
+        for (int spin = 0; r == 0 && spin < (1 << 22); spin++) r = ld_agent(&s->rep);
+        if (r == 0) {
+          atomicOr(tb.overflow, 4u);
+          return 0xFFFFFFFFu;
+        }
+        v.w0 = ld_agent(&s->w0);
+        v.w1 = ld_agent(&s->w1);
       }
       if ((r & 0xFFFFFFull) == len) {
-        bool eq = s->w0 == g.w0 && s->w1 == g.w1;
-        if (!eq) eq = atomicOr(&s->w0, 0ull) == g.w0 && atomicOr(&s->w1, 0ull) == g.w1;
+        bool eq = v.w0 == g.w0 && v.w1 == g.w1;
+        if (!eq) {  // w0/w1 may have been read before rep: re-read them after it
+          eq = ld_agent(&s->w0) == g.w0 && ld_agent(&s->w1) == g.w1;
+        }
         if (eq && len > 16) {
           const uint64_t ro = r >> 24;
           for (uint64_t i = 16; i < len && eq; i++) eq = tb.text[ro + i] == tb.text[off + i];
@@ -410,14 +517,34 @@ __device__ uint32_t raw_insert(const RawTable &tb, const TokSig &g, uint64_t off
   atomicOr(tb.overflow, 1u);
   return 0xFFFFFFFFu;
 }
+__device__ __forceinline__ uint32_t raw_insert(const RawTable &tb, const TokSig &g, uint64_t off, uint64_t len) {
+  return raw_insert(tb, g, off, len, ld_slot_plain(&tb.slots[g.h & tb.mask]));
+}
 
 // ============================================================================
 // K3: tokenization (raw tokens -> raw-vocab slots)
 // ============================================================================
+// Byte-parallel TagTokenizer for records whose markup is simple: a raw token is
+// a maximal run of non-split bytes whose first byte lies outside every tag /
+// comment / PI / entity span (spans begin and end on split characters, so a run
+// is either wholly inside a span or wholly outside).
+//
+// A workgroup owns a contiguous range of records and walks their bytes as ONE
+// stream of 4 KiB chunks (records are ~4 KiB: a chunk-per-record walk would
+// leave most of every second chunk idle).  Per chunk: coalesced 16-byte loads
+// into LDS (+1 KiB lookahead), the overlapping records' spans into LDS, per-lane
+// split classes over 16 bytes, span coverage by a block max-scan, token ranks by
+// a block sum-scan.  Each kept token is then read as 8-byte LDS words (no
+// byte-serial loop), its signature is mixed word-wise, and its raw-vocabulary
+// slot is found with the home slot's load issued for two tokens at once.
+// Token i of record r goes to tokstream[(rs[r] >> 1) + i]; ntok[r] is written by
+// the lane holding r's last byte.
 constexpr int kTokNT = 256;
-constexpr int kTokBytes = 16;
-constexpr int kChunk = kTokNT * kTokBytes;  // 4 KiB of text per block iteration
-constexpr int kStageV = kTokNT + 64;         // staged 16-byte words: chunk + 1 KiB lookahead
+constexpr int kTokWords = 4;                      // 16-byte words per lane
+constexpr int kTokBytes = 16 * kTokWords;         // 64 bytes per lane
+constexpr int kChunk = kTokNT * kTokBytes;        // 16 KiB of text per block step
+constexpr int kStageV = kTokNT * kTokWords + 64;  // staged 16-byte words: chunk + 1 KiB lookahead
+constexpr int kRecWin = 384;  // records overlapping one chunk: fast-path records are >= kMinFastRec bytes
 
 // entity span end: '&' [a-z0-9#]* ';'  (TagTokenizer.onAmpersand 644-662); p if none
 template <typename B>
@@ -449,96 +576,234 @@ __device__ __forceinline__ int64_t lt_span_end_f(B &&byte, int64_t n, int64_t p)
   return n;
 }
 
-// Byte-parallel TagTokenizer for records whose markup is simple: a raw token is
-// a maximal run of non-split bytes whose first byte lies outside every tag /
-// comment / PI / entity span (spans begin and end on split characters, so a run
-// is either wholly inside a span or wholly outside).  The block walks the record
-// in 4 KiB chunks: coalesced 16-byte loads into LDS, per-lane split classes over
-// 16 bytes, span coverage by a block max-scan, token order by a block sum-scan.
-__global__ __launch_bounds__(kTokNT) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n, const uint64_t *rs,
-                                                     const uint64_t *re, int64_t nR, const uint8_t *slow,
-                                                     uint32_t *tokstream, int32_t *ntok, RawTable tb) {
-  __shared__ uint4 st4[kStageV];
-  __shared__ int64_t sc64[kTokNT / 64 + 1];
-  __shared__ int32_t sc32[kTokNT / 64 + 1];
+// Chunk-relative positions: position c_lo + p of the text is stage byte p
+// (the stage starts at the chunk's first aligned word), so the per-lane state
+// is 32-bit.  Record bounds in the window are clamped to [-1, kFar].
+constexpr int32_t kFar = 1 << 30;
+
+struct TokLds {
+  uint4 st4[kStageV];
+  int32_t rs[kRecWin], re[kRecWin];  // chunk-relative, clamped
+  int64_t tbase[kRecWin];            // tokstream offset of the record (rs >> 1)
+  int32_t c0[kRecWin];
+  int32_t rid[kRecWin];               // record index
+  int32_t sc32[kTokNT / 64 + 1];
+};
+
+// byte at chunk-relative position p (stage, or global beyond the lookahead)
+__device__ __forceinline__ uint8_t tok_byte(const uint8_t *stg, const uint8_t *t, int64_t c_lo, int32_t p) {
+  return (p >= 0 && p < kStageV * 16) ? stg[p] : t[c_lo + p];
+}
+__device__ __noinline__ int32_t lt_span_rel(const uint8_t *stg, const uint8_t *t, int64_t c_lo, int32_t e, int32_t p) {
+  if (p + 1 >= e) return e;
+  const uint8_t c = tok_byte(stg, t, c_lo, p + 1);
+  if (c == '!' && p + 3 < e && tok_byte(stg, t, c_lo, p + 2) == '-' && tok_byte(stg, t, c_lo, p + 3) == '-') {
+    for (int32_t i = p + 1; i + 2 < e; i++)
+      if (tok_byte(stg, t, c_lo, i) == '-' && tok_byte(stg, t, c_lo, i + 1) == '-' && tok_byte(stg, t, c_lo, i + 2) == '>')
+        return i + 2;
+    return e;
+  }
+  if (c == '?') {
+    for (int32_t i = p + 1; i + 1 < e; i++)
+      if (tok_byte(stg, t, c_lo, i) == '?' && tok_byte(stg, t, c_lo, i + 1) == '>') return i + 1;
+    return e;
+  }
+  for (int32_t i = p + (c == '/' ? 2 : 1); i < e; i++)
+    if (tok_byte(stg, t, c_lo, i) == '>') return i;
+  return e;
+}
+__device__ __noinline__ int32_t amp_span_rel(const uint8_t *stg, const uint8_t *t, int64_t c_lo, int32_t e, int32_t p) {
+  for (int32_t i = p + 1; i < e; i++) {
+    const uint8_t d = tok_byte(stg, t, c_lo, i);
+    if ((d >= 'a' && d <= 'z') || (d >= '0' && d <= '9') || d == '#') continue;
+    return d == ';' ? i : p;
+  }
+  return p;
+}
+
+// first split byte at or after byte k of the 16-byte window (lo, hi); 16 if none
+__device__ __forceinline__ int first_split16(uint64_t lo, uint64_t hi, int k) {
+  for (int i = k; i < 16; i++) {
+    const uint8_t b = (uint8_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 0xFF);
+    if (is_split_byte(b)) return i;
+  }
+  return 16;
+}
+
+// signature of the token starting at chunk-relative x (its first byte is a word
+// char); e bounds it (the record end).  Long tokens continue byte-wise.
+__device__ __noinline__ TokSig tok_sig_long(const uint8_t *stg, const uint8_t *t, int64_t c_lo, int32_t x, int32_t e,
+                                            int32_t *len_o) {
+  int32_t y = x;
+  while (y < e && !is_split_byte(tok_byte(stg, t, c_lo, y))) y++;
+  *len_o = y - x;
+  return sig_bytes(t + c_lo + x, y - x);
+}
+
+__global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n,
+                                                     const uint64_t *__restrict__ rs_g,
+                                                     const uint64_t *__restrict__ re_g,
+                                                     const int32_t *__restrict__ frec, int64_t nF, int64_t rpb,
+                                                     uint32_t *__restrict__ tokstream, int32_t *__restrict__ ntok,
+                                                     RawTable tb) {
+  __shared__ TokLds L;
+  __shared__ int32_t s_adv;
+  const int64_t f0 = blockIdx.x * rpb;
+  if (f0 >= nF) return;
+  const int64_t f1 = min(nF, f0 + rpb);
   const int64_t mis = (int64_t)((uintptr_t)t & 15);
   const uint4 *a4 = reinterpret_cast<const uint4 *>(t - mis);
-  const int64_t nq = n + mis;  // aligned address space: position p lives at q = p + mis
-  const uint8_t *stg = reinterpret_cast<const uint8_t *>(st4);
+  const int64_t nq = n + mis;
+  const uint8_t *stg = reinterpret_cast<const uint8_t *>(L.st4);
+  const uint64_t *st8 = reinterpret_cast<const uint64_t *>(L.st4);
   const int tid = threadIdx.x;
-  for (int64_t r = blockIdx.x; r < nR; r += gridDim.x) {
-    if (slow[r]) continue;
-    const int64_t s = (int64_t)rs[r], e = (int64_t)re[r];
-    uint32_t *out = tokstream + (s >> 1);
-    int64_t mask_carry = -1;  // furthest span end of markup that started in earlier chunks
-    int32_t tok_carry = 0;
-    uint8_t last_prev = ' ';  // byte before the chunk (record start counts as a split)
-    for (int64_t Q = (s + mis) & ~(int64_t)15; Q < e + mis; Q += kChunk) {
-      for (int i = tid; i < kStageV; i += kTokNT) {
-        const int64_t q = Q + 16 * (int64_t)i;
-        st4[i] = q < nq ? a4[q >> 4] : make_uint4(0, 0, 0, 0);
+  const int64_t end_all = (int64_t)re_g[frec[f1 - 1]];
+  int64_t fcur = f0;        // first fast record not wholly before the current chunk
+  int64_t mask_carry = -1;  // absolute end of the furthest span begun in earlier chunks
+  int32_t tok_carry = 0;    // tokens of the record continuing from the previous chunk
+  int64_t Q = ((int64_t)rs_g[frec[f0]] + mis) & ~(int64_t)15;
+  uint8_t prev_chunk_byte = Q - mis > 0 ? t[Q - mis - 1] : (uint8_t)' ';
+  for (; Q < end_all + mis; Q += kChunk) {
+    const int64_t c_lo = Q - mis;  // chunk = positions c_lo + [0, kChunk)
+    for (int i = tid; i < kRecWin; i += kTokNT) {
+      const int64_t f = fcur + i;
+      const int32_t r = f < f1 ? frec[f] : -1;
+      const int64_t a = r >= 0 ? (int64_t)rs_g[r] : INT64_MAX;
+      const bool ok = a < c_lo + kChunk;
+      const int64_t b = ok ? (int64_t)re_g[r] : INT64_MAX;
+      L.rs[i] = ok ? (int32_t)max<int64_t>(a - c_lo, -1) : kFar;
+      L.re[i] = ok ? (int32_t)min<int64_t>(b - c_lo, kFar) : kFar;
+      L.tbase[i] = ok ? (a >> 1) : 0;
+      L.rid[i] = ok ? r : -1;
+      L.c0[i] = 0;
+    }
+    for (int i = tid; i < kStageV; i += kTokNT) {
+      const int64_t q = Q + 16 * (int64_t)i;
+      L.st4[i] = q < nq ? a4[q >> 4] : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    const int32_t p0 = kTokBytes * tid;
+    int j;  // window record holding p0 (or -1)
+    {
+      int lo = 0, hi = kRecWin;
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (L.rs[m] <= p0)
+          lo = m + 1;
+        else
+          hi = m;
       }
-      __syncthreads();
-      auto byte_at = [&](int64_t p) -> uint8_t {
-        const int64_t o = p + mis - Q;
-        return (o >= 0 && o < kStageV * 16) ? stg[o] : t[p];
-      };
-      const int64_t p0 = Q + 16 * (int64_t)tid - mis;
-      // pass 1: token-start candidates and spans over this lane's 16 bytes
-      uint32_t cand = 0;
-      int64_t lane_max = -1;
-      uint8_t prev = tid == 0 ? last_prev : stg[16 * tid - 1];
-      if (p0 - 1 < s) prev = ' ';
-      const uint4 v = st4[tid];
-      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int i = 0; i < kTokBytes; i++) {
-        const int64_t p = p0 + i;
-        const uint8_t b = (uint8_t)(wv[i >> 2] >> (8 * (i & 3)));
-        if (p >= s && p < e) {
-          const bool sp = is_split_byte(b);
-          if (!sp && is_split_byte(prev) && lane_max < p) cand |= 1u << i;
+      j = lo - 1;
+    }
+    const int32_t mc = (int32_t)max<int64_t>(min<int64_t>(mask_carry - c_lo, kFar), -1);
+    // pass 1: token-start candidates and spans over this lane's 64 bytes
+    uint64_t cand = 0;
+    int32_t lane_max = -1;
+    uint8_t prev = tid > 0 ? stg[p0 - 1] : prev_chunk_byte;
+    int jj = j;
+    int32_t rs_next = jj + 1 < kRecWin ? L.rs[jj + 1] : kFar;
+    int32_t re_cur = jj >= 0 ? L.re[jj] : -1;
+    for (int w = 0; w < kTokWords; w++) {
+      const uint64_t wlo = st8[2 * (kTokWords * tid + w)], whi = st8[2 * (kTokWords * tid + w) + 1];
+#pragma unroll 4
+      for (int i = 0; i < 16; i++) {
+        const int32_t p = p0 + 16 * w + i;
+        const uint8_t b = (uint8_t)((i < 8 ? wlo >> (8 * i) : whi >> (8 * (i - 8))) & 0xFF);
+        while (rs_next <= p) {
+          jj++;
+          re_cur = L.re[jj];
+          rs_next = jj + 1 < kRecWin ? L.rs[jj + 1] : kFar;
+        }
+        if (p < re_cur) {
+          if (!is_split_byte(b) && is_split_byte(prev) && lane_max < p) cand |= 1ull << (16 * w + i);
           if (b == '<') {
-            int64_t q = lt_span_end_f(byte_at, e, p);
+            const int32_t q = lt_span_rel(stg, t, c_lo, re_cur, p);
             lane_max = q > lane_max ? q : lane_max;
           } else if (b == '&') {
-            int64_t q = amp_span_end_f(byte_at, e, p);
+            const int32_t q = amp_span_rel(stg, t, c_lo, re_cur, p);
             lane_max = q > lane_max ? q : lane_max;
           }
         }
-        prev = p < s ? (uint8_t)' ' : b;
+        prev = b;
       }
-      int64_t blk_max;
-      int64_t before = block_excl_max<kTokNT, int64_t>(lane_max, (int64_t)-1, sc64, &blk_max);
-      before = before > mask_carry ? before : mask_carry;
-      uint32_t keep = 0;
-#pragma unroll
-      for (int i = 0; i < kTokBytes; i++)
-        if (((cand >> i) & 1u) && p0 + i > before) keep |= 1u << i;
-      int32_t blk_cnt;
-      int32_t idx = block_excl_sum<kTokNT, int32_t>(__popc(keep), sc32, &blk_cnt) + tok_carry;
-      // pass 2: hash each kept token [x, first split byte) and insert it
-      while (keep) {
-        const int i = __ffs(keep) - 1;
-        keep &= keep - 1;
-        const int64_t x = p0 + i;
-        int64_t y = x;
-        TokSig g{0xcbf29ce484222325ull, 0, 0};
-        while (y < e) {
-          const uint8_t b = byte_at(y);
-          if (is_split_byte(b)) break;
-          sig_add(g, b, y - x);
-          y++;
-        }
-        sig_end(g, y - x);
-        out[idx++] = raw_insert(tb, g, (uint64_t)x, (uint64_t)(y - x));
-      }
-      mask_carry = blk_max > mask_carry ? blk_max : mask_carry;
-      tok_carry += blk_cnt;
-      last_prev = stg[kChunk - 1];
-      __syncthreads();  // stage is overwritten by the next chunk
     }
-    if (tid == 0) ntok[r] = tok_carry;
+    int32_t blk_max;
+    int32_t before = block_excl_max<kTokNT, int32_t>(lane_max, -1, L.sc32, &blk_max);
+    before = before > mc ? before : mc;
+    // candidates at or below `before` lie inside a span begun in an earlier lane
+    const int32_t cut = before - p0 + 1;  // bits [0, cut) are covered
+    const uint64_t keep_all =
+        cut <= 0 ? cand : (cut >= kTokBytes ? 0ull : cand & ~((1ull << cut) - 1ull));
+    int32_t blk_cnt;
+    const int32_t base = block_excl_sum<kTokNT, int32_t>(__popcll(keep_all), L.sc32, &blk_cnt);
+    // c0: chunk rank of the first token of every record that starts in this lane
+    for (int k = (j < 0 ? 0 : j); k < kRecWin && L.rs[k] < p0 + kTokBytes; k++)
+      if (L.rs[k] >= p0) L.c0[k] = base + __popcll(keep_all & ((1ull << (L.rs[k] - p0)) - 1ull));
+    __syncthreads();
+    const int32_t carry0 = L.rs[0] < 0 ? tok_carry : 0;  // window record 0 began in an earlier chunk
+    // pass 2: signature + raw-vocabulary slot of every kept token
+    uint64_t keep = keep_all;
+    int32_t idx = base;
+    int jt = j < 0 ? 0 : j;
+    while (keep) {
+      const int i0 = __ffsll((unsigned long long)keep) - 1;
+      keep &= keep - 1;
+      const int32_t x = p0 + i0;
+      while (jt + 1 < kRecWin && L.rs[jt + 1] <= x) jt++;
+      const int32_t e = L.re[jt];
+      TokSig g;
+      int32_t len;
+      if (x + 24 <= kStageV * 16) {
+        const int a = x >> 3, sh = (x & 7) * 8;
+        const uint64_t u0 = st8[a], u1 = st8[a + 1], u2 = st8[a + 2];
+        const uint64_t lo = sh ? (u0 >> sh) | (u1 << (64 - sh)) : u0;
+        const uint64_t hi = sh ? (u1 >> sh) | (u2 << (64 - sh)) : u1;
+        len = first_split16(lo, hi, 1);
+        if (len > e - x) len = e - x;
+        if (len < 16) {
+          g.w0 = len >= 8 ? lo : (lo & ((1ull << (8 * len)) - 1));
+          g.w1 = len <= 8 ? 0 : (hi & ((1ull << (8 * (len - 8))) - 1));
+          g.h = sig_fin(sig_head((uint64_t)len, g.w0, g.w1));
+        } else {
+          g = tok_sig_long(stg, t, c_lo, x, e, &len);
+        }
+      } else {
+        g = tok_sig_long(stg, t, c_lo, x, e, &len);
+      }
+      const SlotVal v = ld_slot_plain(&tb.slots[g.h & tb.mask]);
+      // a hit at the home slot (the common case) is decided inline
+      const bool hit = len <= 16 && v.key == g.h && v.rep != 0 && (v.rep & 0xFFFFFFull) == (uint64_t)len &&
+                       v.w0 == g.w0 && v.w1 == g.w1;
+      const uint32_t slot = hit ? (uint32_t)(g.h & tb.mask) : raw_insert(tb, g, (uint64_t)(c_lo + x), (uint64_t)len, v);
+      const int32_t r0k = jt == 0 ? L.c0[0] - carry0 : L.c0[jt];
+      tokstream[L.tbase[jt] + (idx - r0k)] = slot;
+      idx++;
+    }
+    // ntok of every record whose last byte is in this lane (no token starts at its '>')
+    for (int k = (j < 0 ? 0 : j); k < kRecWin && L.rs[k] < p0 + kTokBytes; k++) {
+      const int32_t last = L.re[k] - 1;
+      if (last >= p0 && last < p0 + kTokBytes) {
+        const int32_t r0k = k == 0 ? L.c0[0] - carry0 : L.c0[k];
+        ntok[L.rid[k]] = base + __popcll(keep_all & ((1ull << (last - p0)) - 1ull)) - r0k;
+      }
+    }
+    // next chunk: records wholly before it are dropped from the window; the one
+    // running into it carries its token count
+    if (tid == 0) {
+      int adv = 0, kl = -1;
+      for (int k = 0; k < kRecWin && L.rs[k] < kChunk; k++) {
+        kl = k;
+        if (L.re[k] <= kChunk) adv = k + 1;
+      }
+      s_adv = adv;
+      L.sc32[0] = (kl >= 0 && L.re[kl] > kChunk) ? blk_cnt - (kl == 0 ? L.c0[0] - carry0 : L.c0[kl]) : 0;
+    }
+    if (blk_max >= 0) mask_carry = max<int64_t>(mask_carry, c_lo + blk_max);
+    prev_chunk_byte = stg[kChunk - 1];
+    __syncthreads();
+    fcur += s_adv;
+    tok_carry = L.sc32[0];
+    __syncthreads();  // LDS is overwritten by the next chunk
   }
 }
 
@@ -580,81 +845,123 @@ __global__ void k_tok_slow(const uint8_t *__restrict__ t, const uint64_t *rs, co
 // ============================================================================
 // K4: vocabulary
 // ============================================================================
+// The distinct raw tokens are first compacted into rlist (ascending slot order),
+// so one lane per listed token does real work (a sweep over the hash slots left
+// most lanes of a wave idle).  Every output of raw token i lives in its own pool
+// region [poff[i], poff[i] + len_bytes) -- outputs never exceed the raw token's
+// UTF-8 length (stems only shrink; acronym pieces are disjoint substrings; the
+// one lowercase expansion, U+0130, is 2 units for 2 bytes) -- so no shared
+// allocation counter is touched.  Output 0 is candidate i; further outputs
+// (acronym splits, rare) and, for those tokens, a copy of output 0 go to an
+// overflow list keyed (slot << 32 | ordinal).
+constexpr uint64_t kNoCand = ~0ull;
+
 struct CandOut {
   uint16_t *pool;
-  unsigned long long *pool_used;
-  uint64_t pool_cap;
-  uint64_t *cand_key;   // (raw slot << 32) | ordinal
-  uint64_t *cand_str;   // (pool offset << 16) | len
-  unsigned long long *ncand;
-  uint64_t cand_cap;
+  const int64_t *poff;  // per list index, units
+  uint64_t *cand_str;   // (pool offset << 16) | len, [0, nraw) primary, [nraw, nraw + ovf_cap) overflow
+  int64_t nraw;
+  uint64_t *ovf_key;    // (raw slot << 32) | ordinal
+  unsigned long long *novf;
+  uint64_t ovf_cap;
   int32_t *raw_nout;
   int32_t *max_nout;
+  unsigned int *err;  // bit 1: an output overran its token's pool region (cannot happen; checked)
 };
 
-__device__ void emit_final(const CandOut &co, uint32_t slot, uint32_t ordinal, const uint16_t *w, int l) {
-  unsigned long long po = atomicAdd(co.pool_used, (unsigned long long)l);
-  unsigned long long ci = atomicAdd(co.ncand, 1ull);
-  if (po + l <= co.pool_cap) {
-    for (int i = 0; i < l; i++) co.pool[po + i] = w[i];
-  }
-  if (ci < co.cand_cap) {
-    co.cand_key[ci] = ((uint64_t)slot << 32) | ordinal;
-    co.cand_str[ci] = ((uint64_t)po << 16) | (uint64_t)l;
+__device__ __forceinline__ void ovf_push(const CandOut &co, uint32_t slot, uint32_t ord, uint64_t cs) {
+  unsigned long long j = atomicAdd(co.novf, 1ull);
+  if (j < co.ovf_cap) {
+    co.ovf_key[j] = ((uint64_t)slot << 32) | ord;
+    co.cand_str[co.nraw + j] = cs;
   }
 }
 
-// normalize + stop + stem one decoded raw token (units), emitting finals
-__device__ void vocab_one(const CandOut &co, uint32_t slot, const uint16_t *units, int nu, uint16_t *work,
-                          int work_cap) {
+__device__ __forceinline__ void vocab_finish(const CandOut &co, int64_t i, uint32_t slot, uint32_t nout) {
+  co.raw_nout[slot] = (int32_t)nout;
+  if (nout == 0) co.cand_str[i] = kNoCand;
+  if (nout > 1) {
+    ovf_push(co, slot, 0, co.cand_str[i]);
+    atomicMax(co.max_nout, (int32_t)nout);
+  }
+}
+
+// normalize + stop + stem one decoded raw token (units) of list index i
+__device__ void vocab_one(const CandOut &co, int64_t i, uint32_t slot, const uint16_t *units, int nu,
+                          uint16_t *work, int work_cap) {
   uint32_t ord = 0;
+  uint64_t used = 0;
   Stemmer st;
   normalize_raw(units, nu, work, work_cap, [&](const uint16_t *p, int l) {
     if (is_stopword(p, l)) return;
-    for (int i = 0; i < l; i++) st.b[i] = p[i];
+    for (int k = 0; k < l; k++) st.b[k] = p[k];
     st.len = l;
     st.run();
-    emit_final(co, slot, ord, st.b, st.len);
+    const uint64_t po = (uint64_t)co.poff[i] + used;
+    if (po + (uint64_t)st.len > (uint64_t)co.poff[i + 1]) {
+      atomicOr(co.err, 1u);
+      return;
+    }
+    for (int k = 0; k < st.len; k++) co.pool[po + k] = st.b[k];
+    used += (uint64_t)st.len;
+    const uint64_t cs = (po << 16) | (uint64_t)st.len;
+    if (ord == 0)
+      co.cand_str[i] = cs;
+    else
+      ovf_push(co, slot, ord, cs);
     ord++;
   });
-  co.raw_nout[slot] = (int32_t)ord;
-  if (ord > 1) atomicMax(co.max_nout, (int32_t)ord);
+  vocab_finish(co, i, slot, ord);
 }
 
 // Fast path for the common raw token: only [a-z0-9] (checkTokenStatus == Clean), so
 // normalization is the identity and the token goes straight to stop list + stemmer.
-__device__ bool vocab_clean(const CandOut &co, uint32_t slot, const uint8_t *p, uint64_t len) {
+__device__ bool vocab_clean(const CandOut &co, int64_t i, uint32_t slot, const uint8_t *p, uint64_t len) {
   if (len > 48) return false;
   StemmerT<64> st;
-  for (uint64_t i = 0; i < len; i++) {
-    uint8_t c = p[i];
+  for (uint64_t k = 0; k < len; k++) {
+    uint8_t c = p[k];
     if (!((c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'))) return false;
-    st.b[i] = c;
+    st.b[k] = c;
   }
   uint32_t ord = 0;
-  if (!(len > 100 / 6 && len >= 100) && !is_stopword(st.b, (int)len)) {
+  if (!is_stopword(st.b, (int)len)) {  // <= 48 ASCII bytes: addToken's >= 100-byte rule cannot apply
     st.len = (int)len;
     st.run();
-    emit_final(co, slot, 0, st.b, st.len);
+    const uint64_t po = (uint64_t)co.poff[i];
+    for (int k = 0; k < st.len; k++) co.pool[po + k] = st.b[k];
+    co.cand_str[i] = (po << 16) | (uint64_t)st.len;
     ord = 1;
   }
-  co.raw_nout[slot] = (int32_t)ord;
+  vocab_finish(co, i, slot, ord);
   return true;
 }
 
 constexpr int kShortRaw = 200;
 
-__global__ void k_vocab(const RawTable tb, CandOut co, int64_t *long_list, unsigned long long *nlong,
-                        uint64_t long_cap) {
-  for (uint64_t slot = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; slot <= tb.mask;
-       slot += (uint64_t)gridDim.x * blockDim.x) {
-    if (tb.slots[slot].key == 0) continue;
+__global__ void k_not_flags(const uint8_t *a, int64_t n, uint8_t *f) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    f[i] = !a[i];
+}
+__global__ void k_raw_flags(const RawSlot *slots, uint64_t n, uint8_t *flag) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < n; s += (uint64_t)gridDim.x * blockDim.x)
+    flag[s] = slots[s].key != 0;
+}
+__global__ void k_raw_lens(const RawSlot *slots, const int32_t *rlist, int64_t nraw, int64_t *lens) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= nraw; i += (int64_t)gridDim.x * blockDim.x)
+    lens[i] = i < nraw ? (int64_t)(slots[rlist[i]].rep & 0xFFFFFFull) : 0;
+}
+
+__global__ void k_vocab(const RawTable tb, const int32_t *rlist, int64_t nraw, CandOut co, int64_t *long_list,
+                        unsigned long long *nlong, uint64_t long_cap) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nraw; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t slot = (uint32_t)rlist[i];
     uint64_t r = tb.slots[slot].rep;
     uint64_t off = r >> 24, len = r & 0xFFFFFFull;
-    if (vocab_clean(co, (uint32_t)slot, tb.text + off, len)) continue;
+    if (vocab_clean(co, i, slot, tb.text + off, len)) continue;
     if (len > kShortRaw) {
-      unsigned long long i = atomicAdd(nlong, 1ull);
-      if (i < long_cap) long_list[i] = (int64_t)slot;
+      unsigned long long j = atomicAdd(nlong, 1ull);
+      if (j < long_cap) long_list[j] = i;
       continue;
     }
     uint16_t units[kShortRaw + 2];
@@ -667,17 +974,18 @@ __global__ void k_vocab(const RawTable tb, CandOut co, int64_t *long_list, unsig
       for (int x = 0; x < k; x++) units[nu++] = tmp[x];
       p += used;
     }
-    vocab_one(co, (uint32_t)slot, units, nu, work, 4 * kShortRaw + 16);
+    vocab_one(co, i, slot, units, nu, work, 4 * kShortRaw + 16);
   }
 }
 
-__global__ void k_vocab_long(const RawTable tb, CandOut co, const int64_t *long_list, int64_t nlong,
-                             const int64_t *scr_off, uint16_t *scr) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nlong; i += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t slot = (uint64_t)long_list[i];
+__global__ void k_vocab_long(const RawTable tb, const int32_t *rlist, CandOut co, const int64_t *long_list,
+                             int64_t nlong, const int64_t *scr_off, uint16_t *scr) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < nlong; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = long_list[j];
+    const uint32_t slot = (uint32_t)rlist[i];
     uint64_t r = tb.slots[slot].rep;
     uint64_t off = r >> 24, len = r & 0xFFFFFFull;
-    uint16_t *units = scr + scr_off[i];
+    uint16_t *units = scr + scr_off[j];
     int nu = 0;
     for (uint64_t p = 0; p < len;) {
       uint16_t tmp[2];
@@ -687,7 +995,7 @@ __global__ void k_vocab_long(const RawTable tb, CandOut co, const int64_t *long_
       p += used;
     }
     uint16_t *work = units + len + 8;
-    vocab_one(co, (uint32_t)slot, units, nu, work, (int)(4 * len + 16));
+    vocab_one(co, i, slot, units, nu, work, (int)(4 * len + 16));
   }
 }
 
@@ -707,13 +1015,17 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
                                uint32_t *cand_final, unsigned int *overflow) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncand; c += (int64_t)gridDim.x * blockDim.x) {
     uint64_t cs = cand_str[c];
+    if (cs == kNoCand) {  // raw token with no output (stopword / dropped)
+      cand_final[c] = 0xFFFFFFFFu;
+      continue;
+    }
     const uint16_t *w = pool + (cs >> 16);
     int l = (int)(cs & 0xFFFF);
     uint64_t h = hash_u16(w, l);
     uint64_t slot = h & fmask;
     uint32_t res = 0xFFFFFFFFu;
     for (uint64_t probe = 0; probe <= fmask; probe++) {
-      unsigned long long k = fkeys[slot];
+      unsigned long long k = ld_agent(&fkeys[slot]);
       if (k == 0) {
         unsigned long long old = atomicCAS(&fkeys[slot], 0ull, (unsigned long long)h);
         if (old == 0) {
@@ -724,8 +1036,8 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
         k = old;
       }
       if (k == h) {
-        unsigned long long rr = freps[slot];
-        for (int spin = 0; rr == 0 && spin < (1 << 22); spin++) rr = atomicOr(&freps[slot], 0ull);
+        unsigned long long rr = ld_agent(&freps[slot]);
+        for (int spin = 0; rr == 0 && spin < (1 << 22); spin++) rr = ld_agent(&freps[slot]);
         if (rr != 0) {
           uint64_t os = cand_str[rr - 1];
           const uint16_t *o = pool + (os >> 16);
@@ -836,16 +1148,22 @@ __global__ void k_final_gather(const uint32_t *order, int64_t V, const uint32_t 
   }
 }
 
-// raw slot -> term ids.  cand sorted by (slot, ordinal).
-__global__ void k_raw_term(const uint64_t *ckey_s, const uint32_t *cidx_s, int64_t ncand, const uint32_t *cand_final,
-                           const int32_t *rank_of_slot, const int32_t *raw_nout, int32_t *raw_term,
-                           int32_t *multi_term) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ncand; i += (int64_t)gridDim.x * blockDim.x) {
-    int32_t term = rank_of_slot[cand_final[cidx_s[i]]];
-    multi_term[i] = term;
-    uint32_t slot = (uint32_t)(ckey_s[i] >> 32);
-    uint32_t ord = (uint32_t)ckey_s[i];
-    if (ord == 0) raw_term[slot] = raw_nout[slot] == 1 ? term : -(int32_t)(2 + i);
+// raw slot -> term ids.  Primary candidate i (list index) gives raw_term[rlist[i]]
+// for single-output tokens; multi-output tokens are resolved from the overflow
+// list sorted by (slot, ordinal): multi_term[j..j+nout) and raw_term = -(2 + j).
+__global__ void k_raw_term(const int32_t *rlist, int64_t nraw, const uint32_t *cand_final, const int32_t *rank_of_slot,
+                           const int32_t *raw_nout, int32_t *raw_term) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nraw; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t slot = rlist[i];
+    if (raw_nout[slot] == 1) raw_term[slot] = rank_of_slot[cand_final[i]];
+  }
+}
+__global__ void k_raw_multi(const uint64_t *okey_s, const uint32_t *oidx_s, int64_t novf, int64_t nraw,
+                            const uint32_t *cand_final, const int32_t *rank_of_slot, int32_t *raw_term,
+                            int32_t *multi_term) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < novf; j += (int64_t)gridDim.x * blockDim.x) {
+    multi_term[j] = rank_of_slot[cand_final[nraw + oidx_s[j]]];
+    if ((uint32_t)okey_s[j] == 0) raw_term[(uint32_t)(okey_s[j] >> 32)] = -(int32_t)(2 + j);
   }
 }
 
@@ -1078,9 +1396,10 @@ __global__ void k_compact_flags(const uint8_t *flag, int64_t n, int64_t *list, u
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     if (flag[i]) list[atomicAdd(cnt, 1ull)] = i;
 }
-__global__ void k_long_lens(const int64_t *list, int64_t n, const RawSlot *slots, int64_t *lens) {
+__global__ void k_long_lens(const int64_t *list, int64_t n, const int32_t *rlist, const RawSlot *slots,
+                            int64_t *lens) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    lens[i] = 5 * (int64_t)(slots[list[i]].rep & 0xFFFFFFull) + 32;
+    lens[i] = 5 * (int64_t)(slots[rlist[list[i]]].rep & 0xFFFFFFull) + 32;
 }
 __global__ void k_big_list(const int32_t *prec, int64_t n, int64_t *list, unsigned long long *cnt) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -1165,13 +1484,16 @@ enum {
   W_S, W_E, W_C, W_CNT, W_EOF, W_NEXTS, W_RS, W_RE, W_DOCNO, W_SLOW, W_SLOWLIST, W_SCROFF, W_U16, W_BOFF,
   W_TOK, W_NTOK, W_RKEYS, W_RREPS, W_POOL, W_CKEY, W_CSTR, W_NOUT, W_LONG, W_FKEYS, W_FREPS, W_CFINAL,
   W_VSLOT, W_KHI, W_KLO, W_VIDX, W_T0, W_T1, W_T2, W_T3, W_RAWTERM, W_MULTI, W_PERM, W_PREC, W_PTERM, W_PVAL,
-  W_MAXNOUT
+  W_MAXNOUT, W_SS, W_SE, W_SC, W_RLIST, W_RFLAG, W_POFF, W_OVFKEY, W_FREC,
+  W_NSLOTS
 };
+constexpr int kBuildWs = 64;  // build slots live at ctx->ws[64..127]
+static_assert(W_NSLOTS <= 64, "too many build workspace slots");
 
 sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st) {
   if (!cx->has_map) throw Error(SME_ENOMAP, "no docno mapping loaded (sme_load_docno_mapping)");
   if (cx->cfg.k != 1) throw Error(SME_ENOTIMPL, "K > 1 term k-gram indexes are not built on the device yet");
-  auto &W = cx->ws;
+  DevBuf *W = cx->ws + kBuildWs;
   Prof prof(st);
   auto cub_tmp = [&](size_t bytes) { return cx->cub_tmp.get(bytes); };
   unsigned long long *cnt = W[W_CNT].as<unsigned long long>(16);
@@ -1204,18 +1526,18 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   prof.mark("scan_tags");
 
   // sort S, E, C positions
-  auto sort_u64 = [&](uint64_t *&buf, int64_t cnt_, int slot_alt) {
-    if (cnt_ < 2) return;
+  // sorted copies land in spare workspace slots (no device-to-device copy back)
+  auto sort_u64 = [&](uint64_t *buf, int64_t cnt_, int slot_alt) -> uint64_t * {
+    if (cnt_ < 2) return buf;
     uint64_t *alt = W[slot_alt].as<uint64_t>(cnt_);
     size_t tb = 0;
     SME_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, buf, alt, (int)cnt_, 0, bits_for(n), st));
     SME_HIP(hipcub::DeviceRadixSort::SortKeys(cub_tmp(tb), tb, buf, alt, (int)cnt_, 0, bits_for(n), st));
-    SME_HIP(hipMemcpyAsync(buf, alt, cnt_ * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+    return alt;
   };
-  uint64_t *S = W[W_S].as<uint64_t>(capS), *E = W[W_E].as<uint64_t>(capE), *C = W[W_C].as<uint64_t>(capC);
-  sort_u64(S, nS, W_T0);
-  sort_u64(E, nE, W_T0);
-  sort_u64(C, nC, W_T0);
+  uint64_t *S = sort_u64(W[W_S].as<uint64_t>(capS), nS, W_SS);
+  uint64_t *E = sort_u64(W[W_E].as<uint64_t>(capE), nE, W_SE);
+  uint64_t *C = sort_u64(W[W_C].as<uint64_t>(capC), nC, W_SC);
 
   // ---------------- K1b records ----------------
   int64_t *e_of = W[W_EOF].as<int64_t>(nS + 1), *next_s = W[W_NEXTS].as<int64_t>(nS + 1);
@@ -1276,24 +1598,43 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   prof.mark("docno_sort");
 
   // ---------------- K3 tokenize ----------------
-  uint64_t rcap = next_pow2(std::max<uint64_t>(1ull << 20, std::min<uint64_t>(n / 256, 1ull << 30)));
+  // Raw-vocabulary table: sized from the previous build's distinct-token count
+  // (load <= 1/2, so the hot part stays cache resident), or from the corpus size
+  // the first time; a probe run longer than kMaxProbe retries with a 4x table.
+  uint64_t rcap = cx->raw_cap_hint
+                      ? cx->raw_cap_hint
+                      : next_pow2(std::max<uint64_t>(1ull << 20, std::min<uint64_t>(n / 256, 1ull << 30)));
   uint32_t *tok = W[W_TOK].as<uint32_t>(n / 2 + 2);
   int32_t *ntok = W[W_NTOK].as<int32_t>(nR + 1);
   RawTable tb;
   unsigned int *ovf = reinterpret_cast<unsigned int *>(cnt + 8);
+  // fast-path records (ascending), for the stream tokenizer
+  int32_t *frec = W[W_FREC].as<int32_t>(nR + 1);
+  int64_t nF = 0;
+  if (nR > 0) {
+    uint8_t *fflag = W[W_RFLAG].as<uint8_t>(nR);
+    hipLaunchKernelGGL(k_not_flags, dim3(grid_for(nR)), dim3(256), 0, st, slow, nR, fflag);
+    size_t tbb = 0;
+    hipcub::CountingInputIterator<int32_t> it(0);
+    int32_t *d_nf = reinterpret_cast<int32_t *>(cnt + 14);
+    SME_HIP(hipcub::DeviceSelect::Flagged(nullptr, tbb, it, fflag, frec, d_nf, (int)nR, st));
+    SME_HIP(hipcub::DeviceSelect::Flagged(cub_tmp(tbb), tbb, it, fflag, frec, d_nf, (int)nR, st));
+    nF = d2h(d_nf, st);
+  }
   for (int attempt = 0;; attempt++) {
     tb.slots = W[W_RKEYS].as<RawSlot>(rcap);
     tb.mask = rcap - 1;
     tb.text = t;
     tb.overflow = ovf;
-    tb.count = W[W_MAXNOUT].as<unsigned long long>(4) + 1;
     SME_HIP(hipMemsetAsync(tb.slots, 0, rcap * sizeof(RawSlot), st));
-    SME_HIP(hipMemsetAsync(tb.count, 0, 8, st));
     SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
     if (nR > 0) {
-      hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)std::min<int64_t>(nR, 65536)), dim3(kTokNT), 0, st, t,
-                         (int64_t)n, rs, re, nR, slow, tok, ntok, tb);
-      SME_CHECK_LAUNCH();
+      if (nF > 0) {
+        const int64_t tgrid = std::min<int64_t>(nF, 4096), rpb = (nF + tgrid - 1) / tgrid;
+        hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)((nF + rpb - 1) / rpb)), dim3(kTokNT), 0, st, t, (int64_t)n, rs,
+                           re, frec, nF, rpb, tok, ntok, tb);
+        SME_CHECK_LAUNCH();
+      }
     }
     if (nslow > 0) {
       int64_t *slist = W[W_SLOWLIST].as<int64_t>(nslow);
@@ -1320,29 +1661,51 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   prof.mark("tokenize");
 
   // ---------------- K4 vocabulary ----------------
+  // distinct raw tokens -> rlist (ascending slot order)
+  uint8_t *rflag = W[W_RFLAG].as<uint8_t>(rcap);
+  int32_t *rlist = W[W_RLIST].as<int32_t>(rcap);
+  int32_t *d_nsel = reinterpret_cast<int32_t *>(cnt + 13);
+  hipLaunchKernelGGL(k_raw_flags, dim3(grid_for((int64_t)rcap)), dim3(256), 0, st, tb.slots, rcap, rflag);
+  {
+    size_t tbb = 0;
+    hipcub::CountingInputIterator<int32_t> it(0);
+    SME_HIP(hipcub::DeviceSelect::Flagged(nullptr, tbb, it, rflag, rlist, d_nsel, (int)rcap, st));
+    SME_HIP(hipcub::DeviceSelect::Flagged(cub_tmp(tbb), tbb, it, rflag, rlist, d_nsel, (int)rcap, st));
+  }
+  const int64_t nraw = d2h(d_nsel, st);
+  cx->raw_cap_hint = next_pow2(std::max<uint64_t>(1ull << 20, 2 * (uint64_t)nraw));
+  int64_t *poff = W[W_POFF].as<int64_t>(nraw + 1);
+  {
+    int64_t *lens = W[W_T0].as<int64_t>(nraw + 1);
+    hipLaunchKernelGGL(k_raw_lens, dim3(grid_for(nraw + 1)), dim3(256), 0, st, tb.slots, rlist, nraw, lens);
+    size_t tbb = 0;
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, lens, poff, (int)nraw + 1, st));
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, lens, poff, (int)nraw + 1, st));
+  }
+  const int64_t pool_units = d2h(poff + nraw, st);
   CandOut co;
-  const uint64_t nraw = d2h(tb.count, st);
-  uint64_t cand_cap = std::max<uint64_t>(cx->vocab_cand_cap, nraw + nraw / 8 + 1024);
-  uint64_t pool_cap = std::max<uint64_t>(cx->vocab_pool_cap, 12 * cand_cap);
+  co.pool = W[W_POOL].as<uint16_t>(pool_units + 1);
+  co.poff = poff;
+  co.nraw = nraw;
   co.raw_nout = W[W_NOUT].as<int32_t>(rcap);
   int32_t *max_nout = W[W_MAXNOUT].as<int32_t>(4);  // must survive the counter resets below
   co.max_nout = max_nout;
+  co.err = ovf;
   int64_t *long_list = nullptr;
   uint64_t long_cap = std::max<uint64_t>(cx->vocab_long_cap, 4096);
-  int64_t ncand = 0, nlong = 0;
+  uint64_t ovf_cap = std::max<uint64_t>(cx->vocab_ovf_cap, 4096);
+  int64_t novf = 0, nlong = 0;
   for (int attempt = 0;; attempt++) {
-    co.pool = W[W_POOL].as<uint16_t>(pool_cap);
-    co.pool_cap = pool_cap;
-    co.cand_key = W[W_CKEY].as<uint64_t>(cand_cap);
-    co.cand_str = W[W_CSTR].as<uint64_t>(cand_cap);
-    co.cand_cap = cand_cap;
-    co.pool_used = cnt + 3;
-    co.ncand = cnt + 4;
+    co.cand_str = W[W_CSTR].as<uint64_t>(nraw + ovf_cap);
+    co.ovf_key = W[W_OVFKEY].as<uint64_t>(ovf_cap);
+    co.ovf_cap = ovf_cap;
+    co.novf = cnt + 4;
     long_list = W[W_LONG].as<int64_t>(long_cap);
-    SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
+    SME_HIP(hipMemsetAsync(cnt, 0, 13 * sizeof(unsigned long long), st));
     SME_HIP(hipMemsetAsync(max_nout, 0, sizeof(int32_t), st));
-    hipLaunchKernelGGL(k_vocab, dim3(grid_for((int64_t)rcap, 256, 16384)), dim3(256), 0, st, tb, co, long_list,
-                       cnt + 5, long_cap);
+    if (nraw > 0)
+      hipLaunchKernelGGL(k_vocab, dim3(grid_for(nraw, 256, 16384)), dim3(256), 0, st, tb, rlist, nraw, co,
+                         long_list, cnt + 5, long_cap);
     SME_CHECK_LAUNCH();
     nlong = (int64_t)d2h(cnt + 5, st);
     if ((uint64_t)nlong > long_cap) {
@@ -1351,31 +1714,33 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     }
     if (nlong > 0) {
       int64_t *lens = W[W_T0].as<int64_t>(nlong + 1), *soff = W[W_T1].as<int64_t>(nlong + 1);
-      hipLaunchKernelGGL(k_long_lens, dim3(grid_for(nlong)), dim3(256), 0, st, long_list, nlong, tb.slots, lens);
+      hipLaunchKernelGGL(k_long_lens, dim3(grid_for(nlong)), dim3(256), 0, st, long_list, nlong, rlist, tb.slots,
+                         lens);
       SME_HIP(hipMemsetAsync(lens + nlong, 0, sizeof(int64_t), st));
       size_t tbb = 0;
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, lens, soff, (int)nlong + 1, st));
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, lens, soff, (int)nlong + 1, st));
       int64_t tot = d2h(soff + nlong, st);
       uint16_t *scr = W[W_U16].as<uint16_t>(tot + 1);
-      hipLaunchKernelGGL(k_vocab_long, dim3(grid_for(nlong, 64)), dim3(64), 0, st, tb, co, long_list, nlong, soff,
-                         scr);
+      hipLaunchKernelGGL(k_vocab_long, dim3(grid_for(nlong, 64)), dim3(64), 0, st, tb, rlist, co, long_list, nlong,
+                         soff, scr);
       SME_CHECK_LAUNCH();
     }
     unsigned long long hc[2];
-    SME_HIP(hipMemcpyAsync(hc, cnt + 3, sizeof hc, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipMemcpyAsync(hc, cnt + 4, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipMemcpyAsync(hc + 1, cnt + 8, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
-    if (hc[0] <= pool_cap && hc[1] <= cand_cap) {
-      ncand = (int64_t)hc[1];
-      cx->vocab_cand_cap = cand_cap;
-      cx->vocab_pool_cap = pool_cap;
+    if ((unsigned)hc[1] & 1u) throw Error(SME_ELIMIT, "vocabulary pool region overrun");
+    if (hc[0] <= ovf_cap) {
+      novf = (int64_t)hc[0];
       cx->vocab_long_cap = long_cap;
+      cx->vocab_ovf_cap = ovf_cap;
       break;
     }
-    if (attempt > 3) throw Error(SME_ELIMIT, "vocabulary pool");
-    pool_cap = std::max<uint64_t>(pool_cap, hc[0] + 1024);
-    cand_cap = std::max<uint64_t>(cand_cap, hc[1] + 1024);
+    if (attempt > 3) throw Error(SME_ELIMIT, "vocabulary overflow list");
+    ovf_cap = hc[0] + 1024;
   }
+  const int64_t ncand = nraw + novf;
   // final-term dedup
   uint64_t fcap = next_pow2(std::max<int64_t>(1024, 2 * ncand));
   unsigned long long *fkeys = W[W_FKEYS].as<unsigned long long>(fcap);
@@ -1448,19 +1813,22 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   }
   // raw slot -> term ids
   int32_t *raw_term = W[W_RAWTERM].as<int32_t>(rcap);
-  int32_t *multi = W[W_MULTI].as<int32_t>(ncand + 1);
+  int32_t *multi = W[W_MULTI].as<int32_t>(novf + 1);
   SME_HIP(hipMemsetAsync(raw_term, 0xFF, rcap * sizeof(int32_t), st));
-  if (ncand > 0) {
-    uint64_t *ck2 = W[W_T0].as<uint64_t>(ncand);
-    uint32_t *ci = W[W_T1].as<uint32_t>(ncand), *ci2 = W[W_VIDX].as<uint32_t>(ncand);
-    hipLaunchKernelGGL(k_iota_u32, dim3(grid_for(ncand)), dim3(256), 0, st, ci, ncand);
+  if (nraw > 0)
+    hipLaunchKernelGGL(k_raw_term, dim3(grid_for(nraw)), dim3(256), 0, st, rlist, nraw, cand_final, rank_of_slot,
+                       co.raw_nout, raw_term);
+  if (novf > 0) {
+    uint64_t *ok2 = W[W_T0].as<uint64_t>(novf);
+    uint32_t *oi = W[W_T1].as<uint32_t>(novf), *oi2 = W[W_VIDX].as<uint32_t>(novf);
+    hipLaunchKernelGGL(k_iota_u32, dim3(grid_for(novf)), dim3(256), 0, st, oi, novf);
     size_t tbb = 0;
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, co.cand_key, ck2, ci, ci2, (int)ncand, 0, 64, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, co.cand_key, ck2, ci, ci2, (int)ncand, 0, 64, st));
-    hipLaunchKernelGGL(k_raw_term, dim3(grid_for(ncand)), dim3(256), 0, st, ck2, ci2, ncand, cand_final,
-                       rank_of_slot, co.raw_nout, raw_term, multi);
-    SME_CHECK_LAUNCH();
+    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, co.ovf_key, ok2, oi, oi2, (int)novf, 0, 64, st));
+    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, co.ovf_key, ok2, oi, oi2, (int)novf, 0, 64, st));
+    hipLaunchKernelGGL(k_raw_multi, dim3(grid_for(novf)), dim3(256), 0, st, ok2, oi2, novf, nraw, cand_final,
+                       rank_of_slot, raw_term, multi);
   }
+  SME_CHECK_LAUNCH();
   prof.mark("vocabulary");
 
   // ---------------- K5 aggregation ----------------

@@ -17,9 +17,9 @@ struct sme_ctx {
   int64_t map_n = 0;  // entries including the "" sentinel
   bool has_map = false;
   // build workspace, reused across builds (see DevBuf)
-  sme::DevBuf ws[64];  // 0..47 build, 48..63 query / serializer / tokenizer
+  sme::DevBuf ws[128];  // 48..63 query / serializer / tokenizer / reweight, 64..127 build
   sme::DevBuf cub_tmp;
-  uint64_t vocab_cand_cap = 0, vocab_pool_cap = 0, vocab_long_cap = 0;  // learned across builds
+  uint64_t vocab_long_cap = 0, vocab_ovf_cap = 0, raw_cap_hint = 0;  // learned across builds
   std::string profile_json;
   std::vector<std::pair<std::string, float>> last_profile;
 };
