@@ -1363,6 +1363,19 @@ __global__ void k_weights(const uint32_t *key, const int32_t *tf, int64_t P, con
   }
 }
 
+// idf of every term (the same expression k_weights evaluates per posting)
+__global__ void k_term_idf(const int64_t *off, int64_t V, double idf_ref, int64_t N, const int64_t *gdf,
+                           const double *idf_by_df, int64_t sdf, const double *idf_by_q, int mode, double *idf) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
+    if (mode == SME_IDF_REFERENCE) {
+      idf[t] = idf_ref;
+    } else {
+      const int64_t df = gdf ? gdf[t] : off[t + 1] - off[t];
+      idf[t] = df <= sdf ? idf_by_df[df] : idf_by_q[N / df];
+    }
+  }
+}
+
 __global__ void k_composite(const uint32_t *key, const int32_t *tf, int64_t P, int tfbits, uint64_t tfmask,
                             uint64_t *ck) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x)
@@ -1765,8 +1778,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   const int64_t V = (int64_t)hv[1];
   const int term_maxlen = (int)(int32_t)(uint32_t)hv[12];
 
-  sme_index *ix = new sme_index();
-  ix->ctx = cx;
+  sme_index *ix = new sme_index(cx);
   ix->K = cx->cfg.k;
   ix->R = cx->cfg.num_partitions;
   ix->idf_mode = cx->cfg.idf_mode;
@@ -1949,7 +1961,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     // platform libm so the device weights equal the fp64 reference bit for bit.
     std::vector<double> lut(max_tf + 1, 0.0);
     for (int i = 1; i <= max_tf; i++) lut[i] = 1.0 + log((double)i);
-    double *d_lut = W[W_T2].as<double>(max_tf + 1);
+    double *d_lut = ix->d_lut.as<double>(max_tf + 1);
     SME_HIP(hipMemcpyAsync(d_lut, lut.data(), lut.size() * sizeof(double), hipMemcpyHostToDevice, st));
     const int64_t Nn = std::max<int64_t>(nR, 0);
     double idf_ref = log10((double)(Nn / 1));  // stored df of every real term is 1 (T1)
@@ -1961,6 +1973,10 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     double *d_byq = d_bydf + by_df.size();
     SME_HIP(hipMemcpyAsync(d_bydf, by_df.data(), by_df.size() * sizeof(double), hipMemcpyHostToDevice, st));
     SME_HIP(hipMemcpyAsync(d_byq, by_q.data(), by_q.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    double *idf = ix->d_idf.as<double>(V + 1);
+    if (V > 0)
+      hipLaunchKernelGGL(k_term_idf, dim3(grid_for(V)), dim3(256), 0, st, off, V, idf_ref, Nn, nullptr, d_bydf, sdf,
+                         d_byq, ix->idf_mode, idf);
     double *w = ix->d_w.as<double>(PP + 1);
     if (PP > 0)
       hipLaunchKernelGGL(k_weights, dim3(grid_for(PP)), dim3(256), 0, st, key_s, tf_d, PP, d_lut, idf_ref, off, Nn,
@@ -2022,11 +2038,15 @@ void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t 
   std::vector<double> by_df(sdf + 1), by_q(Nn / std::max<int64_t>(sdf, 1) + 2);
   for (int64_t d = 1; d <= sdf; d++) by_df[d] = log10((double)(Nn / d));
   for (size_t q = 0; q < by_q.size(); q++) by_q[q] = log10((double)q);
-  double *d_lut = W[56].as<double>(lut.size());
+  double *d_lut = ix->d_lut.as<double>(lut.size());
   double *d_tab = W[57].as<double>(by_df.size() + by_q.size());
   SME_HIP(hipMemcpyAsync(d_lut, lut.data(), lut.size() * sizeof(double), hipMemcpyHostToDevice, st));
   SME_HIP(hipMemcpyAsync(d_tab, by_df.data(), by_df.size() * sizeof(double), hipMemcpyHostToDevice, st));
   SME_HIP(hipMemcpyAsync(d_tab + by_df.size(), by_q.data(), by_q.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  if (ix->V > 0)
+    hipLaunchKernelGGL(k_term_idf, dim3((unsigned)std::min<int64_t>((ix->V + 255) / 256, 65536)), dim3(256), 0, st,
+                       (const int64_t *)ix->d_off.p, ix->V, idf_ref, Nn, d_gdf, d_tab, sdf, d_tab + by_df.size(),
+                       ix->idf_mode, (double *)ix->d_idf.p);
   if (ix->V > 0)
     hipLaunchKernelGGL(k_reweight, dim3((unsigned)std::min<int64_t>((ix->V + 3) / 4, 65536)),
                        dim3(256), 0, st, (const int64_t *)ix->d_off.p, ix->V, (const int32_t *)ix->d_tf_d.p, d_lut,

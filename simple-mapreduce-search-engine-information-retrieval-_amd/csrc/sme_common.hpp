@@ -28,21 +28,52 @@ struct Error : std::runtime_error {
 
 #define SME_CHECK_LAUNCH() SME_HIP(hipGetLastError())
 
+// Freed device blocks kept for reuse (index arrays are rebuilt every step:
+// hipMalloc/hipFree of gigabytes per build stalls for hundreds of ms).
+struct BufPool {
+  std::vector<std::pair<void *, size_t>> blocks;
+  void *take(size_t bytes, size_t *cap) {
+    size_t best = blocks.size();
+    for (size_t i = 0; i < blocks.size(); i++)
+      if (blocks[i].second >= bytes && blocks[i].second <= 2 * bytes + (64u << 20) &&
+          (best == blocks.size() || blocks[i].second < blocks[best].second))
+        best = i;
+    if (best == blocks.size()) return nullptr;
+    void *p = blocks[best].first;
+    *cap = blocks[best].second;
+    blocks.erase(blocks.begin() + (ptrdiff_t)best);
+    return p;
+  }
+  void put(void *p, size_t cap) { blocks.emplace_back(p, cap); }
+  ~BufPool() {
+    for (auto &b : blocks) (void)hipFree(b.first);
+  }
+};
+
 // A device buffer that grows on demand and is kept across builds, so the
-// timed path does no hipMalloc once warmed up.
+// timed path does no hipMalloc once warmed up.  With a pool, blocks come from
+// and go back to it instead of hipMalloc/hipFree.
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
+  BufPool *pool = nullptr;
   void *get(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes > cap) {
       if (p) {
         SME_HIP(hipDeviceSynchronize());  // in-flight kernels may still use the old block
-        SME_HIP(hipFree(p));
+        if (pool)
+          pool->put(p, cap);
+        else
+          SME_HIP(hipFree(p));
       }
       p = nullptr;
-      size_t nc = bytes + bytes / 8;
-      SME_HIP(hipMalloc(&p, nc));
+      size_t nc = 0;
+      if (pool) p = pool->take(bytes, &nc);
+      if (!p) {
+        nc = bytes + bytes / 8;
+        SME_HIP(hipMalloc(&p, nc));
+      }
       cap = nc;
     }
     return p;
@@ -52,7 +83,12 @@ struct DevBuf {
     return reinterpret_cast<T *>(get(n * sizeof(T)));
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      if (pool)
+        pool->put(p, cap);
+      else
+        (void)hipFree(p);
+    }
     p = nullptr;
     cap = 0;
   }

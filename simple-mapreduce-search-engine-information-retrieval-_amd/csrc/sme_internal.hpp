@@ -9,6 +9,7 @@
 #include "sme_common.hpp"
 
 struct sme_ctx {
+  sme::BufPool pool;  // declared first: destroyed after every DevBuf below
   sme_config cfg{};
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -37,6 +38,8 @@ struct sme_index {
   sme::DevBuf d_docno_d;  // int32 [P]
   sme::DevBuf d_tf_d;     // int32 [P]
   sme::DevBuf d_w;        // double [P]
+  sme::DevBuf d_idf;      // double [V]   idf of every term (query side: w = lut[tf] * idf)
+  sme::DevBuf d_lut;      // double [max_tf + 1]  1 + ln(tf)
   // reduce-output CSR: (tf desc, docno asc) per term (MyReducer.reduce order)
   sme::DevBuf d_docno_o;  // int32 [P]
   sme::DevBuf d_tf_o;     // int32 [P]
@@ -58,6 +61,11 @@ struct sme_index {
   bool h_terms_ready = false;
   // stage timings of the build that produced this index (ms)
   std::vector<std::pair<std::string, float>> profile;
+  explicit sme_index(sme_ctx *c) : ctx(c) {
+    for (sme::DevBuf *b : {&d_term_off, &d_term_chars, &d_off, &d_docno_d, &d_tf_d, &d_w, &d_idf, &d_lut, &d_docno_o,
+                           &d_tf_o, &d_rec_docno, &d_ser})
+      b->pool = &c->pool;
+  }
 };
 
 namespace sme {

@@ -11,13 +11,17 @@
 // Output order: score desc, docno asc (north-star tie-break; equals the
 // reference's stable Collections.sort for single-term queries).
 //
-// Kernel shape: one 256-lane workgroup per query.  Postings are docno-sorted
-// per term, so the workgroup sweeps the docno axis in tiles of kTile docs held
-// as an fp64 accumulator in LDS; for each tile it streams every query term's
-// postings that fall in the tile (coalesced, 256 at a time, the block barrier
-// of __syncthreads_count separates terms so the add order per doc is the
-// query-token order).  Touched accumulator entries feed a per-lane top-k list
-// in LDS; the lists are merged by k rounds of block arg-max.
+// Kernel shape: one 256-lane workgroup per query, sweeping the docno axis in
+// tiles of kTile documents whose fp64 accumulators live in LDS (32 KiB, so four
+// workgroups share a CU).  Postings are docno-sorted per term; for each tile the
+// workgroup streams every query term's postings that fall in it, 1024 per step
+// (4 per lane, coalesced), in query-token order -- one barrier per step, and
+// postings of one term have distinct docnos, so a document's adds happen in
+// token order and the fp64 sum is the reference's.  The weight of a posting is
+// lut[tf] * idf[term] (fp64, no contraction: bit-identical to the build's
+// TF-IDF pass), so a posting costs 8 bytes of HBM (docno, tf), not 12.  Each
+// lane keeps its best KMAX (score, docno) in registers; the lists are merged by
+// k rounds of block arg-max at the end.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -28,25 +32,56 @@ namespace sme {
 
 constexpr int kQNT = 256;
 constexpr int kTile = 4096;
+constexpr int kQPer = 4;  // postings per lane per step
 constexpr int kMaxQTerms = 128;
+constexpr int kLutLds = 256;  // 1 + ln(tf) for tf < 256 from LDS, the rare rest from HBM
 
 __device__ __forceinline__ bool better(double as, int32_t ad, double bs, int32_t bd) {
   return as > bs || (as == bs && ad < bd);
 }
 
+// insert (s, d) into the descending register list ts/td (fully unrolled: no
+// dynamic register indexing)
+template <int K>
+__device__ __forceinline__ void topk_insert(double (&ts)[K], int32_t (&td)[K], double s, int32_t d) {
+  if (!better(s, d, ts[K - 1], td[K - 1])) return;
+  bool done = false;
+#pragma unroll
+  for (int i = K - 1; i >= 1; i--) {
+    if (!done) {
+      if (better(s, d, ts[i - 1], td[i - 1])) {
+        ts[i] = ts[i - 1];
+        td[i] = td[i - 1];
+      } else {
+        ts[i] = s;
+        td[i] = d;
+        done = true;
+      }
+    }
+  }
+  if (!done) {
+    ts[0] = s;
+    td[0] = d;
+  }
+}
+
 template <int KMAX>
 __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off, const int32_t *__restrict__ docno,
-                                                const double *__restrict__ w, const int32_t *__restrict__ terms,
-                                                const int64_t *__restrict__ qoff, int nq, int k, int32_t *out_d,
-                                                double *out_s, int *err) {
+                                                const int32_t *__restrict__ tf, const double *__restrict__ lut,
+                                                int max_tf, const double *__restrict__ idf,
+                                                const int32_t *__restrict__ terms, const int64_t *__restrict__ qoff,
+                                                int nq, int k, int32_t *out_d, double *out_s, int *err) {
   __shared__ double acc[kTile];
-  __shared__ double topS[KMAX * kQNT];
-  __shared__ int32_t topD[KMAX * kQNT];
+  __shared__ double s_lut[kLutLds];
   __shared__ int64_t cur[kMaxQTerms], endp[kMaxQTerms];
-  __shared__ int32_t s_lo;
+  __shared__ double tidf[kMaxQTerms];
+  __shared__ int32_t s_next;
+  __shared__ unsigned long long s_stop;
   __shared__ double red_s[kQNT / 64];
   __shared__ int32_t red_d[kQNT / 64], red_t[kQNT / 64];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (int j = tid; j < kTile; j += kQNT) acc[j] = -1.0;  // untouched (weights are >= 0)
+  for (int j = tid; j < kLutLds; j += kQNT) s_lut[j] = j <= max_tf ? lut[j] : 0.0;
   for (int q = blockIdx.x; q < nq; q += gridDim.x) {
     const int64_t q0 = qoff[q];
     int nt = (int)(qoff[q + 1] - q0);
@@ -54,71 +89,97 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
       if (tid == 0) atomicOr(err, 1);
       nt = kMaxQTerms;
     }
+    if (tid == 0) s_next = 0x7FFFFFFF;
+    __syncthreads();
     for (int i = tid; i < nt; i += kQNT) {
-      int32_t t = terms[q0 + i];
-      cur[i] = t >= 0 ? off[t] : 0;
-      endp[i] = t >= 0 ? off[t + 1] : 0;
+      const int32_t t = terms[q0 + i];
+      const int64_t b = t >= 0 ? off[t] : 0, e = t >= 0 ? off[t + 1] : 0;
+      cur[i] = b;
+      endp[i] = e;
+      tidf[i] = t >= 0 ? idf[t] : 0.0;
+      if (b < e) atomicMin(&s_next, docno[b]);
     }
+    double ts[KMAX];
+    int32_t td[KMAX];
+#pragma unroll
     for (int j = 0; j < KMAX; j++) {
-      topS[j * kQNT + tid] = -INFINITY;
-      topD[j * kQNT + tid] = 0x7FFFFFFF;
+      ts[j] = -INFINITY;
+      td[j] = 0x7FFFFFFF;
     }
     __syncthreads();
-    for (;;) {
-      // next tile starts at the smallest unprocessed docno of any term
-      if (tid == 0) s_lo = 0x7FFFFFFF;
-      __syncthreads();
-      bool any = false;
-      for (int i = tid; i < nt; i += kQNT)
-        if (cur[i] < endp[i]) {
-          atomicMin(&s_lo, docno[cur[i]]);
-          any = true;
-        }
-      if (__syncthreads_count(any) == 0) break;
-      const int32_t lo = s_lo;
+    while (s_next != 0x7FFFFFFF) {  // uniform: read after a barrier
+      const int32_t lo = s_next;
       const int64_t hi = (int64_t)lo + kTile;
-      for (int j = tid; j < kTile; j += kQNT) acc[j] = -1.0;  // untouched (weights are >= 0)
       __syncthreads();
+      if (tid == 0) s_next = 0x7FFFFFFF;
       for (int i = 0; i < nt; i++) {
-        int64_t c = cur[i];
-        const int64_t e = endp[i];
+        const int64_t c = cur[i], e = endp[i];
+        if (c >= e) continue;  // uniform
+        const double w_idf = tidf[i];
+        if (tid == 0) s_stop = (unsigned long long)e;
+        __syncthreads();
+        // Each lane walks its stride of the term's postings until the first docno
+        // >= hi; the smallest stop over lanes is the term's first posting beyond
+        // the tile, and the docno there is that term's next docno.
+        int64_t p = c + tid;
+        int32_t dstop = 0x7FFFFFFF;
         for (;;) {
-          const int64_t p = c + tid;
-          bool in = p < e && (int64_t)docno[p] < hi;
-          int n_in = __syncthreads_count(in);
-          if (in) {
-            const int d = docno[p] - lo;
-            const double v = acc[d];
-            acc[d] = v < 0.0 ? w[p] : v + w[p];
+          int32_t dv[kQPer], fv[kQPer];
+#pragma unroll
+          for (int u = 0; u < kQPer; u++) {
+            const int64_t pu = p + (int64_t)u * kQNT;
+            dv[u] = pu < e ? docno[pu] : 0x7FFFFFFF;
+            fv[u] = pu < e ? tf[pu] : 0;
           }
-          c += n_in;
-          if (n_in < kQNT) break;
+          bool stop = false;
+#pragma unroll
+          for (int u = 0; u < kQPer; u++) {
+            if (stop) continue;
+            if ((int64_t)dv[u] >= hi || p + (int64_t)u * kQNT >= e) {
+              stop = true;
+              p += (int64_t)u * kQNT;
+              dstop = p < e ? dv[u] : 0x7FFFFFFF;
+              continue;
+            }
+            const int d = dv[u] - lo;
+            const double l = fv[u] < kLutLds ? s_lut[fv[u]] : lut[fv[u]];
+            const double w = __dmul_rn(l, w_idf);
+            const double v = acc[d];
+            acc[d] = v < 0.0 ? w : __dadd_rn(v, w);
+          }
+          if (stop) break;
+          p += (int64_t)kQPer * kQNT;
         }
-        if (tid == 0) cur[i] = c;
+        // wave minima first: one LDS atomic per wave, not per lane
+        unsigned long long pm = (unsigned long long)p;
+        int32_t dm = dstop;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const unsigned long long po = __shfl_xor(pm, o, 64);
+          const int32_t dd = __shfl_xor(dm, o, 64);
+          pm = po < pm ? po : pm;
+          dm = dd < dm ? dd : dm;
+        }
+        if (lane == 0) {
+          atomicMin(&s_stop, pm);
+          if (dm != 0x7FFFFFFF) atomicMin(&s_next, dm);
+        }
+        __syncthreads();  // also orders this term's adds before the next term's
+        if (tid == 0) cur[i] = (int64_t)s_stop;
       }
       __syncthreads();
       for (int j = tid; j < kTile; j += kQNT) {
         const double sc = acc[j];
         if (sc < 0.0) continue;
-        const int32_t dn = lo + j;
-        const int last = (k - 1) * kQNT + tid;
-        if (!better(sc, dn, topS[last], topD[last])) continue;
-        int pos = k - 1;
-        while (pos > 0 && better(sc, dn, topS[(pos - 1) * kQNT + tid], topD[(pos - 1) * kQNT + tid])) {
-          topS[pos * kQNT + tid] = topS[(pos - 1) * kQNT + tid];
-          topD[pos * kQNT + tid] = topD[(pos - 1) * kQNT + tid];
-          pos--;
-        }
-        topS[pos * kQNT + tid] = sc;
-        topD[pos * kQNT + tid] = dn;
+        acc[j] = -1.0;
+        topk_insert<KMAX>(ts, td, sc, lo + j);
       }
       __syncthreads();
     }
     // merge the per-lane lists: k rounds of block arg-max over list heads
-    int head = 0;
     for (int r = 0; r < k; r++) {
-      double bs = head < k ? topS[head * kQNT + tid] : -INFINITY;
-      int32_t bd = head < k ? topD[head * kQNT + tid] : 0x7FFFFFFF;
+      double bs = ts[0];
+      int32_t bd = td[0];
       int32_t bt = tid;
       for (int o = 32; o > 0; o >>= 1) {
         double os = __shfl_xor(bs, o, 64);
@@ -129,10 +190,10 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
           bt = ot;
         }
       }
-      if ((tid & 63) == 0) {
-        red_s[tid >> 6] = bs;
-        red_d[tid >> 6] = bd;
-        red_t[tid >> 6] = bt;
+      if (lane == 0) {
+        red_s[wave] = bs;
+        red_d[wave] = bd;
+        red_t[wave] = bt;
       }
       __syncthreads();
       bs = red_s[0];
@@ -144,7 +205,15 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
           bd = red_d[x];
           bt = red_t[x];
         }
-      if (tid == bt) head++;
+      if (tid == bt) {  // pop the head: shift the winner's list left
+#pragma unroll
+        for (int j = 0; j < KMAX - 1; j++) {
+          ts[j] = ts[j + 1];
+          td[j] = td[j + 1];
+        }
+        ts[KMAX - 1] = -INFINITY;
+        td[KMAX - 1] = 0x7FFFFFFF;
+      }
       if (tid == 0) {
         const bool valid = bs != -INFINITY;
         out_d[(int64_t)q * k + r] = valid ? bd : -1;
@@ -163,14 +232,16 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   SME_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
   const int64_t *off = (const int64_t *)ix->d_off.p;
   const int32_t *dn = (const int32_t *)ix->d_docno_d.p;
-  const double *w = (const double *)ix->d_w.p;
-  unsigned grid = (unsigned)std::min(nq, 65536);
+  const int32_t *tf = (const int32_t *)ix->d_tf_d.p;
+  const double *lut = (const double *)ix->d_lut.p;
+  const double *idf = (const double *)ix->d_idf.p;
+  unsigned grid = (unsigned)std::min(nq, 1 << 20);
   if (k <= 16) {
-    hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, w, d_terms, d_qoff, nq, k, d_out_docno,
-                       d_out_score, err);
+    hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff, nq, k,
+                       d_out_docno, d_out_score, err);
   } else if (k <= 32) {
-    hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, w, d_terms, d_qoff, nq, k, d_out_docno,
-                       d_out_score, err);
+    hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff, nq, k,
+                       d_out_docno, d_out_score, err);
   } else {
     throw Error(SME_ENOTIMPL, "top-k with k > 32 is not built yet");
   }
