@@ -103,14 +103,16 @@ def main():
             ix.close()
         ix = step()
     barrier()
+    profs = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
         if ix is not None:
             ix.close()
         ix = step()
+        profs.append(ctx.last_build_profile())  # device events; the step has synchronised already
     barrier()
     dt = (time.perf_counter() - t0) / a.steps
-    prof = ctx.last_build_profile()
+    prof = {k: round(sum(p.get(k, 0.0) for p in profs) / len(profs), 4) for k in profs[-1]}
     N, V, P = ix.N, ix.V, ix.P
     t_max = dt
     tot_bytes = nbytes
@@ -123,7 +125,13 @@ def main():
         tot_bytes = float(ts[:, 1].sum())
     gbs = tot_bytes / t_max / 1e9
     alg_bytes = nbytes + 8 * P + 8 * (V + 1)  # A_build = B + 8P + 8(V+1) per GPU
-    achieved = alg_bytes / dt / 1e9
+    # dominant kernel: the stream tokenizer (k_tok_fast).  Algorithmic bytes per
+    # launch = the text it tokenizes, read once (B); its duration is the mean of
+    # the HIP events bracketing the launch on its stream over the timed steps.
+    achieved_build = alg_bytes / dt / 1e9
+    tok_ms = prof.get("tok_kernel")
+    tok_gbs = nbytes / (tok_ms * 1e-3) / 1e9 if tok_ms else None
+    traffic = pmc_traffic("k_tok_fast", a)
 
     # ---- queries (c3) ----
     query = None
@@ -146,9 +154,16 @@ def main():
         "config": {"workload": "c2: %d docs/GPU x U[400,600] tokens, V_w=%d, Zipf s=1, K=1 index + TF-IDF"
                                % (a.docs, a.vocab), "docs_per_gpu": a.docs, "text_bytes_per_gpu": nbytes,
                    "N": N, "V": V, "P": P, "parallelism": "doc-sharded x%d" % world},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "what": "whole build step: algorithmic bytes B + 8P + 8(V+1) per GPU / step time"},
+        "roofline": {"bound": "hbm", "kernel": "k_tok_fast", "achieved": round(tok_gbs, 2) if tok_gbs else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(tok_gbs / HBM_PEAK_GBS, 5) if tok_gbs else None,
+                     "traffic": traffic, "kernel_ms": tok_ms,
+                     "what": "dominant kernel k_tok_fast: algorithmic bytes = text bytes B read once per launch, / "
+                             "mean launch time (HIP events on its stream); traffic = PMC HBM bytes per launch "
+                             "(profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)"},
+        "build_roofline": {"achieved": round(achieved_build, 2), "unit": "GB/s",
+                           "frac": round(achieved_build / HBM_PEAK_GBS, 5),
+                           "what": "whole build step: A_build = B + 8P + 8(V+1) per GPU / step time"},
         "stage_ms": prof,
     }
     if query is not None:
@@ -212,11 +227,15 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     qstep()
     barrier()
     steps = max(1, a.steps // 2)
+    kms = []
     t0 = time.perf_counter()
     for _ in range(steps):
         qstep()
+        kms.append(ix.ctx.last_build_profile().get("query_kernel"))
     barrier()
     dt = (time.perf_counter() - t0) / steps
+    kms = [x for x in kms if x is not None]
+    qk_ms = sum(kms) / len(kms) if kms else None
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -226,14 +245,34 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     # algorithmic bytes: postings of distinct batch terms read once (docno + weight = 12 B here)
     tv = terms[terms >= 0]
     uniq = np.unique(tv)
-    alg = 12 * int(df[uniq].sum()) + 4 * int(nt.sum()) + 12 * k * a.queries
-    touched = 12 * int(df[tv].sum())
+    # SURVEY 8d A_q with this layout's 8 B per posting (int32 docno + int32 tf)
+    alg = 8 * int(df[uniq].sum()) + 4 * int(nt.sum()) + 12 * k * a.queries
+    touched = 8 * int(df[tv].sum())
+    t_k = (qk_ms * 1e-3) if qk_ms else dt
     return {"metric": "top-10 queries/sec", "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
             "terms_per_query": "U{2..8} drawn by df (seed 7)", "ms_per_batch": round(dt * 1e3, 3),
-            "roofline": {"bound": "hbm", "achieved": round(alg / dt / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(alg / dt / 1e9 / HBM_PEAK_GBS, 6),
-                         "what": "A_q = 12*sum(df of distinct batch terms) + 4*sum|q| + 12*k*Q"},
-            "postings_touched_GBps": round(touched / dt / 1e9, 2)}
+            "roofline": {"bound": "hbm", "kernel": "k_query", "kernel_ms": qk_ms,
+                         "achieved": round(alg / t_k / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(alg / t_k / 1e9 / HBM_PEAK_GBS, 6), "traffic": pmc_traffic("k_query", a),
+                         "what": "A_q = 8*sum(df of distinct batch terms) + 4*sum|q| + 12*k*Q per launch / "
+                                 "mean launch time (HIP events)"},
+            "postings_touched_GBps": round(touched / t_k / 1e9, 2),
+            "postings_touched_what": "8 B x postings of every query term (re-reads across queries included)"}
+
+
+def pmc_traffic(kernel, a):
+    """HBM bytes per launch of `kernel` from the committed PMC passes
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench config), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if d.get("docs") != a.docs or d.get("vocab") != a.vocab:
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None else k.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(synth, n_docs, V):

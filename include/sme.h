@@ -144,7 +144,9 @@ int sme_synth_corpus(int device, const uint8_t *vocab, const int64_t *vocab_off,
                      size_t *nbytes);
 void sme_synth_free(void *d_corpus);
 
-/* Timing of the last build, per stage, in milliseconds (device events). */
+/* Timing of the last build, per stage, in milliseconds (device events on the
+ * build stream), as a JSON object; "tok_kernel" brackets exactly the tokenizer
+ * launch and "query_kernel" (if a query batch ran) the last scoring launch. */
 int sme_last_build_profile(const sme_ctx *ctx, const char **json);
 
 #ifdef __cplusplus

@@ -382,6 +382,7 @@ int sme_last_build_profile(const sme_ctx *cx, const char **json) {
     os << "{";
     for (size_t i = 0; i < cx->last_profile.size(); i++)
       os << (i ? "," : "") << "\"" << cx->last_profile[i].first << "\":" << cx->last_profile[i].second;
+    if (cx->last_query_ms >= 0) os << (cx->last_profile.empty() ? "" : ",") << "\"query_kernel\":" << cx->last_query_ms;
     os << "}";
     const_cast<sme_ctx *>(cx)->profile_json = os.str();
     *json = cx->profile_json.c_str();

@@ -23,6 +23,7 @@ struct sme_ctx {
   uint64_t vocab_long_cap = 0, vocab_ovf_cap = 0, raw_cap_hint = 0;  // learned across builds
   std::string profile_json;
   std::vector<std::pair<std::string, float>> last_profile;
+  float last_query_ms = -1.0f;  // device time of the last query kernel launch
 };
 
 struct sme_index {

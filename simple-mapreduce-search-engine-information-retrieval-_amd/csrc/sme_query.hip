@@ -236,6 +236,11 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   const double *lut = (const double *)ix->d_lut.p;
   const double *idf = (const double *)ix->d_idf.p;
   unsigned grid = (unsigned)std::min(nq, 1 << 20);
+  // events on the launch stream bracket the scoring kernel (bench.py roofline)
+  hipEvent_t e0, e1;
+  SME_HIP(hipEventCreate(&e0));
+  SME_HIP(hipEventCreate(&e1));
+  SME_HIP(hipEventRecord(e0, st));
   if (k <= 16) {
     hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff, nq, k,
                        d_out_docno, d_out_score, err);
@@ -246,9 +251,15 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     throw Error(SME_ENOTIMPL, "top-k with k > 32 is not built yet");
   }
   SME_CHECK_LAUNCH();
+  SME_HIP(hipEventRecord(e1, st));
   int h_err = 0;
   SME_HIP(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, st));
   SME_HIP(hipStreamSynchronize(st));
+  float ms = 0;
+  SME_HIP(hipEventElapsedTime(&ms, e0, e1));
+  ix->ctx->last_query_ms = ms;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   if (h_err) throw Error(SME_ELIMIT, "a query has more than 128 terms");
 }
 

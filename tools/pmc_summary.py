@@ -1,0 +1,54 @@
+"""Per-launch HBM traffic from rocprofv3 PMC passes -> profiles/pmc_traffic.json.
+
+usage: python tools/pmc_summary.py DOCS VOCAB FETCH_DIR WRITE_DIR [KERNEL ...]
+
+FETCH_DIR / WRITE_DIR hold the run_counter_collection.csv of two separate
+`rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` runs of
+`bench.py --docs DOCS --vocab VOCAB ...` (one counter group per run: FETCH_SIZE
+takes 3 TCC slots, WRITE_SIZE 2).  Both counters are in KiB.  Per
+MI355X_MICROARCH.md (HBM section) FETCH_SIZE reports half the bytes of wide
+streaming reads on gfx950, so the fetch side is doubled; WRITE_SIZE is exact
+for 16-byte streaming stores.  Values are averaged over the kernel's dispatches
+(warm-up builds included: a build's kernels see the same bytes every step).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_kernel(d, counter):
+    out = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            out.setdefault(name, []).append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    docs, vocab, fdir, wdir = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    wanted = sys.argv[5:] or ["k_tok_fast", "k_query"]
+    fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
+    res = {"docs": docs, "vocab": vocab,
+           "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), mean over dispatches; separate --pmc passes",
+           "kernels": {}}
+    for k in wanted:
+        fk = [v for n, v in fetch.items() if k in n]
+        wk = [v for n, v in write.items() if k in n]
+        if not fk or not wk:
+            continue
+        f = sum(fk[0]) / len(fk[0]) * 1024
+        w = sum(wk[0]) / len(wk[0]) * 1024
+        res["kernels"][k] = {"fetch_bytes_raw": round(f), "write_bytes": round(w), "dispatches": len(fk[0]),
+                             "hbm_bytes_per_launch": round(2 * f + w)}
+    os.makedirs("profiles", exist_ok=True)
+    json.dump(res, open("profiles/pmc_traffic.json", "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
