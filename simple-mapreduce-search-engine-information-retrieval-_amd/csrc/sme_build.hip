@@ -26,6 +26,7 @@
 //   K8 sort by (term, tf desc)  stable -> MyReducer.reduce's output order
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <limits.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1363,6 +1364,53 @@ __global__ void k_weights(const uint32_t *key, const int32_t *tf, int64_t P, con
   }
 }
 
+// Packed 32-bit sort path (the common case): a posting's (docno, tf) fits one
+// u32 as (docno - dmin) * F + tf when (dmax - dmin + 1) * F < 2^32, F = max_tf + 1.
+__global__ void k_pair_stats(const uint64_t *val, int64_t P, unsigned int *max_tf) {
+  unsigned int m = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x)
+    m = max(m, (unsigned int)(uint32_t)val[i]);
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(max_tf, m);
+}
+__global__ void k_docno_range(const int32_t *docno, int64_t n, int *mn, int *mx) {
+  int a = INT_MAX, b = INT_MIN;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    a = min(a, docno[i]);
+    b = max(b, docno[i]);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a = min(a, __shfl_xor(a, o, 64));
+    b = max(b, __shfl_xor(b, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(mn, a);
+    atomicMax(mx, b);
+  }
+}
+__global__ void k_pack_pairs(const uint64_t *val, int64_t P, int64_t dmin, uint32_t F, uint32_t *v32) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t v = val[i];
+    v32[i] = (uint32_t)(((int64_t)(int32_t)(uint32_t)(v >> 32) - dmin) * (int64_t)F + (int64_t)(uint32_t)v);
+  }
+}
+__global__ void k_unpack_packed(const uint32_t *v32, int64_t P, int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = v32[i];
+    docno[i] = (int32_t)((int64_t)(v / F) + dmin);
+    tf[i] = (int32_t)(v % F);
+  }
+}
+__global__ void k_composite32(const uint32_t *key, const int32_t *tf, int64_t P, int tfbits, uint32_t tfmask,
+                              uint32_t *ck) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x)
+    ck[i] = (key[i] << tfbits) | (tfmask - (uint32_t)tf[i]);
+}
+__global__ void k_composite32_tf(const uint32_t *ck, int64_t P, uint32_t tfmask, int32_t *tf) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x)
+    tf[i] = (int32_t)(tfmask - (ck[i] & tfmask));
+}
+
 // idf of every term (the same expression k_weights evaluates per posting)
 __global__ void k_term_idf(const int64_t *off, int64_t V, double idf_ref, int64_t N, const int64_t *gdf,
                            const double *idf_by_df, int64_t sdf, const double *idf_by_q, int mode, double *idf) {
@@ -1921,44 +1969,87 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   // ---------------- K6 sort by term ----------------
   const int tbits = bits_for((uint64_t)std::max<int64_t>(V, 1));
   uint32_t *key_s = W[W_T0].as<uint32_t>(P + 1);
-  uint64_t *val_s = W[W_T1].as<uint64_t>(P + 1);
-  if (P > 0) {
-    size_t tbb = 0;
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, p_term, key_s, p_val, val_s, (int)P, 0, tbits, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, p_term, key_s, p_val, val_s, (int)P, 0, tbits, st));
-  }
   int64_t Pm = P;
-  if (dup_docno && P > 0) {
-    // MyReducer.reduce: equal docnos (duplicate docids) are merged by summing tf
-    uint64_t *ck = W[W_PVAL].as<uint64_t>(P), *ck2 = W[W_T2].as<uint64_t>(P);
-    int32_t *tfv = reinterpret_cast<int32_t *>(W[W_PTERM].as<uint32_t>(P)), *tf2 = W[W_T3].as<int32_t>(P);
-    hipLaunchKernelGGL(k_dup_keys, dim3(grid_for(P)), dim3(256), 0, st, key_s, val_s, P, ck, tfv);
-    int64_t *nout = reinterpret_cast<int64_t *>(cnt + 10);
-    size_t tbb = 0;
-    SME_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tbb, ck, ck2, tfv, tf2, nout, hipcub::Sum(), (int)P, st));
-    SME_HIP(hipcub::DeviceReduce::ReduceByKey(cub_tmp(tbb), tbb, ck, ck2, tfv, tf2, nout, hipcub::Sum(), (int)P, st));
-    Pm = d2h(nout, st);
-    hipLaunchKernelGGL(k_dup_unpack, dim3(grid_for(Pm)), dim3(256), 0, st, ck2, tf2, Pm, key_s, val_s);
-    ix->P = Pm;
+  int32_t max_tf = 1;
+  // packed path: u32 keys and u32 values through both sorts (no duplicate docnos)
+  bool packed = false;
+  int64_t dmin = 0;
+  uint32_t F = 0;
+  if (P > 0 && !dup_docno) {
+    unsigned int *mtf = reinterpret_cast<unsigned int *>(cnt + 11);
+    int *dmn = reinterpret_cast<int *>(cnt + 12), *dmx = dmn + 1;
+    SME_HIP(hipMemsetAsync(mtf, 0, sizeof(unsigned int), st));
+    const int h_init[2] = {INT_MAX, INT_MIN};
+    SME_HIP(hipMemcpyAsync(dmn, h_init, sizeof h_init, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_pair_stats, dim3(grid_for(P, 256, 2048)), dim3(256), 0, st, p_val, P, mtf);
+    hipLaunchKernelGGL(k_docno_range, dim3(grid_for(nR, 256, 1024)), dim3(256), 0, st, docno, nR, dmn, dmx);
+    unsigned int h_mtf = d2h(mtf, st);
+    int h_r[2];
+    SME_HIP(hipMemcpyAsync(h_r, dmn, sizeof h_r, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    const uint64_t Fq = (uint64_t)h_mtf + 1, D = (uint64_t)((int64_t)h_r[1] - (int64_t)h_r[0] + 1);
+    max_tf = std::max<int32_t>(1, (int32_t)h_mtf);
+    packed = D * Fq < (1ull << 32) && tbits + bits_for((uint64_t)max_tf) <= 32;
+    dmin = h_r[0];
+    F = (uint32_t)Fq;
   }
+  int32_t *docno_d = nullptr, *tf_d = nullptr;
+  int64_t *off = nullptr;
+  if (packed) {
+    uint32_t *v32 = reinterpret_cast<uint32_t *>(W[W_T1].as<uint64_t>(P + 1));
+    uint32_t *v32s = W[W_T2].as<uint32_t>(P + 1);
+    hipLaunchKernelGGL(k_pack_pairs, dim3(grid_for(P)), dim3(256), 0, st, p_val, P, dmin, F, v32);
+    size_t tbb = 0;
+    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, p_term, key_s, v32, v32s, (int)P, 0, tbits, st));
+    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, p_term, key_s, v32, v32s, (int)P, 0, tbits, st));
+    off = ix->d_off.as<int64_t>(V + 1);
+    SME_HIP(hipMemsetAsync(off, 0, (V + 1) * sizeof(int64_t), st));
+    hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, V);
+    docno_d = ix->d_docno_d.as<int32_t>(P + 1);
+    tf_d = ix->d_tf_d.as<int32_t>(P + 1);
+    hipLaunchKernelGGL(k_unpack_packed, dim3(grid_for(P)), dim3(256), 0, st, v32s, P, dmin, F, docno_d, tf_d);
+    SME_CHECK_LAUNCH();
+  } else {
+    uint64_t *val_s = W[W_T1].as<uint64_t>(P + 1);
+    if (P > 0) {
+      size_t tbb = 0;
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, p_term, key_s, p_val, val_s, (int)P, 0, tbits, st));
+      SME_HIP(
+          hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, p_term, key_s, p_val, val_s, (int)P, 0, tbits, st));
+    }
+    if (dup_docno && P > 0) {
+      // MyReducer.reduce: equal docnos (duplicate docids) are merged by summing tf
+      uint64_t *ck = W[W_PVAL].as<uint64_t>(P), *ck2 = W[W_T2].as<uint64_t>(P);
+      int32_t *tfv = reinterpret_cast<int32_t *>(W[W_PTERM].as<uint32_t>(P)), *tf2 = W[W_T3].as<int32_t>(P);
+      hipLaunchKernelGGL(k_dup_keys, dim3(grid_for(P)), dim3(256), 0, st, key_s, val_s, P, ck, tfv);
+      int64_t *nout = reinterpret_cast<int64_t *>(cnt + 10);
+      size_t tbb = 0;
+      SME_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tbb, ck, ck2, tfv, tf2, nout, hipcub::Sum(), (int)P, st));
+      SME_HIP(
+          hipcub::DeviceReduce::ReduceByKey(cub_tmp(tbb), tbb, ck, ck2, tfv, tf2, nout, hipcub::Sum(), (int)P, st));
+      Pm = d2h(nout, st);
+      hipLaunchKernelGGL(k_dup_unpack, dim3(grid_for(Pm)), dim3(256), 0, st, ck2, tf2, Pm, key_s, val_s);
+    }
+    off = ix->d_off.as<int64_t>(V + 1);
+    SME_HIP(hipMemsetAsync(off, 0, (V + 1) * sizeof(int64_t), st));
+    if (Pm > 0) hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(Pm)), dim3(256), 0, st, key_s, Pm, off, V);
+    docno_d = ix->d_docno_d.as<int32_t>(Pm + 1);
+    tf_d = ix->d_tf_d.as<int32_t>(Pm + 1);
+    if (Pm > 0) hipLaunchKernelGGL(k_unpack_vals, dim3(grid_for(Pm)), dim3(256), 0, st, val_s, Pm, docno_d, tf_d);
+    SME_CHECK_LAUNCH();
+    if (Pm > 0) {
+      int32_t *mx = reinterpret_cast<int32_t *>(cnt + 11);
+      size_t tbb = 0;
+      SME_HIP(hipcub::DeviceReduce::Max(nullptr, tbb, tf_d, mx, (int)Pm, st));
+      SME_HIP(hipcub::DeviceReduce::Max(cub_tmp(tbb), tbb, tf_d, mx, (int)Pm, st));
+      max_tf = std::max(1, d2h(mx, st));
+    }
+  }
+  ix->P = Pm;
   const int64_t PP = Pm;
-  int64_t *off = ix->d_off.as<int64_t>(V + 1);
-  SME_HIP(hipMemsetAsync(off, 0, (V + 1) * sizeof(int64_t), st));
-  if (PP > 0) hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(PP)), dim3(256), 0, st, key_s, PP, off, V);
-  int32_t *docno_d = ix->d_docno_d.as<int32_t>(PP + 1), *tf_d = ix->d_tf_d.as<int32_t>(PP + 1);
-  if (PP > 0) hipLaunchKernelGGL(k_unpack_vals, dim3(grid_for(PP)), dim3(256), 0, st, val_s, PP, docno_d, tf_d);
-  SME_CHECK_LAUNCH();
   prof.mark("sort_term");
 
   // ---------------- K7 weights ----------------
-  int32_t max_tf = 1;
-  if (PP > 0) {
-    int32_t *mx = reinterpret_cast<int32_t *>(cnt + 11);
-    size_t tbb = 0;
-    SME_HIP(hipcub::DeviceReduce::Max(nullptr, tbb, tf_d, mx, (int)PP, st));
-    SME_HIP(hipcub::DeviceReduce::Max(cub_tmp(tbb), tbb, tf_d, mx, (int)PP, st));
-    max_tf = std::max(1, d2h(mx, st));
-  }
   ix->max_tf = max_tf;
   {
     // LUT[tf] = 1 + ln(tf) and idf tables, evaluated once on the host with the
@@ -1994,14 +2085,27 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   int32_t *docno_o = ix->d_docno_o.as<int32_t>(PP + 1), *tf_o = ix->d_tf_o.as<int32_t>(PP + 1);
   if (PP > 0) {
     const int tfb = bits_for((uint64_t)max_tf);
-    const uint64_t tfmask = (1ull << tfb) - 1;
-    uint64_t *ck = W[W_PVAL].as<uint64_t>(PP), *ck2 = W[W_T2].as<uint64_t>(PP);
-    hipLaunchKernelGGL(k_composite, dim3(grid_for(PP)), dim3(256), 0, st, key_s, tf_d, PP, tfb, tfmask, ck);
-    size_t tbb = 0;
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, ck, ck2, docno_d, docno_o, (int)PP, 0, tbits + tfb, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, ck, ck2, docno_d, docno_o, (int)PP, 0, tbits + tfb,
-                                               st));
-    hipLaunchKernelGGL(k_composite_tf, dim3(grid_for(PP)), dim3(256), 0, st, ck2, PP, tfmask, tf_o);
+    if (tbits + tfb <= 32) {  // u32 composite (term, tf desc)
+      const uint32_t tfmask = (uint32_t)((1ull << tfb) - 1);
+      uint32_t *ck = reinterpret_cast<uint32_t *>(W[W_PVAL].as<uint64_t>(PP)), *ck2 = W[W_T2].as<uint32_t>(PP);
+      hipLaunchKernelGGL(k_composite32, dim3(grid_for(PP)), dim3(256), 0, st, key_s, tf_d, PP, tfb, tfmask, ck);
+      size_t tbb = 0;
+      SME_HIP(
+          hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, ck, ck2, docno_d, docno_o, (int)PP, 0, tbits + tfb, st));
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, ck, ck2, docno_d, docno_o, (int)PP, 0,
+                                                 tbits + tfb, st));
+      hipLaunchKernelGGL(k_composite32_tf, dim3(grid_for(PP)), dim3(256), 0, st, ck2, PP, tfmask, tf_o);
+    } else {
+      const uint64_t tfmask = (1ull << tfb) - 1;
+      uint64_t *ck = W[W_PVAL].as<uint64_t>(PP), *ck2 = W[W_T2].as<uint64_t>(PP);
+      hipLaunchKernelGGL(k_composite, dim3(grid_for(PP)), dim3(256), 0, st, key_s, tf_d, PP, tfb, tfmask, ck);
+      size_t tbb = 0;
+      SME_HIP(
+          hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, ck, ck2, docno_d, docno_o, (int)PP, 0, tbits + tfb, st));
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, ck, ck2, docno_d, docno_o, (int)PP, 0,
+                                                 tbits + tfb, st));
+      hipLaunchKernelGGL(k_composite_tf, dim3(grid_for(PP)), dim3(256), 0, st, ck2, PP, tfmask, tf_o);
+    }
     SME_CHECK_LAUNCH();
   }
   prof.mark("sort_tf");
