@@ -1281,6 +1281,95 @@ __global__ __launch_bounds__(kAggNT) void k_agg(AggIn in, int64_t nR, int32_t *p
   }
 }
 
+// Wave-per-record aggregation (the common case): each wave owns a 1024-entry
+// LDS table, so records proceed independently with no workgroup barriers.
+// Records with more than kWLimit distinct terms are flagged (-1) and handled by
+// the block-wide k_agg / global-table path.  Pairs of record i (docno order)
+// are written at pair_off[i] in 16 coalesced rounds of 64 table entries.
+constexpr int kWCap = 1024;
+constexpr int kWLimit = 768;
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ bool aggw_insert(int32_t *keys, int32_t *cnt, int32_t term, int32_t *distinct) {
+  uint32_t h = hash32((uint32_t)term) & (kWCap - 1);
+  for (int probe = 0; probe < kWCap; probe++) {
+    const int32_t old = atomicCAS(&keys[h], -1, term);
+    if (old == -1) {
+      atomicAdd(distinct, 1);
+      atomicAdd(&cnt[h], 1);
+      return true;
+    }
+    if (old == term) {
+      atomicAdd(&cnt[h], 1);
+      return true;
+    }
+    h = (h + 1) & (kWCap - 1);
+  }
+  return false;
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t *prec, const int64_t *pair_off,
+                                                  uint32_t *p_term, uint64_t *p_val) {
+  __shared__ int32_t keys_all[kAggNT / 64][kWCap];
+  __shared__ int32_t cnt_all[kAggNT / 64][kWCap];
+  __shared__ int32_t dist_all[kAggNT / 64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int32_t *keys = keys_all[wv], *cnt = cnt_all[wv];
+  int32_t *distinct = &dist_all[wv];
+  const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
+  for (int64_t i = (int64_t)blockIdx.x * (kAggNT / 64) + wv; i < nR; i += nwaves) {
+    if (EMIT && prec[i] < 0) continue;  // big record: block path
+    const int64_t r = in.perm[i];
+#pragma unroll
+    for (int k = 0; k < kWCap / 64; k++) {
+      keys[k * 64 + lane] = -1;
+      cnt[k * 64 + lane] = 0;
+    }
+    if (lane == 0) *distinct = 0;
+    wave_sync_lds();
+    const uint32_t *ts = in.tokstream + (in.rs[r] >> 1);
+    const int32_t nt = in.ntok[r];
+    bool ok = true;
+    for (int32_t t = lane; t < nt; t += 64) {
+      const uint32_t slot = ts[t];
+      const int32_t rt = in.raw_term[slot];
+      if (rt >= 0) {
+        ok &= aggw_insert(keys, cnt, rt, distinct);
+      } else if (rt <= -2) {
+        const int32_t m0 = -rt - 2, mn = in.raw_nout[slot];
+        for (int32_t m = 0; m < mn; m++) ok &= aggw_insert(keys, cnt, in.multi_term[m0 + m], distinct);
+      }
+    }
+    wave_sync_lds();
+    const int32_t d = *distinct;
+    const bool big = __any(!ok) || d > kWLimit;
+    if (!EMIT) {
+      if (lane == 0) prec[i] = big ? -1 : d;
+      wave_sync_lds();
+      continue;
+    }
+    int64_t base = pair_off[i];
+    const uint64_t dn = (uint64_t)(uint32_t)in.docno[r] << 32;
+#pragma unroll 4
+    for (int k = 0; k < kWCap / 64; k++) {
+      const int32_t key = keys[k * 64 + lane];
+      const uint64_t m = __ballot(key >= 0);
+      if (key >= 0) {
+        const int64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
+        p_term[o] = (uint32_t)key;
+        p_val[o] = dn | (uint32_t)cnt[k * 64 + lane];
+      }
+      base += __popcll(m);
+    }
+    wave_sync_lds();
+  }
+}
+
 // records with more than kAggLimit distinct terms: table in global scratch
 __global__ __launch_bounds__(kAggNT) void k_agg_big(AggIn in, const int64_t *big_list, int64_t nbig,
                                                     const int64_t *tab_off, const int64_t *tab_cap, int32_t *gkeys,
@@ -1907,9 +1996,9 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   ai.docno = docno;
   int32_t *prec = W[W_PREC].as<int32_t>(nR + 1);
   int64_t *pair_off = W[W_T3].as<int64_t>(nR + 1);  // rank_of_slot no longer needed
-  unsigned agg_grid = (unsigned)std::min<int64_t>(std::max<int64_t>(nR, 1), 65536);
+  unsigned agg_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
   if (nR > 0) {
-    hipLaunchKernelGGL(k_agg<false>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, prec, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL(k_agg_w<false>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, prec, nullptr, nullptr, nullptr);
     SME_CHECK_LAUNCH();
   }
   // big records
@@ -1956,7 +2045,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   uint64_t *p_val = W[W_PVAL].as<uint64_t>(P + 1);
   if (nR > 0) {
     // big records are flagged in prec via a negative marker: keep a copy of flags
-    hipLaunchKernelGGL(k_agg<true>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, prec, pair_off, p_term, p_val);
+    hipLaunchKernelGGL(k_agg_w<true>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, prec, pair_off, p_term, p_val);
     SME_CHECK_LAUNCH();
   }
   if (nbig > 0) {
