@@ -87,14 +87,12 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    n_tensor = torch.zeros(1, dtype=torch.int64, device="cuda")
+    D = importlib.import_module(PKG + ".dist") if dist is not None else None
 
     def step():
         ix = ctx.build_device(d_corpus.value, nbytes, stream)
-        if dist is not None:
-            n_tensor.fill_(ix.N)
-            dist.all_reduce(n_tensor)
-            ix.reweight(int(n_tensor.item()), None, stream)  # idf = log10(N_global)
+        if D is not None:
+            ix.reweight(D.global_count(ix.N), None, stream)  # idf = log10(N_global): RCCL all-reduce of N
         return ix
 
     ix = None
@@ -207,21 +205,8 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
         ix.query_topk_device(d_terms.data_ptr(), d_qoff.data_ptr(), a.queries, k, out_d.data_ptr(), out_s.data_ptr(),
                              stream)
         if dist is not None:
-            # merge per-shard top-k: all-gather (score, docno) lists, keep the best k per query
-            gs = [torch.empty_like(out_s) for _ in range(world)]
-            gd = [torch.empty_like(out_d) for _ in range(world)]
-            dist.all_gather(gs, out_s)
-            dist.all_gather(gd, out_d)
-            s = torch.cat(gs, 1)
-            d = torch.cat(gd, 1).to(torch.int64)
-            valid = d >= 0
-            s = torch.where(valid, s, torch.full_like(s, -float("inf")))
-            d = torch.where(valid, d, torch.full_like(d, 1 << 40))
-            # (score desc, docno asc): stable sort by docno, then stable sort by -score
-            i1 = torch.argsort(d, dim=1, stable=True)
-            s1, d1 = torch.gather(s, 1, i1), torch.gather(d, 1, i1)
-            i2 = torch.argsort(-s1, dim=1, stable=True)[:, :k]
-            return torch.gather(d1, 1, i2), torch.gather(s1, 1, i2)
+            # per-shard top-k lists -> global top-k (RCCL all-gather + merge, dist.merge_topk)
+            return importlib.import_module(PKG + ".dist").merge_topk(out_d, out_s, k)
         return out_d
 
     qstep()
