@@ -588,6 +588,7 @@ struct TokLds {
   int64_t tbase[kRecWin];            // tokstream offset of the record (rs >> 1)
   int32_t c0[kRecWin];
   int32_t rid[kRecWin];               // record index
+  uint64_t smask[kTokNT];             // split-byte mask of every lane's 64 bytes
   int32_t sc32[kTokNT / 64 + 1];
 };
 
@@ -697,35 +698,57 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
       j = lo - 1;
     }
     const int32_t mc = (int32_t)max<int64_t>(min<int64_t>(mask_carry - c_lo, kFar), -1);
-    // pass 1: token-start candidates and spans over this lane's 64 bytes
-    uint64_t cand = 0;
-    int32_t lane_max = -1;
-    uint8_t prev = tid > 0 ? stg[p0 - 1] : prev_chunk_byte;
-    int jj = j;
-    int32_t rs_next = jj + 1 < kRecWin ? L.rs[jj + 1] : kFar;
-    int32_t re_cur = jj >= 0 ? L.re[jj] : -1;
+    // pass 1: byte classes of this lane's 64 bytes as bit masks (bit i = byte p0 + i)
+    uint64_t S = 0, SPN = 0;  // split bytes; '<' / '&' bytes (span starters)
+#pragma unroll 1
     for (int w = 0; w < kTokWords; w++) {
       const uint64_t wlo = st8[2 * (kTokWords * tid + w)], whi = st8[2 * (kTokWords * tid + w) + 1];
-#pragma unroll 4
+      uint32_t s16 = 0, x16 = 0;
+#pragma unroll
       for (int i = 0; i < 16; i++) {
-        const int32_t p = p0 + 16 * w + i;
-        const uint8_t b = (uint8_t)((i < 8 ? wlo >> (8 * i) : whi >> (8 * (i - 8))) & 0xFF);
-        while (rs_next <= p) {
-          jj++;
-          re_cur = L.re[jj];
-          rs_next = jj + 1 < kRecWin ? L.rs[jj + 1] : kFar;
+        const uint32_t b = (uint32_t)((i < 8 ? wlo >> (8 * i) : whi >> (8 * (i - 8))) & 0xFF);
+        s16 |= (uint32_t)is_split_byte(b) << i;
+        x16 |= (uint32_t)(b == '<' || b == '&') << i;
+      }
+      S |= (uint64_t)s16 << (16 * w);
+      SPN |= (uint64_t)x16 << (16 * w);
+    }
+    L.smask[tid] = S;
+    // bytes inside a (fast-path) record: all of them unless a record boundary
+    // falls in this lane
+    uint64_t IN;
+    const bool whole = j >= 0 && L.re[j] >= p0 + kTokBytes;
+    if (whole) {
+      IN = ~0ull;
+    } else {
+      IN = 0;
+      int jj = j;
+      for (int i = 0; i < kTokBytes; i++) {
+        const int32_t p = p0 + i;
+        while (jj + 1 < kRecWin && L.rs[jj + 1] <= p) jj++;
+        if (jj >= 0 && p < L.re[jj]) IN |= 1ull << i;
+      }
+    }
+    const uint64_t prev_split = is_split_byte(tid > 0 ? stg[p0 - 1] : prev_chunk_byte) ? 1ull : 0ull;
+    uint64_t cand = IN & ~S & ((S << 1) | prev_split);
+    int32_t lane_max = -1;
+    uint64_t sp = SPN & IN;
+    if (sp) {  // rare: markup / entities in this lane
+      int jj = j;
+      while (sp) {
+        const int i = __ffsll((unsigned long long)sp) - 1;
+        sp &= sp - 1;
+        const int32_t p = p0 + i;
+        while (jj + 1 < kRecWin && L.rs[jj + 1] <= p) jj++;
+        const int32_t e = L.re[jj];
+        const int32_t q = stg[p] == '<' ? lt_span_rel(stg, t, c_lo, e, p) : amp_span_rel(stg, t, c_lo, e, p);
+        lane_max = q > lane_max ? q : lane_max;
+        // tokens may not start inside the span (p, q]
+        const int32_t hi_bit = q - p0;
+        if (hi_bit > i) {
+          const uint64_t upto = hi_bit >= 63 ? ~0ull : ((1ull << (hi_bit + 1)) - 1ull);
+          cand &= ~(upto & ~((1ull << (i + 1)) - 1ull));
         }
-        if (p < re_cur) {
-          if (!is_split_byte(b) && is_split_byte(prev) && lane_max < p) cand |= 1ull << (16 * w + i);
-          if (b == '<') {
-            const int32_t q = lt_span_rel(stg, t, c_lo, re_cur, p);
-            lane_max = q > lane_max ? q : lane_max;
-          } else if (b == '&') {
-            const int32_t q = amp_span_rel(stg, t, c_lo, re_cur, p);
-            lane_max = q > lane_max ? q : lane_max;
-          }
-        }
-        prev = b;
       }
     }
     int32_t blk_max;
@@ -755,11 +778,20 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
       TokSig g;
       int32_t len;
       if (x + 24 <= kStageV * 16) {
+        // token end: first split byte after x, from this lane's or the next lane's mask
+        const uint64_t rest = S >> i0 >> 1;  // bytes x+1 .. p0+63
+        if (rest) {
+          len = __ffsll((unsigned long long)rest);
+        } else if (tid + 1 < kTokNT && L.smask[tid + 1]) {
+          len = (kTokBytes - i0) + __ffsll((unsigned long long)L.smask[tid + 1]) - 1;
+        } else {
+          len = 16;  // long, or running past the chunk: handled below
+        }
         const int a = x >> 3, sh = (x & 7) * 8;
         const uint64_t u0 = st8[a], u1 = st8[a + 1], u2 = st8[a + 2];
         const uint64_t lo = sh ? (u0 >> sh) | (u1 << (64 - sh)) : u0;
         const uint64_t hi = sh ? (u1 >> sh) | (u2 << (64 - sh)) : u1;
-        len = first_split16(lo, hi, 1);
+        if (len >= 16) len = first_split16(lo, hi, 1);
         if (len > e - x) len = e - x;
         if (len < 16) {
           g.w0 = len >= 8 ? lo : (lo & ((1ull << (8 * len)) - 1));
