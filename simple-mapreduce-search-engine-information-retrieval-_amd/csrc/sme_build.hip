@@ -47,21 +47,22 @@ namespace sme {
 // of `tag` may start at p) iff the chain of partial prefixes ending right
 // before p has even length (each active partial prefix makes the next '<'
 // a consumed mismatch; XMLInputFormat.java:188-193 resets without re-testing).
-__device__ bool doc_tag_valid(const uint8_t *t, int64_t p, const char *tag, int tl) {
+template <typename B>
+__device__ bool doc_tag_valid(const B &t, int64_t p, const char *tag, int tl) {
   int chain = 0;
   int64_t x = p;
   for (;;) {
     int64_t q = -1;
     for (int j = 1; j < tl; j++) {
       if (x - j < 0) break;
-      if (t[x - j] == '<') {
+      if (t(x - j) == '<') {
         q = x - j;
         break;
       }
     }
     if (q < 0) break;
     bool pre = true;
-    for (int64_t k = 1; k < x - q; k++) pre &= (t[q + k] == (uint8_t)tag[k]);
+    for (int64_t k = 1; k < x - q; k++) pre &= (t(q + k) == (uint8_t)tag[k]);
     if (!pre) break;
     chain++;
     x = q;
@@ -71,31 +72,32 @@ __device__ bool doc_tag_valid(const uint8_t *t, int64_t p, const char *tag, int 
 
 // Span end (inclusive) of the markup starting at '<' p for a record known to be
 // "simple" (see lt_simple); -1 if none.
-__device__ __forceinline__ int64_t lt_span_end(const uint8_t *t, int64_t n, int64_t p) {
+template <typename B>
+__device__ __forceinline__ int64_t lt_span_end(const B &t, int64_t n, int64_t p) {
   if (p + 1 >= n) return n;
-  uint8_t c = t[p + 1];
+  uint8_t c = t(p + 1);
   if (c == '/') {
     for (int64_t i = p + 2; i < n; i++)
-      if (t[i] == '>') return i;
+      if (t(i) == '>') return i;
     return n;
   }
   if (c == '!') {
-    if (p + 3 < n && t[p + 2] == '-' && t[p + 3] == '-') {
+    if (p + 3 < n && t(p + 2) == '-' && t(p + 3) == '-') {
       for (int64_t i = p + 1; i + 2 < n; i++)
-        if (t[i] == '-' && t[i + 1] == '-' && t[i + 2] == '>') return i + 2;
+        if (t(i) == '-' && t(i + 1) == '-' && t(i + 2) == '>') return i + 2;
       return n;
     }
     for (int64_t i = p + 1; i < n; i++)
-      if (t[i] == '>') return i;
+      if (t(i) == '>') return i;
     return n;
   }
   if (c == '?') {
     for (int64_t i = p + 1; i + 1 < n; i++)
-      if (t[i] == '?' && t[i + 1] == '>') return i + 1;
+      if (t(i) == '?' && t(i + 1) == '>') return i + 1;
     return n;
   }
   for (int64_t i = p + 1; i < n; i++)
-    if (t[i] == '>') return i;
+    if (t(i) == '>') return i;
   return n;
 }
 
@@ -104,31 +106,47 @@ __device__ __forceinline__ int64_t lt_span_end(const uint8_t *t, int64_t n, int6
 // space / non-ASCII byte before the first '>' (no attribute parsing, no Zs
 // name end) and a name other than script/style (no ignore mode).
 // TagTokenizer.java:179-202 (end), 155-177 (comment, PI), 291-393 (begin).
-__device__ bool lt_simple(const uint8_t *t, int64_t n, int64_t p) {
+template <typename B>
+__device__ bool lt_simple(const B &t, int64_t n, int64_t p) {
   if (p + 1 >= n) return false;
-  uint8_t c = t[p + 1];
+  uint8_t c = t(p + 1);
   int64_t q;
   if (c == '/' || c == '!' || c == '?') {
     q = lt_span_end(t, n, p);
     if (q >= n) return false;
     for (int64_t i = p + 1; i <= q; i++)
-      if (t[i] == '<') return false;
+      if (t(i) == '<') return false;
     return true;
   }
   int64_t i = p + 1;
   for (; i < n; i++) {
-    uint8_t b = t[i];
+    uint8_t b = t(i);
     if (b == '>') break;
     if (b == ' ' || b >= 0x80 || b == '<') return false;
   }
   if (i >= n) return false;
   int64_t len = i - (p + 1);
-  auto lc = [&](int64_t k) { uint8_t b = t[p + 1 + k]; return (b >= 'A' && b <= 'Z') ? b + 32 : b; };
+  auto lc = [&](int64_t k) { uint8_t b = t(p + 1 + k); return (b >= 'A' && b <= 'Z') ? b + 32 : b; };
   if (len == 6 && lc(0) == 's' && lc(1) == 'c' && lc(2) == 'r' && lc(3) == 'i' && lc(4) == 'p' && lc(5) == 't')
     return false;
   if (len == 5 && lc(0) == 's' && lc(1) == 't' && lc(2) == 'y' && lc(3) == 'l' && lc(4) == 'e') return false;
   return true;
 }
+
+// byte accessors for the markup tests: plain global text, or an LDS stage of it
+struct GlobalBytes {
+  const uint8_t *t;
+  __device__ __forceinline__ uint8_t operator()(int64_t p) const { return t[p]; }
+};
+struct StagedBytes {
+  const uint8_t *stg;  // stage: text [base, base + len)
+  const uint8_t *t;
+  int64_t base, len;
+  __device__ __forceinline__ uint8_t operator()(int64_t p) const {
+    const int64_t o = p - base;
+    return (o >= 0 && o < len) ? stg[o] : t[p];
+  }
+};
 
 struct ScanOut {
   uint64_t *S, *E, *C;
@@ -140,7 +158,7 @@ struct ScanOut {
 // atomic per list per flush: a same-address global atomic per tag (one lane per
 // wave, ~6 tags per record) serialises at the memory side (~14 ns each).
 constexpr int kScanNT = 256;
-constexpr int kScanBuf = 1024;  // per list; one 4 KiB block step adds at most 4096 '<'
+constexpr int kScanBuf = 1024;  // per list; overflow beyond it falls back to one global atomic per tag
 
 struct ScanLds {
   uint64_t buf[3][kScanBuf];
@@ -160,12 +178,13 @@ __device__ __forceinline__ void scan_push(ScanLds &L, const ScanOut &o, int list
   }
 }
 
-__device__ __forceinline__ void scan_lt(const uint8_t *__restrict__ t, int64_t n, int64_t p, const ScanOut &o,
+template <typename B>
+__device__ __forceinline__ void scan_lt(const B &t, int64_t n, int64_t p, const ScanOut &o,
                                         ScanLds &L) {
-  if (p + 5 <= n && t[p + 1] == 'D' && t[p + 2] == 'O' && t[p + 3] == 'C' && t[p + 4] == '>') {
+  if (p + 5 <= n && t(p + 1) == 'D' && t(p + 2) == 'O' && t(p + 3) == 'C' && t(p + 4) == '>') {
     if (doc_tag_valid(t, p, "<DOC>", 5)) scan_push(L, o, 0, (uint64_t)p);
-  } else if (p + 6 <= n && t[p + 1] == '/' && t[p + 2] == 'D' && t[p + 3] == 'O' && t[p + 4] == 'C' &&
-             t[p + 5] == '>') {
+  } else if (p + 6 <= n && t(p + 1) == '/' && t(p + 2) == 'D' && t(p + 3) == 'O' && t(p + 4) == 'C' &&
+             t(p + 5) == '>') {
     if (doc_tag_valid(t, p, "</DOC>", 6)) scan_push(L, o, 1, (uint64_t)p);
   }
   if (!lt_simple(t, n, p)) scan_push(L, o, 2, (uint64_t)p);
@@ -197,40 +216,86 @@ __device__ __forceinline__ uint32_t has_lt(uint32_t w) {  // bytes equal to '<' 
   return (x - 0x01010101u) & ~x & 0x80808080u;
 }
 
-// One pass over the text with coalesced 16-byte loads: consecutive lanes read
-// consecutive 16-byte words; only words containing '<' are looked at bytewise.
-__global__ __launch_bounds__(kScanNT) void k_scan_tags(const uint8_t *__restrict__ t, int64_t n, ScanOut o) {
-  __shared__ ScanLds L;
-  if (threadIdx.x < 3) L.cnt[threadIdx.x] = 0;
+// K1a: one streaming pass over the text collects the position of every '<'
+// (coalesced 16-byte loads, 4 words per lane per step; positions buffered in LDS
+// and flushed with one global atomic per flush).
+constexpr int kLtBuf = 2048;
+struct LtLds {
+  uint64_t buf[kLtBuf];
+  unsigned cnt;
+  unsigned long long base;
+};
+
+__global__ __launch_bounds__(kScanNT) void k_scan_lt(const uint8_t *__restrict__ t, int64_t n, uint64_t *lt,
+                                                     uint64_t cap, unsigned long long *nlt) {
+  __shared__ LtLds L;
+  if (threadIdx.x == 0) L.cnt = 0;
   __syncthreads();
-  const uintptr_t mis = (uintptr_t)t & 15;
+  const int64_t mis = (int64_t)((uintptr_t)t & 15);
   const uint4 *a = reinterpret_cast<const uint4 *>(t - mis);
-  const int64_t nv = (int64_t)((n + mis + 15) >> 4);
-  const int64_t stride = (int64_t)gridDim.x * kScanNT;
-  for (int64_t v0 = blockIdx.x * (int64_t)kScanNT; v0 < nv; v0 += stride) {
-    const int64_t v = v0 + threadIdx.x;
-    if (v < nv) {
-      const uint4 q = a[v];
-      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-      uint32_t lts = 0;  // '<' bytes of the 16-byte word; examined out of the unrolled loop
+  const int64_t nv = (n + mis + 15) >> 4;
+  constexpr int kU = 4;
+  auto flush = [&]() {
+    __syncthreads();
+    const unsigned c = min(L.cnt, (unsigned)kLtBuf);
+    if (threadIdx.x == 0) L.base = c ? atomicAdd(nlt, (unsigned long long)c) : 0ull;
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < c; i += kScanNT)
+      if (L.base + i < cap) lt[L.base + i] = L.buf[i];
+    __syncthreads();
+    if (threadIdx.x == 0) L.cnt = 0;
+    __syncthreads();
+  };
+  const int64_t stride = (int64_t)gridDim.x * kScanNT * kU;
+  for (int64_t v0 = blockIdx.x * (int64_t)kScanNT * kU; v0 < nv; v0 += stride) {
+    uint4 qs[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int64_t v = v0 + u * kScanNT + threadIdx.x;
+      qs[u] = v < nv ? a[v] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int64_t v = v0 + u * kScanNT + threadIdx.x;
+      const uint32_t w[4] = {qs[u].x, qs[u].y, qs[u].z, qs[u].w};
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         if (!has_lt(w[k])) continue;
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-          if (((w[k] >> (8 * j)) & 0xFF) == '<') lts |= 1u << (4 * k + j);
-      }
-      while (lts) {
-        const int b = __ffs(lts) - 1;
-        lts &= lts - 1;
-        const int64_t p = 16 * v + b - (int64_t)mis;
-        if (p < 0 || p >= n) continue;
-        scan_lt(t, n, p, o, L);
+        for (int j = 0; j < 4; j++) {
+          if (((w[k] >> (8 * j)) & 0xFF) != '<') continue;
+          const int64_t p = 16 * v + 4 * k + j - mis;
+          if (p < 0 || p >= n) continue;
+          const unsigned i = atomicAdd(&L.cnt, 1u);
+          if (i < (unsigned)kLtBuf) {
+            L.buf[i] = (uint64_t)p;
+          } else {  // more '<' in one step than the buffer holds
+            const unsigned long long g = atomicAdd(nlt, 1ull);
+            if (g < cap) lt[g] = (uint64_t)p;
+          }
+        }
       }
     }
     __syncthreads();
+    if (L.cnt >= kLtBuf / 2) flush();  // block-uniform (read after the barrier)
+  }
+  flush();
+}
+
+// K1b: one lane per '<': <DOC> / </DOC> with the reader's reset quirk, and the
+// "simple markup" test, into the S / E / C lists
+__global__ __launch_bounds__(kScanNT) void k_tag_classify(const uint8_t *__restrict__ t, int64_t n,
+                                                          const uint64_t *lt, int64_t nlt, ScanOut o) {
+  __shared__ ScanLds L;
+  if (threadIdx.x < 3) L.cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const GlobalBytes gb{t};
+  for (int64_t i0 = blockIdx.x * (int64_t)kScanNT; i0 < nlt; i0 += (int64_t)gridDim.x * kScanNT) {
+    const int64_t i = i0 + threadIdx.x;
+    if (i < nlt) scan_lt(gb, n, (int64_t)lt[i], o, L);
+    __syncthreads();
     const bool full = L.cnt[0] >= kScanBuf / 2 || L.cnt[1] >= kScanBuf / 2 || L.cnt[2] >= kScanBuf / 2;
-    if (full) scan_flush(L, o);  // block-uniform condition (read after the barrier)
+    if (full) scan_flush(L, o);
   }
   scan_flush(L, o);
 }
@@ -1666,7 +1731,7 @@ enum {
   W_S, W_E, W_C, W_CNT, W_EOF, W_NEXTS, W_RS, W_RE, W_DOCNO, W_SLOW, W_SLOWLIST, W_SCROFF, W_U16, W_BOFF,
   W_TOK, W_NTOK, W_RKEYS, W_RREPS, W_POOL, W_CKEY, W_CSTR, W_NOUT, W_LONG, W_FKEYS, W_FREPS, W_CFINAL,
   W_VSLOT, W_KHI, W_KLO, W_VIDX, W_T0, W_T1, W_T2, W_T3, W_RAWTERM, W_MULTI, W_PERM, W_PREC, W_PTERM, W_PVAL,
-  W_MAXNOUT, W_SS, W_SE, W_SC, W_RLIST, W_RFLAG, W_POFF, W_OVFKEY, W_FREC,
+  W_MAXNOUT, W_SS, W_SE, W_SC, W_RLIST, W_RFLAG, W_POFF, W_OVFKEY, W_FREC, W_LT,
   W_NSLOTS
 };
 constexpr int kBuildWs = 64;  // build slots live at ctx->ws[64..127]
@@ -1681,7 +1746,23 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   unsigned long long *cnt = W[W_CNT].as<unsigned long long>(16);
 
   // ---------------- K1 scan ----------------
-  uint64_t capS = std::max<uint64_t>(1024, n / 512), capE = capS, capC = std::max<uint64_t>(1024, n / 4096);
+  // every '<' position, then the tag classification over that list
+  uint64_t capL = std::max<uint64_t>(cx->lt_cap_hint, std::max<uint64_t>(4096, n / 256));
+  uint64_t *ltpos = nullptr;
+  int64_t nlt = 0;
+  for (int attempt = 0;; attempt++) {
+    ltpos = W[W_LT].as<uint64_t>(capL);
+    SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_scan_lt, dim3(grid_for((int64_t)ceil_div(n, 64), 256, 4096)), dim3(kScanNT), 0, st, t,
+                       (int64_t)n, ltpos, capL, cnt + 3);
+    SME_CHECK_LAUNCH();
+    nlt = (int64_t)d2h(cnt + 3, st);
+    if ((uint64_t)nlt <= capL) break;
+    if (attempt > 2) throw Error(SME_ELIMIT, "'<' list capacity");
+    capL = (uint64_t)nlt + 1024;
+  }
+  cx->lt_cap_hint = std::max<uint64_t>(cx->lt_cap_hint, (uint64_t)nlt + (uint64_t)nlt / 8 + 1024);
+  uint64_t capS = std::max<uint64_t>(1024, (uint64_t)nlt + 1), capE = capS, capC = capS;
   unsigned long long h_cnt[3];
   for (int attempt = 0;; attempt++) {
     ScanOut so;
@@ -1692,9 +1773,10 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     so.capE = (uint32_t)std::min<uint64_t>(capE, 0xFFFFFFFFu);
     so.capC = (uint32_t)std::min<uint64_t>(capC, 0xFFFFFFFFu);
     so.cnt = cnt;
-    SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_scan_tags, dim3(grid_for((int64_t)ceil_div(n, 16), 256, 8192)), dim3(256), 0, st, t,
-                       (int64_t)n, so);
+    SME_HIP(hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), st));
+    if (nlt > 0)
+      hipLaunchKernelGGL(k_tag_classify, dim3(grid_for(nlt, 256, 8192)), dim3(kScanNT), 0, st, t, (int64_t)n, ltpos,
+                         nlt, so);
     SME_CHECK_LAUNCH();
     SME_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof h_cnt, hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
