@@ -86,7 +86,8 @@ int sme_build_index_device(sme_ctx *ctx, const void *d_corpus, size_t nbytes, vo
 void sme_index_free(sme_index *ix);
 
 /* N = records mapped (= df of the " " doc-counter key), V = distinct terms
- * (K-grams) excluding the doc counter, P = postings (distinct (term, docno)). */
+ * (K-grams when K > 1) excluding the doc counter, P = postings (distinct
+ * (term, docno)).  K > 1 needs K * ceil(log2(distinct terms)) <= 63. */
 int sme_index_stats(const sme_index *ix, uint64_t *N, uint64_t *V, uint64_t *P);
 
 /* Serialized records of reduce partition `part` in key order, framed as in a
@@ -105,7 +106,8 @@ int sme_index_csr(sme_index *ix, const int64_t **offsets, const int32_t **docno,
 int sme_index_device_arrays(sme_index *ix, const int64_t **d_offsets, const int32_t **d_docno,
                             const double **d_weight);
 
-/* Term string of term id t (modified-UTF-8 bytes as written by writeUTF). */
+/* Term string of index term t (modified-UTF-8 bytes as written by writeUTF);
+ * for K > 1 (t is a k-gram) its first element k_gram[0], the forward-index key. */
 int sme_index_term(sme_index *ix, int64_t t, const uint8_t **utf8, size_t *n);
 
 /* GalagoTokenizer.processContent on one UTF-8 string, run through the same
@@ -114,8 +116,10 @@ int sme_index_term(sme_index *ix, int64_t t, const uint8_t **utf8, size_t *n);
 int sme_tokenize(sme_ctx *ctx, const uint8_t *utf8, size_t n, uint8_t *buf, size_t cap,
                  int64_t *offs, int cap_tok, int *ntok);
 
-/* Map processed terms (UTF-8, offs delimits n terms) to term ids; -1 if absent
- * (getValue skips unknown terms silently). */
+/* Map processed terms (UTF-8, offs delimits n terms) to index term ids; -1 if
+ * absent (getValue skips unknown terms silently).  For K > 1 a term maps to the
+ * LAST k-gram (TermDF order) starting with it, as the forward index's Hashtable
+ * keeps it (IntDocVectorsForwardIndex.java:107-120). */
 int sme_lookup_terms(sme_index *ix, const uint8_t *terms, const int64_t *offs, int n,
                      int32_t *term_ids);
 

@@ -561,13 +561,28 @@ void or_index_term_postings(const or_index *ix, int t, int32_t *docno, int32_t *
 /* ------------------------------------------------------------------ */
 /* query: rank()                                                        */
 
+/* TermDF.compareTo on two index terms (TermDF.java:64-70) */
+static int term_key_cmp(const term_rec *a, const term_rec *b) {
+  int m = a->k < b->k ? a->k : b->k;
+  for (int i = 0; i < m; i++) {
+    int c = js_cmp(a->gram[i].p, a->gram[i].n, b->gram[i].p, b->gram[i].n);
+    if (c) return c;
+  }
+  return a->k - b->k;
+}
+
 static int find_term(const or_index *ix, const uint16_t *w, int n) {
-  /* IntDocVectorsForwardIndex keys the forward index by k_gram[0] (T11) */
+  /* IntDocVectorsForwardIndex keys the forward index by k_gram[0] (T11): the
+   * forward file lists every record in global TermDF order
+   * (BuildIntDocVectorsForwardIndex.java:139-153) and the ctor's Hashtable.put
+   * keeps the LAST entry per first element (IntDocVectorsForwardIndex.java:107-120). */
+  int best = -1;
   for (int t = 0; t < ix->nterms; t++) {
     const jstr *g = &ix->terms[t].gram[0];
-    if (g->n == n && (n == 0 || memcmp(g->p, w, (size_t)n * 2) == 0)) return t;
+    if (g->n == n && (n == 0 || memcmp(g->p, w, (size_t)n * 2) == 0))
+      if (best < 0 || term_key_cmp(&ix->terms[t], &ix->terms[best]) > 0) best = t;
   }
-  return -1;
+  return best;
 }
 
 typedef struct {

@@ -112,12 +112,17 @@ void u16_to_mutf8(const uint16_t *u, size_t n, std::vector<uint8_t> &o) {
 
 void ensure_host_terms(sme_index *ix) {
   if (ix->h_terms_ready) return;
-  ix->h_term_off.resize(ix->V + 1);
-  SME_HIP(hipMemcpy(ix->h_term_off.data(), ix->d_term_off.p, (ix->V + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
-  ix->h_term_chars.resize(ix->h_term_off[ix->V] + 1);
-  if (ix->h_term_off[ix->V] > 0)
-    SME_HIP(hipMemcpy(ix->h_term_chars.data(), ix->d_term_chars.p, ix->h_term_off[ix->V] * sizeof(uint16_t),
+  const int64_t Vt = ix->Vt;
+  ix->h_term_off.resize(Vt + 1);
+  SME_HIP(hipMemcpy(ix->h_term_off.data(), ix->d_term_off.p, (Vt + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+  ix->h_term_chars.resize(ix->h_term_off[Vt] + 1);
+  if (ix->h_term_off[Vt] > 0)
+    SME_HIP(hipMemcpy(ix->h_term_chars.data(), ix->d_term_chars.p, ix->h_term_off[Vt] * sizeof(uint16_t),
                       hipMemcpyDeviceToHost));
+  if (ix->K > 1 && ix->V > 0) {
+    ix->h_gram.resize((size_t)(ix->V * ix->K));
+    SME_HIP(hipMemcpy(ix->h_gram.data(), ix->d_gram.p, ix->h_gram.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  }
   ix->h_terms_ready = true;
 }
 }  // namespace
@@ -152,12 +157,17 @@ int sme_create(const sme_config *cfg, sme_ctx **out) {
   });
 }
 
-void sme_destroy(sme_ctx *cx) {
-  if (!cx) return;
+static void ctx_release(sme_ctx *cx) {
   (void)hipSetDevice(cx->device);
   (void)hipDeviceSynchronize();
   if (cx->own_stream) (void)hipStreamDestroy(cx->own_stream);
   delete cx;
+}
+
+void sme_destroy(sme_ctx *cx) {
+  if (!cx) return;
+  cx->destroyed = true;
+  if (cx->live_indexes == 0) ctx_release(cx);
 }
 
 int sme_load_docno_mapping(sme_ctx *cx, const uint8_t *m, size_t n) {
@@ -221,9 +231,11 @@ int sme_build_index(sme_ctx *cx, const uint8_t *corpus, size_t nbytes, sme_index
 
 void sme_index_free(sme_index *ix) {
   if (!ix) return;
-  (void)hipSetDevice(ix->ctx->device);
+  sme_ctx *cx = ix->ctx;
+  (void)hipSetDevice(cx->device);
   (void)hipDeviceSynchronize();
-  delete ix;
+  delete ix;  // buffers go back to the context's pool
+  if (cx->live_indexes == 0 && cx->destroyed) ctx_release(cx);
 }
 
 int sme_index_stats(const sme_index *ix, uint64_t *N, uint64_t *V, uint64_t *P) {
@@ -297,7 +309,8 @@ int sme_index_term(sme_index *ix, int64_t t, const uint8_t **utf8, size_t *n) {
     set_device(ix->ctx);
     ensure_host_terms(ix);
     ix->h_term_tmp.clear();
-    u16_to_mutf8(ix->h_term_chars.data() + ix->h_term_off[t], (size_t)(ix->h_term_off[t + 1] - ix->h_term_off[t]),
+    const int64_t c = ix->K > 1 ? (int64_t)ix->h_gram[(size_t)(t * ix->K)] : t;  // k_gram[0] of a k-gram
+    u16_to_mutf8(ix->h_term_chars.data() + ix->h_term_off[c], (size_t)(ix->h_term_off[c + 1] - ix->h_term_off[c]),
                  ix->h_term_tmp);
     *utf8 = ix->h_term_tmp.data();
     *n = ix->h_term_tmp.size();

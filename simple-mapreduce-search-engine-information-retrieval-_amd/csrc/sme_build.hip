@@ -32,6 +32,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <memory>
 #include <chrono>
 
 #include "sme_internal.hpp"
@@ -326,7 +327,9 @@ __global__ void k_chain(const uint64_t *S, int64_t nS, const uint64_t *E, int64_
     atomicAdd(bad + 2, 1ull);
     int64_t ns = lower_bound_u64(S, nS, E[e] + 6);
     next_s[i] = ns;
-    if (ns != i + 1 && ns < nS) atomicAdd(bad, 1ull);
+    // a start tag inside record i (nested <DOC>) or past the last end tag breaks
+    // "records = the start tags that have an end tag": walk the chain instead
+    if (ns != i + 1 && i + 1 < nS) atomicAdd(bad, 1ull);
   }
 }
 
@@ -1676,6 +1679,164 @@ __global__ void k_pair_counts(const int32_t *prec, const int32_t *bcount, int64_
 }
 
 // ============================================================================
+// K >= 2: term k-grams (TermKGramDocIndexer.java:138-159)
+// ============================================================================
+// A record's term stream is its raw tokens expanded to term ids in order (a raw
+// token gives 0..n terms, T13).  Every window of K consecutive terms is a
+// k-gram; packed MSB-first with tb bits per term id into a u64, numeric key
+// order IS TermDF.compareTo order (element-wise String.compareTo on equal-length
+// arrays; term ids are ranks in that order).  Requires K * tb <= 63.
+constexpr int kGCap = 1024;
+constexpr int kGLimit = 768;
+
+__device__ __forceinline__ int32_t nterms_of(const AggIn &in, uint32_t slot) {
+  const int32_t rt = in.raw_term[slot];
+  return rt >= 0 ? 1 : (rt <= -2 ? in.raw_nout[slot] : 0);
+}
+
+// term-stream length of every record (docno order i)
+__global__ __launch_bounds__(kAggNT) void k_tcount(AggIn in, int64_t nR, int64_t *tcnt) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
+  for (int64_t i = (int64_t)blockIdx.x * (kAggNT / 64) + wv; i < nR; i += nwaves) {
+    const int64_t r = in.perm[i];
+    const uint32_t *ts = in.tokstream + (in.rs[r] >> 1);
+    const int32_t nt = in.ntok[r];
+    int64_t c = 0;
+    for (int32_t t = lane; t < nt; t += 64) c += nterms_of(in, ts[t]);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) tcnt[i] = c;
+  }
+}
+
+// the term stream itself, in token order
+__global__ __launch_bounds__(kAggNT) void k_twrite(AggIn in, int64_t nR, const int64_t *toff, int32_t *tstream) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
+  for (int64_t i = (int64_t)blockIdx.x * (kAggNT / 64) + wv; i < nR; i += nwaves) {
+    const int64_t r = in.perm[i];
+    const uint32_t *ts = in.tokstream + (in.rs[r] >> 1);
+    const int32_t nt = in.ntok[r];
+    int64_t o = toff[i];
+    for (int32_t t0 = 0; t0 < nt; t0 += 64) {
+      const int32_t t = t0 + lane;
+      const uint32_t slot = t < nt ? ts[t] : 0u;
+      const int32_t c = t < nt ? nterms_of(in, slot) : 0;
+      const int32_t inc = wave_incl_sum(c);
+      const int64_t at = o + inc - c;
+      if (c == 1 && in.raw_term[slot] >= 0) {
+        tstream[at] = in.raw_term[slot];
+      } else if (c > 0) {
+        const int32_t m0 = -in.raw_term[slot] - 2;
+        for (int32_t m = 0; m < c; m++) tstream[at + m] = in.multi_term[m0 + m];
+      }
+      o += __shfl(inc, 63, 64);
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t gram_key(const int32_t *ts, int K, int tb) {
+  uint64_t k = 0;
+  for (int j = 0; j < K; j++) k = (k << tb) | (uint64_t)(uint32_t)ts[j];
+  return k;
+}
+
+__device__ __forceinline__ bool gram_insert(uint64_t *keys, int32_t *cnt, uint64_t key, int32_t *distinct) {
+  uint32_t h = (uint32_t)fmix64(key) & (kGCap - 1);
+  for (int probe = 0; probe < kGCap; probe++) {
+    const unsigned long long old = atomicCAS((unsigned long long *)&keys[h], ~0ull, (unsigned long long)key);
+    if (old == ~0ull) {
+      atomicAdd(distinct, 1);
+      atomicAdd(&cnt[h], 1);
+      return true;
+    }
+    if (old == key) {
+      atomicAdd(&cnt[h], 1);
+      return true;
+    }
+    h = (h + 1) & (kGCap - 1);
+  }
+  return false;
+}
+
+// per record (wave): k-gram tf in an LDS table.  Records with more than kGLimit
+// distinct grams emit one (gram, docno, 1) pair per occurrence instead (flag
+// big[i]); the reducer-style merge of equal (gram, docno) sums them afterwards.
+template <bool EMIT>
+__global__ __launch_bounds__(kAggNT) void k_gram_agg(const int32_t *tstream, const int64_t *toff, int64_t nR,
+                                                     const int64_t *perm, const int32_t *docno_r, int K, int tb,
+                                                     int64_t *pcount, uint8_t *big, const int64_t *pair_off,
+                                                     uint64_t *pkey, uint64_t *pval) {
+  __shared__ uint64_t keys_all[kAggNT / 64][kGCap];
+  __shared__ int32_t cnt_all[kAggNT / 64][kGCap];
+  __shared__ int32_t dist_all[kAggNT / 64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint64_t *keys = keys_all[wv];
+  int32_t *cnt = cnt_all[wv];
+  int32_t *distinct = &dist_all[wv];
+  const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
+  for (int64_t i = (int64_t)blockIdx.x * (kAggNT / 64) + wv; i < nR; i += nwaves) {
+    const int32_t *ts = tstream + toff[i];
+    const int64_t m = toff[i + 1] - toff[i];
+    const int64_t ng = m >= K ? m - K + 1 : 0;
+    const uint64_t dn = (uint64_t)(uint32_t)docno_r[perm[i]] << 32;
+    if (EMIT && big[i]) {
+      for (int64_t j = lane; j < ng; j += 64) {
+        pkey[pair_off[i] + j] = gram_key(ts + j, K, tb);
+        pval[pair_off[i] + j] = dn | 1u;
+      }
+      continue;
+    }
+    for (int k = lane; k < kGCap; k += 64) {
+      keys[k] = ~0ull;
+      cnt[k] = 0;
+    }
+    if (lane == 0) *distinct = 0;
+    wave_sync_lds();
+    bool ok = true;
+    for (int64_t j = lane; j < ng; j += 64) ok &= gram_insert(keys, cnt, gram_key(ts + j, K, tb), distinct);
+    wave_sync_lds();
+    const int32_t d = *distinct;
+    const bool isbig = __any(!ok) || d > kGLimit;
+    if (!EMIT) {
+      if (lane == 0) {
+        pcount[i] = isbig ? ng : d;
+        big[i] = isbig;
+      }
+      wave_sync_lds();
+      continue;
+    }
+    int64_t base = pair_off[i];
+    for (int k = 0; k < kGCap / 64; k++) {
+      const uint64_t key = keys[k * 64 + lane];
+      const uint64_t mb = __ballot(key != ~0ull);
+      if (key != ~0ull) {
+        const int64_t o = base + __popcll(mb & ((1ull << lane) - 1ull));
+        pkey[o] = key;
+        pval[o] = dn | (uint32_t)cnt[k * 64 + lane];
+      }
+      base += __popcll(mb);
+    }
+    wave_sync_lds();
+  }
+}
+
+__global__ void k_gram_flags(const uint64_t *k, int64_t P, uint32_t *f) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x)
+    f[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+}
+// gram id per pair (inclusive scan - 1) and the components of every gram
+__global__ void k_gram_ids(const uint64_t *k, const uint32_t *incl, int64_t P, int K, int tb, uint32_t *gid,
+                           int32_t *gcomp) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = incl[i] - 1;
+    gid[i] = g;
+    if (i == 0 || k[i] != k[i - 1])
+      for (int j = 0; j < K; j++) gcomp[(int64_t)g * K + j] = (int32_t)((k[i] >> (tb * (K - 1 - j))) & ((1ull << tb) - 1));
+  }
+}
+
+// ============================================================================
 // host orchestration
 // ============================================================================
 struct Prof {
@@ -1739,7 +1900,6 @@ static_assert(W_NSLOTS <= 64, "too many build workspace slots");
 
 sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st) {
   if (!cx->has_map) throw Error(SME_ENOMAP, "no docno mapping loaded (sme_load_docno_mapping)");
-  if (cx->cfg.k != 1) throw Error(SME_ENOTIMPL, "K > 1 term k-gram indexes are not built on the device yet");
   DevBuf *W = cx->ws + kBuildWs;
   Prof prof(st);
   auto cub_tmp = [&](size_t bytes) { return cx->cub_tmp.get(bytes); };
@@ -2034,6 +2194,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   const int term_maxlen = (int)(int32_t)(uint32_t)hv[12];
 
   sme_index *ix = new sme_index(cx);
+  std::unique_ptr<sme_index> ix_guard(ix);  // freed (back to the pool) if a later stage throws
   ix->K = cx->cfg.k;
   ix->R = cx->cfg.num_partitions;
   ix->idf_mode = cx->cfg.idf_mode;
@@ -2099,6 +2260,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   prof.mark("vocabulary");
 
   // ---------------- K5 aggregation ----------------
+  const int K = cx->cfg.k;
+  int64_t Vi = V;  // index "terms": terms for K = 1, distinct k-grams for K >= 2
   AggIn ai;
   ai.rs = rs;
   ai.tokstream = tok;
@@ -2108,6 +2271,10 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   ai.multi_term = multi;
   ai.perm = perm;
   ai.docno = docno;
+  int64_t P = 0;
+  uint32_t *p_term = nullptr;
+  uint64_t *p_val = nullptr;
+  if (K == 1) {
   int32_t *prec = W[W_PREC].as<int32_t>(nR + 1);
   int64_t *pair_off = W[W_T3].as<int64_t>(nR + 1);  // rank_of_slot no longer needed
   unsigned agg_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
@@ -2153,10 +2320,10 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, prec64, pair_off, (int)nR + 1, st));
     SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, prec64, pair_off, (int)nR + 1, st));
   }
-  const int64_t P = d2h(pair_off + nR, st);
+  P = d2h(pair_off + nR, st);
   ix->P = P;
-  uint32_t *p_term = W[W_PTERM].as<uint32_t>(P + 1);
-  uint64_t *p_val = W[W_PVAL].as<uint64_t>(P + 1);
+  p_term = W[W_PTERM].as<uint32_t>(P + 1);
+  p_val = W[W_PVAL].as<uint64_t>(P + 1);
   if (nR > 0) {
     // big records are flagged in prec via a negative marker: keep a copy of flags
     hipLaunchKernelGGL(k_agg_w<true>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, prec, pair_off, p_term, p_val);
@@ -2167,10 +2334,66 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
                        nbig, boff, bcap, gkeys, gcnt, bcount, pair_off, p_term, p_val, 1);
     SME_CHECK_LAUNCH();
   }
+  } else {
+    // K >= 2: term streams, k-gram pairs per record, gram ids in TermDF order
+    const int tb = bits_for((uint64_t)std::max<int64_t>(V, 1));
+    if ((int64_t)K * tb > 63)
+      throw Error(SME_ENOTIMPL, "K * ceil(log2(V)) > 63: k-gram keys do not fit 64 bits");
+    const unsigned g_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
+    int64_t *tcnt = W[W_T2].as<int64_t>(nR + 1), *toff = W[W_T3].as<int64_t>(nR + 1);
+    if (nR > 0) hipLaunchKernelGGL(k_tcount, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, tcnt);
+    SME_HIP(hipMemsetAsync(tcnt + nR, 0, sizeof(int64_t), st));
+    size_t tbb = 0;
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, tcnt, toff, (int)nR + 1, st));
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, tcnt, toff, (int)nR + 1, st));
+    const int64_t M = d2h(toff + nR, st);
+    int32_t *tstream = W[W_U16].as<int32_t>(M + 1);
+    if (nR > 0) hipLaunchKernelGGL(k_twrite, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, toff, tstream);
+    int64_t *pcount = W[W_T1].as<int64_t>(nR + 1), *pair_off = W[W_T0].as<int64_t>(nR + 1);
+    uint8_t *bigf = W[W_SLOW].as<uint8_t>(nR + 1);
+    if (nR > 0)
+      hipLaunchKernelGGL(k_gram_agg<false>, dim3(g_grid), dim3(kAggNT), 0, st, tstream, toff, nR, perm, docno, K, tb,
+                         pcount, bigf, nullptr, nullptr, nullptr);
+    SME_HIP(hipMemsetAsync(pcount + nR, 0, sizeof(int64_t), st));
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, pcount, pair_off, (int)nR + 1, st));
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, pcount, pair_off, (int)nR + 1, st));
+    const int64_t Pg = d2h(pair_off + nR, st);
+    uint64_t *pkey = W[W_KHI].as<uint64_t>(Pg + 1), *pval0 = W[W_KLO].as<uint64_t>(Pg + 1);
+    if (nR > 0)
+      hipLaunchKernelGGL(k_gram_agg<true>, dim3(g_grid), dim3(kAggNT), 0, st, tstream, toff, nR, perm, docno, K, tb,
+                         pcount, bigf, pair_off, pkey, pval0);
+    SME_CHECK_LAUNCH();
+    // sort pairs by gram key (stable: docno order within a gram)
+    uint64_t *pkey_s = W[W_CKEY].as<uint64_t>(Pg + 1);
+    p_val = W[W_PVAL].as<uint64_t>(Pg + 1);
+    if (Pg > 0) {
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, pkey, pkey_s, pval0, p_val, (int)Pg, 0, K * tb, st));
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, pkey, pkey_s, pval0, p_val, (int)Pg, 0, K * tb,
+                                                 st));
+    }
+    uint32_t *gflag = W[W_VSLOT].as<uint32_t>(Pg + 1), *gincl = W[W_VIDX].as<uint32_t>(Pg + 1);
+    p_term = W[W_PTERM].as<uint32_t>(Pg + 1);
+    int64_t Vg = 0;
+    if (Pg > 0) {
+      hipLaunchKernelGGL(k_gram_flags, dim3(grid_for(Pg)), dim3(256), 0, st, pkey_s, Pg, gflag);
+      SME_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tbb, gflag, gincl, (int)Pg, st));
+      SME_HIP(hipcub::DeviceScan::InclusiveSum(cub_tmp(tbb), tbb, gflag, gincl, (int)Pg, st));
+      Vg = (int64_t)d2h(gincl + Pg - 1, st);
+      int32_t *gcomp = ix->d_gram.as<int32_t>(Vg * K + 1);
+      hipLaunchKernelGGL(k_gram_ids, dim3(grid_for(Pg)), dim3(256), 0, st, pkey_s, gincl, Pg, K, tb, p_term, gcomp);
+      SME_CHECK_LAUNCH();
+    } else {
+      ix->d_gram.get(16);
+    }
+    P = Pg;
+    Vi = Vg;
+    ix->P = P;
+    dup_docno = true;  // occurrences of big records and equal docnos merge in the reducer step
+  }
   prof.mark("aggregate");
 
   // ---------------- K6 sort by term ----------------
-  const int tbits = bits_for((uint64_t)std::max<int64_t>(V, 1));
+  const int tbits = bits_for((uint64_t)std::max<int64_t>(Vi, 1));
   uint32_t *key_s = W[W_T0].as<uint32_t>(P + 1);
   int64_t Pm = P;
   int32_t max_tf = 1;
@@ -2178,7 +2401,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   bool packed = false;
   int64_t dmin = 0;
   uint32_t F = 0;
-  if (P > 0 && !dup_docno) {
+  if (P > 0 && !dup_docno && K == 1) {
     unsigned int *mtf = reinterpret_cast<unsigned int *>(cnt + 11);
     int *dmn = reinterpret_cast<int *>(cnt + 12), *dmx = dmn + 1;
     SME_HIP(hipMemsetAsync(mtf, 0, sizeof(unsigned int), st));
@@ -2205,9 +2428,9 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     size_t tbb = 0;
     SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, p_term, key_s, v32, v32s, (int)P, 0, tbits, st));
     SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, p_term, key_s, v32, v32s, (int)P, 0, tbits, st));
-    off = ix->d_off.as<int64_t>(V + 1);
-    SME_HIP(hipMemsetAsync(off, 0, (V + 1) * sizeof(int64_t), st));
-    hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, V);
+    off = ix->d_off.as<int64_t>(Vi + 1);
+    SME_HIP(hipMemsetAsync(off, 0, (Vi + 1) * sizeof(int64_t), st));
+    hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, Vi);
     docno_d = ix->d_docno_d.as<int32_t>(P + 1);
     tf_d = ix->d_tf_d.as<int32_t>(P + 1);
     hipLaunchKernelGGL(k_unpack_packed, dim3(grid_for(P)), dim3(256), 0, st, v32s, P, dmin, F, docno_d, tf_d);
@@ -2233,9 +2456,9 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       Pm = d2h(nout, st);
       hipLaunchKernelGGL(k_dup_unpack, dim3(grid_for(Pm)), dim3(256), 0, st, ck2, tf2, Pm, key_s, val_s);
     }
-    off = ix->d_off.as<int64_t>(V + 1);
-    SME_HIP(hipMemsetAsync(off, 0, (V + 1) * sizeof(int64_t), st));
-    if (Pm > 0) hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(Pm)), dim3(256), 0, st, key_s, Pm, off, V);
+    off = ix->d_off.as<int64_t>(Vi + 1);
+    SME_HIP(hipMemsetAsync(off, 0, (Vi + 1) * sizeof(int64_t), st));
+    if (Pm > 0) hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(Pm)), dim3(256), 0, st, key_s, Pm, off, Vi);
     docno_d = ix->d_docno_d.as<int32_t>(Pm + 1);
     tf_d = ix->d_tf_d.as<int32_t>(Pm + 1);
     if (Pm > 0) hipLaunchKernelGGL(k_unpack_vals, dim3(grid_for(Pm)), dim3(256), 0, st, val_s, Pm, docno_d, tf_d);
@@ -2271,9 +2494,9 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     double *d_byq = d_bydf + by_df.size();
     SME_HIP(hipMemcpyAsync(d_bydf, by_df.data(), by_df.size() * sizeof(double), hipMemcpyHostToDevice, st));
     SME_HIP(hipMemcpyAsync(d_byq, by_q.data(), by_q.size() * sizeof(double), hipMemcpyHostToDevice, st));
-    double *idf = ix->d_idf.as<double>(V + 1);
-    if (V > 0)
-      hipLaunchKernelGGL(k_term_idf, dim3(grid_for(V)), dim3(256), 0, st, off, V, idf_ref, Nn, nullptr, d_bydf, sdf,
+    double *idf = ix->d_idf.as<double>(Vi + 1);
+    if (Vi > 0)
+      hipLaunchKernelGGL(k_term_idf, dim3(grid_for(Vi)), dim3(256), 0, st, off, Vi, idf_ref, Nn, nullptr, d_bydf, sdf,
                          d_byq, ix->idf_mode, idf);
     double *w = ix->d_w.as<double>(PP + 1);
     if (PP > 0)
@@ -2317,7 +2540,10 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   int32_t *rdn = ix->d_rec_docno.as<int32_t>(nR + 1);
   if (nR > 0) SME_HIP(hipMemcpyAsync(rdn, docno, nR * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
   prof.mark("finalize");
+  ix->V = Vi;
+  ix->Vt = V;
   ix->profile = prof.finish();
+  ix_guard.release();
   return ix;
 }
 

@@ -24,12 +24,17 @@ struct sme_ctx {
   std::string profile_json;
   std::vector<std::pair<std::string, float>> last_profile;
   float last_query_ms = -1.0f;  // device time of the last query kernel launch
+  // indexes borrow the context (its pool, workspace, stream): sme_destroy defers
+  // the delete until the last index is freed, whatever order a host frees them in
+  int live_indexes = 0;
+  bool destroyed = false;
 };
 
 struct sme_index {
   sme_ctx *ctx = nullptr;
   int K = 1, R = 1, idf_mode = 0;
   int64_t N = 0, V = 0, P = 0;
+  int64_t Vt = 0;  // term vocabulary size (V counts k-grams when K > 1)
   int32_t max_tf = 0;
   // sorted vocabulary (rank order): UTF-16 units
   sme::DevBuf d_term_off;    // int64 [V+1]
@@ -40,6 +45,7 @@ struct sme_index {
   sme::DevBuf d_tf_d;     // int32 [P]
   sme::DevBuf d_w;        // double [P]
   sme::DevBuf d_idf;      // double [V]   idf of every term (query side: w = lut[tf] * idf)
+  sme::DevBuf d_gram;     // int32 [V * K]  term ids of every k-gram (K > 1)
   sme::DevBuf d_lut;      // double [max_tf + 1]  1 + ln(tf)
   // reduce-output CSR: (tf desc, docno asc) per term (MyReducer.reduce order)
   sme::DevBuf d_docno_o;  // int32 [P]
@@ -58,12 +64,15 @@ struct sme_index {
   bool h_csr_ready = false;
   std::vector<int64_t> h_term_off;
   std::vector<uint16_t> h_term_chars;
+  std::vector<int32_t> h_gram;
   std::vector<uint8_t> h_term_tmp;
   bool h_terms_ready = false;
   // stage timings of the build that produced this index (ms)
   std::vector<std::pair<std::string, float>> profile;
+  ~sme_index() { ctx->live_indexes--; }  // members (pooled buffers) are released after this body
   explicit sme_index(sme_ctx *c) : ctx(c) {
-    for (sme::DevBuf *b : {&d_term_off, &d_term_chars, &d_off, &d_docno_d, &d_tf_d, &d_w, &d_idf, &d_lut, &d_docno_o,
+    c->live_indexes++;
+    for (sme::DevBuf *b : {&d_term_off, &d_term_chars, &d_off, &d_docno_d, &d_tf_d, &d_w, &d_idf, &d_lut, &d_gram, &d_docno_o,
                            &d_tf_o, &d_rec_docno, &d_ser})
       b->pool = &c->pool;
   }

@@ -358,6 +358,25 @@ __global__ void k_lookup(const int64_t *toff, const uint16_t *tchars, int64_t V,
   }
 }
 
+// K > 1: the forward index is keyed by k_gram[0] and its Hashtable keeps the
+// LAST k-gram (TermDF order) with that first element (IntDocVectorsForwardIndex
+// .java:107-120, T11): the last gram whose first component is the term id.
+__global__ void k_gram_last(const int32_t *gram, int64_t V, int K, int n, int32_t *ids) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int32_t t = ids[i];
+    if (t < 0) continue;
+    int64_t lo = 0, hi = V;  // first gram with first component > t
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (gram[m * K] <= t)
+        lo = m + 1;
+      else
+        hi = m;
+    }
+    ids[i] = (lo > 0 && gram[(lo - 1) * K] == t) ? (int32_t)(lo - 1) : -1;
+  }
+}
+
 void lookup_terms(sme_index *ix, const std::vector<std::vector<uint16_t>> &terms, int32_t *ids, hipStream_t st) {
   const int n = (int)terms.size();
   if (n == 0) return;
@@ -372,7 +391,10 @@ void lookup_terms(sme_index *ix, const std::vector<std::vector<uint16_t>> &terms
   SME_HIP(hipMemcpyAsync(d_qo, qo.data(), qo.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
   SME_HIP(hipMemcpyAsync(d_qc, qc.data(), qc.size() * sizeof(uint16_t), hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_lookup, dim3((n + 255) / 256), dim3(256), 0, st, (const int64_t *)ix->d_term_off.p,
-                     (const uint16_t *)ix->d_term_chars.p, ix->V, d_qo, d_qc, n, d_ids);
+                     (const uint16_t *)ix->d_term_chars.p, ix->Vt, d_qo, d_qc, n, d_ids);
+  if (ix->K > 1)
+    hipLaunchKernelGGL(k_gram_last, dim3((n + 255) / 256), dim3(256), 0, st, (const int32_t *)ix->d_gram.p, ix->V,
+                       ix->K, n, d_ids);
   SME_CHECK_LAUNCH();
   SME_HIP(hipMemcpyAsync(ids, d_ids, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
   SME_HIP(hipStreamSynchronize(st));

@@ -30,22 +30,32 @@ __device__ __forceinline__ void put_be32(uint8_t *p, uint32_t v) {
   p[3] = (uint8_t)v;
 }
 
-__global__ void k_ser_sizes(const int64_t *toff, const uint16_t *tch, const int64_t *off, int64_t V, int R,
-                            int64_t *rec_bytes, uint32_t *part, uint32_t *idx, unsigned long long *psum) {
+// index term t has K components: the term ids gram[t*K ..] for K > 1, or t itself
+__device__ __forceinline__ int64_t comp_of(const int32_t *gram, int K, int64_t t, int j) {
+  return gram ? (int64_t)gram[t * K + j] : t;
+}
+
+__global__ void k_ser_sizes(const int64_t *toff, const uint16_t *tch, const int32_t *gram, int K, const int64_t *off,
+                            int64_t V, int R, int64_t *rec_bytes, uint32_t *part, uint32_t *idx,
+                            unsigned long long *psum) {
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
-    const uint16_t *u = tch + toff[t];
-    const int64_t l = toff[t + 1] - toff[t];
     int64_t ul = 0;
-    uint32_t h = 0;
-    for (int64_t i = 0; i < l; i++) {
-      ul += mutf8_unit_len(u[i]);
-      h = 31u * h + u[i];
+    uint32_t ah = 1u;  // Arrays.hashCode: 31 * h + String.hashCode per element, seed 1
+    for (int j = 0; j < K; j++) {
+      const int64_t c = comp_of(gram, K, t, j);
+      const uint16_t *u = tch + toff[c];
+      const int64_t l = toff[c + 1] - toff[c];
+      uint32_t h = 0;
+      for (int64_t i = 0; i < l; i++) {
+        ul += mutf8_unit_len(u[i]);
+        h = 31u * h + u[i];
+      }
+      ah = 31u * ah + h;
     }
     const int64_t df = off[t + 1] - off[t];
-    const int64_t key = 4 + 2 + ul + 4;
+    const int64_t key = 4 + 2 * (int64_t)K + ul + 4;
     const int64_t val = 4 + (df > 0 ? 2 + kClassLen + 8 * df : 0);
     rec_bytes[t] = 8 + key + val;
-    const uint32_t ah = 31u * 1u + h;  // Arrays.hashCode: 31 * 1 + hash(k_gram[0])
     const uint32_t p = (uint32_t)((int32_t)(ah & 0x7fffffffu) % R);
     part[t] = p;
     idx[t] = (uint32_t)t;
@@ -61,38 +71,48 @@ __global__ void k_ser_offsets(const uint32_t *grp_term, const int64_t *scan, int
   }
 }
 
-// one wave per term
-__global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int64_t *off, const int32_t *docno_o,
-                            const int32_t *tf_o, int64_t V, const int64_t *rec_off, uint8_t *out) {
+// one wave per index term
+__global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int32_t *gram, int K, const int64_t *off,
+                            const int32_t *docno_o, const int32_t *tf_o, int64_t V, const int64_t *rec_off,
+                            uint8_t *out) {
   const int lane = threadIdx.x & 63;
   const int64_t wpb = blockDim.x / 64;
   for (int64_t t = blockIdx.x * wpb + (threadIdx.x >> 6); t < V; t += (int64_t)gridDim.x * wpb) {
-    const uint16_t *u = tch + toff[t];
-    const int64_t l = toff[t + 1] - toff[t];
     const int64_t p0 = off[t], df = off[t + 1] - off[t];
     uint8_t *o = out + rec_off[t];
     int64_t ul = 0;
-    for (int64_t i = 0; i < l; i++) ul += mutf8_unit_len(u[i]);
-    const int64_t key = 10 + ul, val = 4 + (df > 0 ? 2 + kClassLen + 8 * df : 0);
+    for (int j = 0; j < K; j++) {
+      const int64_t c = comp_of(gram, K, t, j);
+      for (int64_t i = toff[c]; i < toff[c + 1]; i++) ul += mutf8_unit_len(tch[i]);
+    }
+    const int64_t key = 4 + 2 * (int64_t)K + ul + 4, val = 4 + (df > 0 ? 2 + kClassLen + 8 * df : 0);
     uint8_t *post = o + 8 + key + 4 + 2 + kClassLen;
     if (lane == 0) {
       put_be32(o, (uint32_t)(key + val));
       put_be32(o + 4, (uint32_t)key);
-      put_be32(o + 8, 1u);
-      o[12] = (uint8_t)(ul >> 8);
-      o[13] = (uint8_t)ul;
-      uint8_t *q = o + 14;
-      for (int64_t i = 0; i < l; i++) {
-        uint16_t c = u[i];
-        if (c >= 1 && c <= 0x7F) {
-          *q++ = (uint8_t)c;
-        } else if (c > 0x7FF) {
-          *q++ = (uint8_t)(0xE0 | ((c >> 12) & 0x0F));
-          *q++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
-          *q++ = (uint8_t)(0x80 | (c & 0x3F));
-        } else {
-          *q++ = (uint8_t)(0xC0 | ((c >> 6) & 0x1F));
-          *q++ = (uint8_t)(0x80 | (c & 0x3F));
+      put_be32(o + 8, (uint32_t)K);
+      uint8_t *q = o + 12;
+      for (int j = 0; j < K; j++) {  // writeUTF per element
+        const int64_t c = comp_of(gram, K, t, j);
+        const uint16_t *u = tch + toff[c];
+        const int64_t l = toff[c + 1] - toff[c];
+        int64_t el = 0;
+        for (int64_t i = 0; i < l; i++) el += mutf8_unit_len(u[i]);
+        q[0] = (uint8_t)(el >> 8);
+        q[1] = (uint8_t)el;
+        q += 2;
+        for (int64_t i = 0; i < l; i++) {
+          uint16_t ch = u[i];
+          if (ch >= 1 && ch <= 0x7F) {
+            *q++ = (uint8_t)ch;
+          } else if (ch > 0x7FF) {
+            *q++ = (uint8_t)(0xE0 | ((ch >> 12) & 0x0F));
+            *q++ = (uint8_t)(0x80 | ((ch >> 6) & 0x3F));
+            *q++ = (uint8_t)(0x80 | (ch & 0x3F));
+          } else {
+            *q++ = (uint8_t)(0xC0 | ((ch >> 6) & 0x1F));
+            *q++ = (uint8_t)(0x80 | (ch & 0x3F));
+          }
         }
       }
       put_be32(q, 1u);  // stored df of a real term (T1)
@@ -144,6 +164,7 @@ void serialize_index(sme_index *ix, hipStream_t st) {
   auto &W = ix->ctx->ws;
   const int64_t V = ix->V, N = ix->N;
   const int R = ix->R;
+  const int32_t *gram = ix->K > 1 ? (const int32_t *)ix->d_gram.p : nullptr;
   int64_t *rec_bytes = W[48].as<int64_t>(V + 1);
   uint32_t *part = W[49].as<uint32_t>(V + 1), *idx = W[50].as<uint32_t>(V + 1);
   uint32_t *part2 = W[51].as<uint32_t>(V + 1), *idx2 = W[52].as<uint32_t>(V + 1);
@@ -153,8 +174,8 @@ void serialize_index(sme_index *ix, hipStream_t st) {
   const int G = (int)std::min<int64_t>(std::max<int64_t>((V + 255) / 256, 1), 8192);
   if (V > 0)
     hipLaunchKernelGGL(k_ser_sizes, dim3(G), dim3(256), 0, st, (const int64_t *)ix->d_term_off.p,
-                       (const uint16_t *)ix->d_term_chars.p, (const int64_t *)ix->d_off.p, V, R, rec_bytes, part, idx,
-                       psum);
+                       (const uint16_t *)ix->d_term_chars.p, gram, ix->K, (const int64_t *)ix->d_off.p, V, R, rec_bytes,
+                       part, idx, psum);
   SME_CHECK_LAUNCH();
   std::vector<unsigned long long> hps(R + 1);
   SME_HIP(hipMemcpyAsync(hps.data(), psum, (R + 1) * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
@@ -180,7 +201,7 @@ void serialize_index(sme_index *ix, hipStream_t st) {
     int64_t *rec_off = grp_bytes;  // reuse after scan
     hipLaunchKernelGGL(k_ser_offsets, dim3(G), dim3(256), 0, st, idx2, scan, V, part, part_sp, sp_bytes, rec_off);
     hipLaunchKernelGGL(k_ser_write, dim3((unsigned)std::min<int64_t>((V + 3) / 4, 65536)), dim3(256), 0, st,
-                       (const int64_t *)ix->d_term_off.p, (const uint16_t *)ix->d_term_chars.p,
+                       (const int64_t *)ix->d_term_off.p, (const uint16_t *)ix->d_term_chars.p, gram, ix->K,
                        (const int64_t *)ix->d_off.p, (const int32_t *)ix->d_docno_o.p, (const int32_t *)ix->d_tf_o.p,
                        V, rec_off, out);
     SME_CHECK_LAUNCH();

@@ -35,15 +35,17 @@ def test_device_process_content_fuzz(ctx):
         assert ctx.process_content(doc) == O.process_content(doc), doc
 
 
-def _check_build(sme, corpus, mapping_ids, R=1, idf_mode=0):
+def _check_build(sme, corpus, mapping_ids, R=1, idf_mode=0, K=1):
     mb = O.write_mapping(mapping_ids)
-    ref = O.OracleIndex(corpus, mb, 1, R)
-    ctx = sme.Context(1, R, idf_mode)
+    ref = O.OracleIndex(corpus, mb, K, R)
+    ctx = sme.Context(K, R, idf_mode)
     ctx.load_docno_mapping(mb)
     ix = ctx.build(corpus)
     assert ix.N == ref.N
     for p in range(R):
         common.compare_partitions(ix.partition_records(p), ref.partition_bytes(p))
+    if K > 1:
+        return ix, ref
     # CSR view equals the oracle's reduce output
     off, dn, tf, df = ix.csr()
     rterms = sorted([t for t in ref.terms() if t[0] != (" ",)], key=lambda t: t[0][0].encode("utf-16-be", "surrogatepass"))
@@ -86,6 +88,15 @@ def test_build_invalid_utf8_and_big_record(sme):
     big = " ".join("t%05d" % i for i in range(5000)).encode()
     docs.append(b"<DOC><DOCNO>BIG</DOCNO>" + big + b"</DOC>")
     _check_build(sme, b"".join(docs), sorted(["U%02d" % i for i in range(20)] + ["BIG"]), R=3)
+
+
+def test_build_nested_doc_tags(sme):
+    """A <DOC> inside a record is content (XMLRecordReader reads to the next
+    </DOC>); a start tag after the last </DOC> opens no record."""
+    corpus = (b"<DOC><DOCNO>A</DOCNO> one <DOC><DOCNO>B</DOCNO> two </DOC>"
+              b"<DOC><DOCNO>C</DOCNO> three </DOC><DOC><DOCNO>D</DOCNO> open")
+    _check_build(sme, corpus, ["A", "B", "C", "D"], R=1)
+    _check_build(sme, corpus, ["A", "B", "C", "D"], R=1, K=2)
 
 
 def test_build_empty_and_no_records(sme):
@@ -136,3 +147,38 @@ def test_forward_index_facade(sme):
     fw = sme.IntDocVectorsForwardIndex(ix)
     fw.getValue(["cat", "dog", "unknownterm"])
     assert fw.rank() == [1, 2]
+
+
+@pytest.mark.parametrize("K,R", [(2, 1), (2, 10), (3, 4)])
+def test_build_kgram_synthetic(sme, synth, K, R):
+    n = 250
+    c = synth.gen_corpus(n, V=600, seed=21, len_lo=1, len_hi=60)
+    _check_build(sme, c, synth.docids(n), R=R, K=K)
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_build_kgram_fuzz(sme, seed):
+    """K = 2 over markup, acronym splits (several terms per raw token), duplicate /
+    missing docids, and a record with more distinct 2-grams than the wave table."""
+    corpus, ids = common.fuzz_corpus(seed, 100)
+    big = " ".join("g%04d" % i for i in range(1500)).encode()
+    corpus += b"<DOC><DOCNO>" + ids[0].encode() + b"</DOCNO>" + big + b"</DOC>"
+    _check_build(sme, corpus, ids, R=1, K=2)
+    _check_build(sme, corpus, ids, R=3, K=2)
+
+
+def test_kgram_queries_first_element_lookup(sme, synth):
+    """K = 2: a query term resolves to the LAST 2-gram starting with it (the
+    forward index's Hashtable), as the oracle's rank() does."""
+    n = 150
+    c = synth.gen_corpus(n, V=300, seed=8, len_lo=10, len_hi=50)
+    ix, ref = _check_build(sme, c, synth.docids(n), R=1, K=2)
+    firsts = sorted(set(ix.term(i) for i in range(ix.V)))[:60]
+    rng = random.Random(5)
+    for q in range(40):
+        tl = [rng.choice(firsts) for _ in range(rng.randint(1, 3))]
+        ids = ix.lookup(tl)
+        dn, sc = ix.query_topk(ids.astype(np.int32), np.array([0, len(ids)], np.int64), 10)
+        rd, rs = ref.query(tl, 10, 0, 0)
+        assert dn[0, :len(rd)].tolist() == rd, (q, tl)
+        assert np.array_equal(sc[0, :len(rd)], np.array(rs))

@@ -81,6 +81,8 @@ def test_record_reader_quirks():
     assert len(recs) == 1 and recs[0] == (0, 24)
     # unterminated record is dropped
     assert O.split_records(b"<DOC> a </DOC><DOC> b") == [(0, 14)]
+    # a nested <DOC> is content of the enclosing record
+    assert O.split_records(b"<DOC> a <DOC> b </DOC> c </DOC>") == [(0, 22)]
 
 
 def test_docno_edge_cases():
