@@ -74,6 +74,14 @@ void sme_destroy(sme_ctx *ctx);
  * Arrays.binarySearch over {"", docids...} on the device. */
 int sme_load_docno_mapping(sme_ctx *ctx, const uint8_t *mapping_file, size_t n);
 
+/* Docno assignment (NumberTrecDocuments.run + TrecDocnoMapping.writeDocnoData,
+ * C/edu/umd/cloud9/collection/trec/NumberTrecDocuments.java:82-168,
+ * TrecDocnoMapping.java:92-125): the distinct docids of the corpus's records in
+ * UTF-8 byte order, numbered 1.., as the mapping FILE BYTES (int32 N, N x
+ * writeUTF(docid)) that sme_load_docno_mapping takes.  *mapping is owned by ctx
+ * until its next call. */
+int sme_number_documents(sme_ctx *ctx, const uint8_t *corpus, size_t nbytes, const uint8_t **mapping, size_t *n);
+
 /* Build from a host corpus (TREC <DOC>..</DOC> records, one split). Copies to HBM. */
 int sme_build_index(sme_ctx *ctx, const uint8_t *corpus, size_t nbytes, sme_index **out);
 

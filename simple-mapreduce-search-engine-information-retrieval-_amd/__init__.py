@@ -42,7 +42,7 @@ EXPORTS = [
     "sme_last_error", "sme_version", "sme_create", "sme_destroy", "sme_load_docno_mapping", "sme_build_index",
     "sme_build_index_device", "sme_index_free", "sme_index_stats", "sme_index_partition_records", "sme_index_csr",
     "sme_index_device_arrays", "sme_index_term", "sme_tokenize", "sme_lookup_terms", "sme_query_topk",
-    "sme_query_topk_device", "sme_last_build_profile", "sme_index_reweight",
+    "sme_query_topk_device", "sme_last_build_profile", "sme_index_reweight", "sme_number_documents",
 ]
 
 
@@ -76,6 +76,7 @@ def lib():
     L.sme_query_topk_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp]
     L.sme_last_build_profile.argtypes = [vp, C.POINTER(C.c_char_p)]
     L.sme_index_reweight.argtypes = [vp, C.c_int64, vp, vp]
+    L.sme_number_documents.argtypes = [vp, C.c_char_p, sz, C.POINTER(vp), C.POINTER(sz)]
     _lib = L
     return L
 
@@ -137,6 +138,12 @@ class Context:
     def load_docno_mapping(self, mapping_bytes):
         _check(lib().sme_load_docno_mapping(self._h, mapping_bytes, len(mapping_bytes)))
 
+    def number_documents(self, corpus):
+        """NumberTrecDocuments + writeDocnoData on the device: the mapping file bytes."""
+        p, n = C.c_void_p(), C.c_size_t()
+        _check(lib().sme_number_documents(self._h, corpus, len(corpus), C.byref(p), C.byref(n)))
+        return C.string_at(p, n.value)
+
     def build(self, corpus):
         """Build from host bytes (copied to HBM)."""
         h = C.c_void_p()
@@ -195,8 +202,10 @@ class Index:
         o, d, t, f = C.POINTER(C.c_int64)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)()
         _check(lib().sme_index_csr(self._h, C.byref(o), C.byref(d), C.byref(t), C.byref(f)))
         V, P = self.V, self.P
-        return (np.ctypeslib.as_array(o, (V + 1,)).copy(), np.ctypeslib.as_array(d, (max(P, 1),))[:P].copy(),
-                np.ctypeslib.as_array(t, (max(P, 1),))[:P].copy(), np.ctypeslib.as_array(f, (max(V, 1),))[:V].copy())
+
+        def arr(ptr, n, dt):  # empty host vectors may hand out NULL
+            return np.ctypeslib.as_array(ptr, (n,)).copy() if n else np.zeros(0, dt)
+        return arr(o, V + 1, np.int64), arr(d, P, np.int32), arr(t, P, np.int32), arr(f, V, np.int32)
 
     def device_arrays(self):
         o, d, w = C.c_void_p(), C.c_void_p(), C.c_void_p()
@@ -252,6 +261,22 @@ class GalagoTokenizer:
 
     def processContent(self, text):  # noqa: N802 (reference name)
         return self.ctx.process_content(text)
+
+
+class NumberTrecDocuments:
+    """NumberTrecDocuments.run(input, output, mappingFile, nMappers) as one device
+    call: returns (and optionally writes) the docno mapping file."""
+
+    def __init__(self, device=0):
+        self.ctx = Context(device=device)
+
+    def run(self, corpus, mapping_file=None):
+        corpus = open(corpus, "rb").read() if isinstance(corpus, str) else corpus
+        m = self.ctx.number_documents(corpus)
+        if mapping_file is not None:
+            with open(mapping_file, "wb") as f:
+                f.write(m)
+        return m
 
 
 class TermKGramDocIndexer:

@@ -203,6 +203,20 @@ int sme_load_docno_mapping(sme_ctx *cx, const uint8_t *m, size_t n) {
   });
 }
 
+int sme_number_documents(sme_ctx *cx, const uint8_t *corpus, size_t nbytes, const uint8_t **mapping, size_t *n) {
+  return guard([&] {
+    if (!cx || !mapping || !n || (!corpus && nbytes)) throw sme::Error(SME_EINVAL, "null argument");
+    set_device(cx);
+    hipStream_t st = cx->own_stream;
+    sme::DevBuf buf;
+    uint8_t *d = buf.as<uint8_t>(nbytes + 16);
+    if (nbytes) SME_HIP(hipMemcpyAsync(d, corpus, nbytes, hipMemcpyHostToDevice, st));
+    sme::number_documents(cx, d, nbytes, st, cx->mapping_out);
+    *mapping = cx->mapping_out.data();
+    *n = cx->mapping_out.size();
+  });
+}
+
 int sme_build_index_device(sme_ctx *cx, const void *d_corpus, size_t nbytes, void *stream, sme_index **out) {
   return guard([&] {
     if (!cx || !out || (!d_corpus && nbytes)) throw sme::Error(SME_EINVAL, "null argument");

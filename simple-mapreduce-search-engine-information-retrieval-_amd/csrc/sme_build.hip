@@ -37,6 +37,7 @@
 
 #include "sme_internal.hpp"
 #include "sme_text.hpp"
+#include "sme_trec.hpp"
 
 namespace sme {
 
@@ -384,36 +385,11 @@ __global__ void k_docno(const uint8_t *t, const uint64_t *rs, const uint64_t *re
                         unsigned long long *err) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nR; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = (int64_t)rs[r], e = (int64_t)re[r];
-    // indexOf("<DOCNO>") then indexOf("</DOCNO>", start)  (TrecDocument.java:78-84)
-    int64_t a = -1;
-    for (int64_t p = s; p + 7 <= e; p++) {
-      if (t[p] == '<' && t[p + 1] == 'D' && t[p + 2] == 'O' && t[p + 3] == 'C' && t[p + 4] == 'N' &&
-          t[p + 5] == 'O' && t[p + 6] == '>') {
-        a = p;
-        break;
-      }
-    }
     int64_t ib, ie;
-    if (a < 0) {
-      ib = ie = 0;  // docid ""
-    } else {
-      int64_t z = -1;
-      for (int64_t p = a; p + 8 <= e; p++) {
-        if (t[p] == '<' && t[p + 1] == '/' && t[p + 2] == 'D' && t[p + 3] == 'O' && t[p + 4] == 'C' &&
-            t[p + 5] == 'N' && t[p + 6] == 'O' && t[p + 7] == '>') {
-          z = p;
-          break;
-        }
-      }
-      if (z < 0) {  // substring(start + 7, -1) throws: the map task fails
-        atomicAdd(err, 1ull);
-        docno[r] = 0;
-        continue;
-      }
-      ib = a + 7;
-      ie = z;
-      while (ib < ie && t[ib] <= 0x20) ib++;  // String.trim(); bytes <= 0x20 are exactly units <= 0x20
-      while (ie > ib && t[ie - 1] <= 0x20) ie--;
+    if (!docid_span(t, s, e, &ib, &ie)) {  // getDocid throws: the map task fails
+      atomicAdd(err, 1ull);
+      docno[r] = 0;
+      continue;
     }
     // Arrays.binarySearch over {"", docids...}
     int64_t lo = 0, hi = mn - 1;
@@ -1898,13 +1874,12 @@ enum {
 constexpr int kBuildWs = 64;  // build slots live at ctx->ws[64..127]
 static_assert(W_NSLOTS <= 64, "too many build workspace slots");
 
-sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st) {
-  if (!cx->has_map) throw Error(SME_ENOMAP, "no docno mapping loaded (sme_load_docno_mapping)");
+// K1 + K1b: record spans of the corpus exactly as XMLRecordReader yields them,
+// plus the sorted positions of every '<' whose markup is not "simple" (C).
+RecordSpans find_records(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st, Prof *prof) {
   DevBuf *W = cx->ws + kBuildWs;
-  Prof prof(st);
   auto cub_tmp = [&](size_t bytes) { return cx->cub_tmp.get(bytes); };
   unsigned long long *cnt = W[W_CNT].as<unsigned long long>(16);
-
   // ---------------- K1 scan ----------------
   // every '<' position, then the tag classification over that list
   uint64_t capL = std::max<uint64_t>(cx->lt_cap_hint, std::max<uint64_t>(4096, n / 256));
@@ -1947,7 +1922,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     capC = std::max<uint64_t>(capC, h_cnt[2]);
   }
   const int64_t nS = (int64_t)h_cnt[0], nE = (int64_t)h_cnt[1], nC = (int64_t)h_cnt[2];
-  prof.mark("scan_tags");
+  if (prof) prof->mark("scan_tags");
 
   // sort S, E, C positions
   // sorted copies land in spare workspace slots (no device-to-device copy back)
@@ -1983,7 +1958,20 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       nR = (int64_t)d2h(cnt + 1, st);
     }
   }
-  prof.mark("records");
+  if (prof) prof->mark("records");
+  return RecordSpans{rs, re, nR, C, nC};
+}
+
+sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st) {
+  if (!cx->has_map) throw Error(SME_ENOMAP, "no docno mapping loaded (sme_load_docno_mapping)");
+  DevBuf *W = cx->ws + kBuildWs;
+  Prof prof(st);
+  auto cub_tmp = [&](size_t bytes) { return cx->cub_tmp.get(bytes); };
+  unsigned long long *cnt = W[W_CNT].as<unsigned long long>(16);
+
+  const RecordSpans rsp = find_records(cx, t, n, st, &prof);
+  uint64_t *rs = rsp.rs, *re = rsp.re, *C = rsp.C;
+  const int64_t nR = rsp.nR, nC = rsp.nC;
 
   // ---------------- K2 docno ----------------
   int32_t *docno = W[W_DOCNO].as<int32_t>(nR + 1);

@@ -23,6 +23,7 @@ struct sme_ctx {
   uint64_t vocab_long_cap = 0, vocab_ovf_cap = 0, raw_cap_hint = 0, lt_cap_hint = 0;  // learned across builds
   std::string profile_json;
   std::vector<std::pair<std::string, float>> last_profile;
+  std::vector<uint8_t> mapping_out;  // last sme_number_documents result
   float last_query_ms = -1.0f;  // device time of the last query kernel launch
   // indexes borrow the context (its pool, workspace, stream): sme_destroy defers
   // the delete until the last index is freed, whatever order a host frees them in
@@ -79,6 +80,15 @@ struct sme_index {
 };
 
 namespace sme {
+struct Prof;  // per-stage device-event timer (sme_build.hip)
+struct RecordSpans {
+  uint64_t *rs, *re;  // record [rs, re) byte spans, in reader order
+  int64_t nR;
+  uint64_t *C;        // sorted positions of '<' whose markup is not "simple"
+  int64_t nC;
+};
+RecordSpans find_records(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, Prof *prof);
+void number_documents(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, std::vector<uint8_t> &out);
 sme_index *build_index(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st);
 void serialize_index(sme_index *ix, hipStream_t st);
 void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t st);

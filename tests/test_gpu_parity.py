@@ -93,10 +93,15 @@ def test_build_invalid_utf8_and_big_record(sme):
 def test_build_nested_doc_tags(sme):
     """A <DOC> inside a record is content (XMLRecordReader reads to the next
     </DOC>); a start tag after the last </DOC> opens no record."""
-    corpus = (b"<DOC><DOCNO>A</DOCNO> one <DOC><DOCNO>B</DOCNO> two </DOC>"
-              b"<DOC><DOCNO>C</DOCNO> three </DOC><DOC><DOCNO>D</DOCNO> open")
-    _check_build(sme, corpus, ["A", "B", "C", "D"], R=1)
-    _check_build(sme, corpus, ["A", "B", "C", "D"], R=1, K=2)
+    corpus = (b"<DOC><DOCNO>AX1</DOCNO> wolf <DOC><DOCNO>BX2</DOCNO> bear moose </DOC>"
+              b"<DOC><DOCNO>CX3</DOCNO> wolf elk </DOC><DOC><DOCNO>DX4</DOCNO> lynx")
+    ids = ["AX1", "BX2", "CX3", "DX4"]
+    ix, ref = _check_build(sme, corpus, ids, R=1)
+    assert ix.N == 2 and ix.V > 0
+    _check_build(sme, corpus, ids, R=1, K=2)
+    # all-stopword records: no postings at all
+    ix, _ = _check_build(sme, b"<DOC><DOCNO>A</DOCNO> one two </DOC>", ["A"], R=1)
+    assert (ix.V, ix.P) == (0, 0)
 
 
 def test_build_empty_and_no_records(sme):
@@ -182,3 +187,63 @@ def test_kgram_queries_first_element_lookup(sme, synth):
         rd, rs = ref.query(tl, 10, 0, 0)
         assert dn[0, :len(rd)].tolist() == rd, (q, tl)
         assert np.array_equal(sc[0, :len(rd)], np.array(rs))
+
+
+def _java_trim(s):
+    b, e = 0, len(s)
+    while b < e and ord(s[b]) <= 0x20:
+        b += 1
+    while e > b and ord(s[e - 1]) <= 0x20:
+        e -= 1
+    return s[b:e]
+
+
+def _mutf8(s):
+    raw = s.encode("utf-16-be", "surrogatepass")
+    out = bytearray()
+    for i in range(0, len(raw), 2):
+        c = (raw[i] << 8) | raw[i + 1]
+        if 1 <= c <= 0x7F:
+            out.append(c)
+        elif c > 0x7FF:
+            out += bytes([0xE0 | (c >> 12), 0x80 | ((c >> 6) & 0x3F), 0x80 | (c & 0x3F)])
+        else:
+            out += bytes([0xC0 | (c >> 6), 0x80 | (c & 0x3F)])
+    return bytes(out)
+
+
+def _ref_number_documents(corpus):
+    """NumberTrecDocuments (map getDocid -> Text, byte-order sort, distinct, 1..N)
+    + writeDocnoData, restated from NumberTrecDocuments.java:82-107 and
+    TrecDocnoMapping.java:92-125 over the oracle's record reader."""
+    ids = set()
+    for off, ln in O.split_records(corpus):
+        text = corpus[off:off + ln].decode("utf-8", "replace")
+        i = text.find("<DOCNO>")
+        d = "" if i < 0 else _java_trim(text[i + 7:text.index("</DOCNO>", i)])
+        ids.add(d.encode("utf-8", "surrogatepass"))
+    out = bytearray(len(ids).to_bytes(4, "big"))
+    for k in sorted(ids):
+        m = _mutf8(k.decode("utf-8", "surrogatepass"))
+        out += len(m).to_bytes(2, "big") + m
+    return bytes(out)
+
+
+def test_number_documents(sme, synth):
+    ctx = sme.Context(1, 1)
+    c = synth.gen_corpus(300, V=500, seed=4, len_lo=5, len_hi=30)
+    m = ctx.number_documents(c)
+    assert m == synth.mapping_bytes(300) == _ref_number_documents(c)
+    fz, _ = common.fuzz_corpus(6, 150)  # duplicate, missing and unmapped docids, <<DOC>, unterminated tail
+    assert ctx.number_documents(fz) == _ref_number_documents(fz)
+    odd = (b"<DOC><DOCNO> caf\xc3\xa9 </DOCNO> x </DOC><DOC><DOCNO>\xf0\x9f\x98\x80z</DOCNO> y </DOC>"
+           b"<DOC><DOCNO>\xc4\xb0d</DOCNO> z </DOC><DOC><DOCNO>a\xffb</DOCNO> w </DOC><DOC> none </DOC>"
+           b"<DOC><DOCNO>ab</DOCNO></DOC><DOC><DOCNO>a</DOCNO></DOC><DOC><DOCNO>ab\x01</DOCNO></DOC>")
+    assert ctx.number_documents(odd) == _ref_number_documents(odd)
+    assert ctx.number_documents(b"no records") == b"\x00\x00\x00\x00"
+    with pytest.raises(sme.SmeError):
+        ctx.number_documents(b"<DOC><DOCNO>A x </DOC>")
+    # the generated mapping drives the index build: docnos 1..N in docid order
+    ctx.load_docno_mapping(ctx.number_documents(fz))
+    ix = ctx.build(fz)
+    assert ix.N == O.OracleIndex(fz, ctx.number_documents(fz), 1, 1).N
