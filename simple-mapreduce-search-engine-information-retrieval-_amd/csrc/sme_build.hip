@@ -1813,6 +1813,238 @@ __global__ void k_gram_ids(const uint64_t *k, const uint32_t *incl, int64_t P, i
 }
 
 // ============================================================================
+// K8: reducer output order -- per term, a STABLE sort by tf descending of the
+// docno-ascending postings (MyReducer.reduce's Collections.sort over
+// PostingWritable.compareTo, TermKGramDocIndexer.java:211, PostingWritable.java:57-59).
+// Segmented counting sort: the term CSR already delimits the segments and tf is a
+// small integer, so one read + one write per posting replaces a full radix sort.
+// ============================================================================
+constexpr int kTfSmall = 64;    // segments up to one wave chunk: rank by lane compares
+constexpr int kTfMedium = 8192; // up to this: 4-wave blocks; beyond: 16-wave blocks
+constexpr int kTfSortMaxTf = 1023;  // LDS counters (max_tf + 1) x 16 x 4 B <= 64 KiB; above: radix sort
+
+// segments of length <= kTfSmall: one wave each; output rank of lane i =
+// #{j : tf_j > tf_i} + #{j < i : tf_j == tf_i}
+__global__ __launch_bounds__(256) void k_tfsort_small(const int64_t *__restrict__ off, int64_t V,
+                                                      const int32_t *__restrict__ docno_d,
+                                                      const int32_t *__restrict__ tf_d, int32_t *docno_o,
+                                                      int32_t *tf_o) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); s < V; s += nw) {
+    const int64_t b = off[s];
+    const int n = (int)(off[s + 1] - b);
+    if (n > kTfSmall || n == 0) continue;  // wave-uniform
+    const bool v = lane < n;
+    const int32_t t = v ? tf_d[b + lane] : 0, d = v ? docno_d[b + lane] : 0;
+    int r = 0;
+    for (int j = 0; j < n; j++) {
+      const int32_t tj = __shfl(t, j, 64);
+      r += (tj > t) || (tj == t && j < lane);
+    }
+    if (v) {
+      docno_o[b + r] = d;
+      tf_o[b + r] = t;
+    }
+  }
+}
+
+// one NW-wave block per segment (length in (lo, hi]): wave w owns a contiguous run
+// of 64-posting chunks.  Pass 1 counts tf per wave, a block scan orders the
+// counters as (tf desc, wave asc), pass 2 places every posting at its counter +
+// its rank among equal-tf lanes of the chunk (ballot), which keeps docno order.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_tfsort_block(const int64_t *__restrict__ off, int64_t V,
+                                                          const int32_t *__restrict__ docno_d,
+                                                          const int32_t *__restrict__ tf_d, int32_t *docno_o,
+                                                          int32_t *tf_o, int64_t lo, int64_t hi, int max_tf) {
+  extern __shared__ int32_t cnt[];  // [(max_tf - tf) * NW + w]
+  __shared__ int32_t wsum[NW];
+  constexpr int NT = NW * 64;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int L = (max_tf + 1) * NW;
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  for (int64_t s = blockIdx.x; s < V; s += gridDim.x) {
+    const int64_t b = off[s], n = off[s + 1] - b;
+    if (n <= lo || n > hi) continue;  // block-uniform
+    for (int j = tid; j < L; j += NT) cnt[j] = 0;
+    __syncthreads();
+    const int64_t nch = (n + 63) >> 6, cpw = (nch + NW - 1) / NW;
+    const int64_t c0 = (int64_t)w * cpw, c1 = c0 + cpw < nch ? c0 + cpw : nch;
+    for (int64_t c = c0; c < c1; c++) {
+      const int64_t i = (c << 6) + lane;
+      const bool v = i < n;
+      const int32_t t = v ? tf_d[b + i] : -1;
+      uint64_t pend = __ballot(v);
+      while (pend) {
+        const int32_t tv = __shfl(t, __ffsll((unsigned long long)pend) - 1, 64);
+        const uint64_t m = __ballot(t == tv);
+        if (lane == 0) cnt[(max_tf - tv) * NW + w] += __popcll(m);
+        pend &= ~m;
+      }
+    }
+    __syncthreads();
+    // exclusive scan of cnt[0..L) (each thread a contiguous run, then across threads)
+    const int per = (L + NT - 1) / NT, j0 = tid * per, j1 = j0 + per < L ? j0 + per : L;
+    int run = 0;
+    for (int j = j0; j < j1; j++) run += cnt[j];
+    int inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    int base = inc - run;
+    for (int k = 0; k < w; k++) base += wsum[k];
+    for (int j = j0; j < j1; j++) {
+      const int c = cnt[j];
+      cnt[j] = base;
+      base += c;
+    }
+    __syncthreads();
+    for (int64_t c = c0; c < c1; c++) {
+      const int64_t i = (c << 6) + lane;
+      const bool v = i < n;
+      const int32_t t = v ? tf_d[b + i] : -1, d = v ? docno_d[b + i] : 0;
+      uint64_t pend = __ballot(v);
+      while (pend) {
+        const int32_t tv = __shfl(t, __ffsll((unsigned long long)pend) - 1, 64);
+        const uint64_t m = __ballot(t == tv);
+        const int slot = (max_tf - tv) * NW + w;
+        const int cb = cnt[slot];
+        if (t == tv) {
+          const int64_t p = b + cb + __popcll(m & lt_mask);
+          docno_o[p] = d;
+          tf_o[p] = t;
+        }
+        if (lane == 0) cnt[slot] = cb + __popcll(m);
+        pend &= ~m;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Segments longer than kTfMedium are cut into tiles of kTfTile postings so that a
+// 1M-posting term spreads over many CUs: (1) per tile tf counts, (2) per segment
+// an exclusive scan of the counts in (tf desc, tile asc) order, (3) per tile the
+// ballot placement of k_tfsort_block from the tile's scanned counters.
+constexpr int kTfTile = 4096;
+
+__global__ void k_tf_ntiles(const int64_t *off, int64_t V, int64_t *nt) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s <= V; s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = s < V ? off[s + 1] - off[s] : 0;
+    nt[s] = n > kTfMedium ? (n + kTfTile - 1) / kTfTile : 0;
+  }
+}
+
+// segment of tile tau: the s with toff[s] <= tau < toff[s + 1]
+__device__ __forceinline__ int64_t tile_segment(const int64_t *toff, int64_t V, int64_t tau) {
+  int64_t lo = 0, hi = V;  // toff[lo] <= tau < toff[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (toff[mid] <= tau) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// (1) one wave per tile: LDS counts (order-free), written as tcnt[tau][max_tf - tf]
+__global__ __launch_bounds__(256) void k_tf_tile_count(const int64_t *__restrict__ off, int64_t V,
+                                                       const int64_t *__restrict__ toff, int64_t ntiles,
+                                                       const int32_t *__restrict__ tf_d, int max_tf,
+                                                       int32_t *tcnt) {
+  extern __shared__ int32_t h[];  // 4 waves x (max_tf + 1)
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, F = max_tf + 1;
+  int32_t *hw = h + w * F;
+  const int64_t nwv = (int64_t)gridDim.x * 4;
+  for (int64_t tau = (int64_t)blockIdx.x * 4 + w; tau < ntiles; tau += nwv) {  // wave-uniform
+    const int64_t s = tile_segment(toff, V, tau);
+    const int64_t b = off[s] + (tau - toff[s]) * kTfTile, e = min(off[s + 1], b + (int64_t)kTfTile);
+    for (int j = lane; j < F; j += 64) hw[j] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (int64_t i = b + lane; i < e; i += 64) atomicAdd(&hw[max_tf - tf_d[i]], 1);
+    __builtin_amdgcn_wave_barrier();
+    for (int j = lane; j < F; j += 64) tcnt[tau * F + j] = hw[j];
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// (2) one block per large segment: counters -> segment-relative start positions
+__global__ __launch_bounds__(256) void k_tf_tile_scan(const int64_t *__restrict__ off, int64_t V,
+                                                      const int64_t *__restrict__ toff, int max_tf, int32_t *tcnt) {
+  __shared__ int32_t wsum[4];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, F = max_tf + 1;
+  for (int64_t s = blockIdx.x; s < V; s += gridDim.x) {
+    const int64_t t0 = toff[s], T = toff[s + 1] - t0;
+    if (T == 0) continue;  // block-uniform
+    int base = 0;          // identical in every thread
+    for (int f = 0; f < F; f++) {
+      for (int64_t j0 = 0; j0 < T; j0 += 256) {
+        const int64_t j = j0 + tid;
+        const int32_t c = j < T ? tcnt[(t0 + j) * F + f] : 0;
+        int inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int u = __shfl_up(inc, o, 64);
+          if (lane >= o) inc += u;
+        }
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        int pre = base;
+        for (int k = 0; k < w; k++) pre += wsum[k];
+        if (j < T) tcnt[(t0 + j) * F + f] = pre + inc - c;
+        base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+      }
+    }
+  }
+}
+
+// (3) one wave per tile: stable placement from the tile's counters
+__global__ __launch_bounds__(256) void k_tf_tile_place(const int64_t *__restrict__ off, int64_t V,
+                                                       const int64_t *__restrict__ toff, int64_t ntiles,
+                                                       const int32_t *__restrict__ docno_d,
+                                                       const int32_t *__restrict__ tf_d, int max_tf,
+                                                       const int32_t *__restrict__ tcnt, int32_t *docno_o,
+                                                       int32_t *tf_o) {
+  extern __shared__ int32_t h[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, F = max_tf + 1;
+  int32_t *hw = h + w * F;
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  const int64_t nwv = (int64_t)gridDim.x * 4;
+  for (int64_t tau = (int64_t)blockIdx.x * 4 + w; tau < ntiles; tau += nwv) {
+    const int64_t s = tile_segment(toff, V, tau);
+    const int64_t sb = off[s];
+    const int64_t b = sb + (tau - toff[s]) * kTfTile, e = min(off[s + 1], b + (int64_t)kTfTile);
+    for (int j = lane; j < F; j += 64) hw[j] = tcnt[tau * F + j];
+    __builtin_amdgcn_wave_barrier();
+    for (int64_t c = b; c < e; c += 64) {
+      const int64_t i = c + lane;
+      const bool v = i < e;
+      const int32_t t = v ? tf_d[i] : -1, d = v ? docno_d[i] : 0;
+      uint64_t pend = __ballot(v);
+      while (pend) {
+        const int32_t tv = __shfl(t, __ffsll((unsigned long long)pend) - 1, 64);
+        const uint64_t m = __ballot(t == tv);
+        const int slot = max_tf - tv;
+        const int cb = hw[slot];
+        if (t == tv) {
+          const int64_t p = sb + cb + __popcll(m & lt_mask);
+          docno_o[p] = d;
+          tf_o[p] = t;
+        }
+        if (lane == 0) hw[slot] = cb + __popcll(m);
+        pend &= ~m;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ============================================================================
 // host orchestration
 // ============================================================================
 struct Prof {
@@ -2497,7 +2729,34 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
 
   // ---------------- K8 reduce-output order ----------------
   int32_t *docno_o = ix->d_docno_o.as<int32_t>(PP + 1), *tf_o = ix->d_tf_o.as<int32_t>(PP + 1);
-  if (PP > 0) {
+  if (PP > 0 && max_tf <= kTfSortMaxTf) {
+    // segmented counting sort over the term CSR (no full-width key sort)
+    hipLaunchKernelGGL(k_tfsort_small, dim3(grid_for(Vi * 64, 256, 8192)), dim3(256), 0, st, off, Vi, docno_d, tf_d,
+                       docno_o, tf_o);
+    const size_t lds4 = (size_t)(max_tf + 1) * 4 * sizeof(int32_t);
+    hipLaunchKernelGGL(k_tfsort_block<4>, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(Vi, 1), 4096)),
+                       dim3(256), lds4, st, off, Vi, docno_d, tf_d, docno_o, tf_o, (int64_t)kTfSmall,
+                       (int64_t)kTfMedium, max_tf);
+    // large segments: tiles spread over the whole chip
+    int64_t *ntl = W[W_FKEYS].as<int64_t>(Vi + 1), *toff = W[W_FREPS].as<int64_t>(Vi + 1);
+    hipLaunchKernelGGL(k_tf_ntiles, dim3(grid_for(Vi + 1)), dim3(256), 0, st, off, Vi, ntl);
+    size_t tbb = 0;
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, ntl, toff, (int)Vi + 1, st));
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, ntl, toff, (int)Vi + 1, st));
+    const int64_t ntiles = d2h(toff + Vi, st);
+    if (ntiles > 0) {
+      const int F = max_tf + 1;
+      int32_t *tcnt = reinterpret_cast<int32_t *>(W[W_CKEY].as<uint64_t>((ntiles * F + 1) / 2 + 1));
+      const unsigned tg = (unsigned)std::min<int64_t>((ntiles + 3) / 4, 8192);
+      hipLaunchKernelGGL(k_tf_tile_count, dim3(tg), dim3(256), (size_t)4 * F * sizeof(int32_t), st, off, Vi, toff,
+                         ntiles, tf_d, max_tf, tcnt);
+      hipLaunchKernelGGL(k_tf_tile_scan, dim3((unsigned)std::min<int64_t>(Vi, 8192)), dim3(256), 0, st, off, Vi,
+                         toff, max_tf, tcnt);
+      hipLaunchKernelGGL(k_tf_tile_place, dim3(tg), dim3(256), (size_t)4 * F * sizeof(int32_t), st, off, Vi, toff,
+                         ntiles, docno_d, tf_d, max_tf, tcnt, docno_o, tf_o);
+    }
+    SME_CHECK_LAUNCH();
+  } else if (PP > 0) {
     const int tfb = bits_for((uint64_t)max_tf);
     if (tbits + tfb <= 32) {  // u32 composite (term, tf desc)
       const uint32_t tfmask = (uint32_t)((1ull << tfb) - 1);

@@ -70,6 +70,16 @@ def test_build_synthetic(sme, synth):
     _check_build(sme, c, synth.docids(n), R=10)
 
 
+def test_build_large_segments(sme, synth):
+    """Terms with df > 8192 and tf up to ~20: every class of the segmented
+    tf-desc sort (one wave, 4-wave and 16-wave blocks) against the reducer order."""
+    n = 12000
+    c = synth.gen_corpus(n, V=250, seed=11, len_lo=50, len_hi=150)
+    ix, _ = _check_build(sme, c, synth.docids(n), R=3)
+    off, _, _, _ = ix.csr()
+    assert int(np.diff(off).max()) > 8192
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_build_fuzz(sme, seed):
     corpus, ids = common.fuzz_corpus(seed, 120)
