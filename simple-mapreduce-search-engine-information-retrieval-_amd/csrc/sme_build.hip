@@ -2785,7 +2785,18 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
 
   // doc-counter postings need every record's docno in input order
   int32_t *rdn = ix->d_rec_docno.as<int32_t>(nR + 1);
-  if (nR > 0) SME_HIP(hipMemcpyAsync(rdn, docno, nR * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+  if (nR > 0) {
+    SME_HIP(hipMemcpyAsync(rdn, docno, nR * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    int *dmn = reinterpret_cast<int *>(cnt + 12), *dmx = dmn + 1;
+    const int h_init[2] = {INT_MAX, INT_MIN};
+    SME_HIP(hipMemcpyAsync(dmn, h_init, sizeof h_init, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_docno_range, dim3(grid_for(nR, 256, 1024)), dim3(256), 0, st, docno, nR, dmn, dmx);
+    int h_r[2];
+    SME_HIP(hipMemcpyAsync(h_r, dmn, sizeof h_r, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    ix->dmin = h_r[0];
+    ix->dmax = h_r[1];
+  }
   prof.mark("finalize");
   ix->V = Vi;
   ix->Vt = V;

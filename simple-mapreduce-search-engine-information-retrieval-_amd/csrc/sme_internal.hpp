@@ -25,6 +25,7 @@ struct sme_ctx {
   std::vector<std::pair<std::string, float>> last_profile;
   std::vector<uint8_t> mapping_out;  // last sme_number_documents result
   float last_query_ms = -1.0f;  // device time of the last query kernel launch
+  bool last_query_tiled = false;  // which scoring kernel it was (k_query_tiled / k_query)
   // indexes borrow the context (its pool, workspace, stream): sme_destroy defers
   // the delete until the last index is freed, whatever order a host frees them in
   int live_indexes = 0;
@@ -37,6 +38,7 @@ struct sme_index {
   int64_t N = 0, V = 0, P = 0;
   int64_t Vt = 0;  // term vocabulary size (V counts k-grams when K > 1)
   int32_t max_tf = 0;
+  int64_t dmin = 0, dmax = -1;  // docno range of the records (query doc tiles)
   // sorted vocabulary (rank order): UTF-16 units
   sme::DevBuf d_term_off;    // int64 [V+1]
   sme::DevBuf d_term_chars;  // uint16

@@ -23,7 +23,10 @@
 // lane keeps its best KMAX (score, docno) in registers; the lists are merged by
 // k rounds of block arg-max at the end.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <math.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "sme_internal.hpp"
 #include "sme_text.hpp"
@@ -62,6 +65,58 @@ __device__ __forceinline__ void topk_insert(double (&ts)[K], int32_t (&td)[K], d
   if (!done) {
     ts[0] = s;
     td[0] = d;
+  }
+}
+
+// merge the per-lane lists: k rounds of block arg-max over list heads; thread 0
+// writes query q's k results (docno -1 / score 0 padding)
+template <int KMAX>
+__device__ __forceinline__ void emit_topk(double (&ts)[KMAX], int32_t (&td)[KMAX], int k, int q, int32_t *out_d,
+                                          double *out_s, double *red_s, int32_t *red_d, int32_t *red_t) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (int r = 0; r < k; r++) {
+    double bs = ts[0];
+    int32_t bd = td[0];
+    int32_t bt = tid;
+    for (int o = 32; o > 0; o >>= 1) {
+      double os = __shfl_xor(bs, o, 64);
+      int32_t od = __shfl_xor(bd, o, 64), ot = __shfl_xor(bt, o, 64);
+      if (better(os, od, bs, bd)) {
+        bs = os;
+        bd = od;
+        bt = ot;
+      }
+    }
+    if (lane == 0) {
+      red_s[wave] = bs;
+      red_d[wave] = bd;
+      red_t[wave] = bt;
+    }
+    __syncthreads();
+    bs = red_s[0];
+    bd = red_d[0];
+    bt = red_t[0];
+    for (int x = 1; x < kQNT / 64; x++)
+      if (better(red_s[x], red_d[x], bs, bd)) {
+        bs = red_s[x];
+        bd = red_d[x];
+        bt = red_t[x];
+      }
+    if (tid == bt) {  // pop the head: shift the winner's list left
+#pragma unroll
+      for (int j = 0; j < KMAX - 1; j++) {
+        ts[j] = ts[j + 1];
+        td[j] = td[j + 1];
+      }
+      ts[KMAX - 1] = -INFINITY;
+      td[KMAX - 1] = 0x7FFFFFFF;
+    }
+    if (tid == 0) {
+      const bool valid = bs != -INFINITY;
+      out_d[(int64_t)q * k + r] = valid ? bd : -1;
+      out_s[(int64_t)q * k + r] = valid ? bs : 0.0;
+    }
+    __syncthreads();
   }
 }
 
@@ -176,36 +231,206 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
       }
       __syncthreads();
     }
-    // merge the per-lane lists: k rounds of block arg-max over list heads
+    emit_topk<KMAX>(ts, td, k, q, out_d, out_s, red_s, red_d, red_t);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Tiled scoring (default path).  The docno axis is cut into fixed tiles of
+// kTile documents starting at the index's smallest docno.  A per-batch skip
+// table gives, for every DISTINCT term of the batch and every tile, the offset
+// of the term's first posting in that tile, so a workgroup knows every term's
+// range in a tile up front: it gathers all of them with one round of coalesced
+// loads into an LDS stage (docno-in-tile | tf << 12), then applies them term by
+// term in query-token order (one LDS barrier per term, no global latency in the
+// ordered part).  Same fp64 operation sequence as k_query: bit-identical scores.
+// ---------------------------------------------------------------------------
+constexpr int kTMaxTerms = 16;  // queries with more terms go through k_query
+constexpr int kWBits = 10;      // tile = 1024 documents: 8 KiB of fp64 accumulators per wave
+constexpr int kWTile = 1 << kWBits;
+constexpr int kWLut = 128;      // 1 + ln(tf) for tf < 128 from LDS
+constexpr int kWBatch = 8;      // 64-posting chunks in flight per wave
+
+__global__ void k_mark_terms(const int32_t *terms, int64_t n, int64_t V, int32_t *mark) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t t = terms[i];
+    if (t >= 0 && t < V) mark[t] = 1;
+  }
+}
+// distinct marked terms -> rows (row = exclusive scan of mark), their df
+__global__ void k_term_rows(const int32_t *mark, const int32_t *row_of, int64_t V, const int64_t *off,
+                            int32_t *term_of_row, int64_t *rdf) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x)
+    if (mark[t]) {
+      term_of_row[row_of[t]] = (int32_t)t;
+      rdf[row_of[t]] = off[t + 1] - off[t];
+    }
+}
+__global__ void k_max_qlen(const int64_t *qoff, int nq, int *mx) {
+  int m = 0;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x)
+    m = max(m, (int)(qoff[q + 1] - qoff[q]));
+  for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(mx, m);
+}
+// sk[row * (T + 1) + j] = first posting (term-relative) with tile >= j; every
+// entry is written exactly once: posting p covers tiles (tile(p-1), tile(p)],
+// the last posting also (tile(last), T].
+__global__ void k_skip_fill(const int64_t *rpre, int64_t nrows, const int32_t *term_of_row, const int64_t *off,
+                            const int32_t *docno, int64_t dmin, int64_t T, int32_t *sk) {
+  const int64_t total = rpre[nrows];
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total; x += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = nrows;  // rpre[lo] <= x < rpre[hi]
+    while (hi - lo > 1) {
+      const int64_t m = (lo + hi) >> 1;
+      if (rpre[m] <= x) lo = m;
+      else hi = m;
+    }
+    const int64_t b = off[term_of_row[lo]], i = x - rpre[lo], n = rpre[lo + 1] - rpre[lo];
+    int32_t *row = sk + lo * (T + 1);
+    const int64_t j = ((int64_t)docno[b + i] - dmin) >> kWBits;
+    const int64_t jp = i == 0 ? -1 : (((int64_t)docno[b + i - 1] - dmin) >> kWBits);
+    for (int64_t jj = jp + 1; jj <= j; jj++) row[jj] = (int32_t)i;
+    if (i == n - 1)
+      for (int64_t jj = j + 1; jj <= T; jj++) row[jj] = (int32_t)n;
+  }
+}
+// rows with df = 0 (possible only for empty terms) never get a posting: all zeros
+__global__ void k_skip_zero_rows(const int64_t *rdf, int64_t nrows, int64_t T, int32_t *sk) {
+  for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x)
+    if (rdf[r] == 0)
+      for (int64_t j = threadIdx.x; j <= T; j += blockDim.x) sk[r * (T + 1) + j] = 0;
+}
+
+// One WAVE per query (no block barriers at all): the wave's fp64 accumulators
+// for a tile of kWTile documents live in its own LDS slice, and a wave's LDS
+// operations execute in program order, so applying term i's postings before
+// term i+1's reproduces the reference's left-to-right sum without any
+// synchronisation.  Per tile: lanes < nt read the term's skip-table entries,
+// then the wave streams the tile's postings of all its terms in batches of
+// kWBatch 64-posting chunks (all loads of a batch in flight together), applies
+// them in query-token order, and folds the tile into per-lane register top-k
+// lists; the next tile is the smallest tile holding a remaining posting.
+template <int KMAX>
+__global__ __launch_bounds__(64) void k_query_wave(const int64_t *__restrict__ off, const int32_t *__restrict__ docno,
+                                                   const int32_t *__restrict__ tf, const double *__restrict__ lut,
+                                                   int max_tf, const double *__restrict__ idf,
+                                                   const int32_t *__restrict__ row_of, const int32_t *__restrict__ sk,
+                                                   int64_t dmin, int64_t T, const int32_t *__restrict__ terms,
+                                                   const int64_t *__restrict__ qoff, int nq, int k, int32_t *out_d,
+                                                   double *out_s) {
+  __shared__ double acc[kWTile];
+  __shared__ double s_lut[kWLut];
+  const int lane = threadIdx.x;
+  for (int j = lane; j < kWTile; j += 64) acc[j] = -1.0;  // untouched (weights are >= 0)
+  for (int j = lane; j < kWLut; j += 64) s_lut[j] = j <= max_tf ? lut[j] : 0.0;
+  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+    const int64_t q0 = qoff[q];
+    const int nt = (int)(qoff[q + 1] - q0);  // <= kTMaxTerms (host checked)
+    // lane i < nt holds term i: postings base, df, idf, skip row
+    int64_t mb = 0;
+    int32_t mdf = 0;
+    double midf = 0.0;
+    const int32_t *mrow = sk;
+    int32_t nx = 0x7FFFFFFF;
+    if (lane < nt) {
+      const int32_t t = terms[q0 + lane];
+      if (t >= 0) {
+        mb = off[t];
+        mdf = (int32_t)(off[t + 1] - mb);
+        midf = idf[t];
+        mrow = sk + (int64_t)row_of[t] * (T + 1);
+        if (mdf > 0) nx = (int32_t)(((int64_t)docno[mb] - dmin) >> kWBits);
+      }
+    }
+    double ts[KMAX];
+    int32_t td[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; j++) {
+      ts[j] = -INFINITY;
+      td[j] = 0x7FFFFFFF;
+    }
+    int32_t tile = nx;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tile = min(tile, __shfl_xor(tile, o, 64));
+    while (tile != 0x7FFFFFFF) {  // wave-uniform
+      int32_t mc = 0, me = 0;
+      if (lane < nt && mdf > 0) {
+        mc = mrow[tile];
+        me = mrow[tile + 1];
+      }
+      // next tile of this term (load overlaps the batch loads below)
+      nx = 0x7FFFFFFF;
+      if (lane < nt && me < mdf) nx = (int32_t)(((int64_t)docno[mb + me] - dmin) >> kWBits);
+      const int64_t dbase = dmin + ((int64_t)tile << kWBits);
+      // walk (term i, position s) over all chunks of the tile, kWBatch at a time
+      int i = 0;
+      int64_t s = __shfl(mb + mc, 0, 64), e = __shfl(mb + me, 0, 64);
+      while (i < nt) {
+        int32_t dv[kWBatch], fv[kWBatch];
+        int ti[kWBatch];
+#pragma unroll
+        for (int m = 0; m < kWBatch; m++) {
+          while (i < nt && s >= e) {  // advance to the next term with postings left in this tile
+            i++;
+            if (i < nt) {
+              s = __shfl(mb + mc, i, 64);
+              e = __shfl(mb + me, i, 64);
+            }
+          }
+          ti[m] = i;
+          const int64_t p = s + lane;
+          const bool v = i < nt && p < e;
+          dv[m] = v ? docno[p] : -1;
+          fv[m] = v ? tf[p] : 0;
+          s += 64;
+        }
+#pragma unroll
+        for (int m = 0; m < kWBatch; m++) {
+          const double widf = __shfl(midf, ti[m], 64);  // all lanes: ti[m] is wave-uniform
+          if (fv[m] == 0) continue;                       // tf >= 1 on every posting
+          const int d = (int)((int64_t)dv[m] - dbase);
+          const int f = fv[m];
+          const double l = f < kWLut ? s_lut[f] : lut[f];
+          const double w = __dmul_rn(l, widf);
+          const double a = acc[d];
+          acc[d] = a < 0.0 ? w : __dadd_rn(a, w);
+        }
+        while (i < nt && s >= e) {
+          i++;
+          if (i < nt) {
+            s = __shfl(mb + mc, i, 64);
+            e = __shfl(mb + me, i, 64);
+          }
+        }
+      }
+      for (int j = lane; j < kWTile; j += 64) {
+        const double sc = acc[j];
+        if (sc < 0.0) continue;
+        acc[j] = -1.0;
+        topk_insert<KMAX>(ts, td, sc, (int32_t)(dbase + j));
+      }
+      tile = nx;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) tile = min(tile, __shfl_xor(tile, o, 64));
+    }
+    // k rounds of wave arg-max over the lanes' list heads
     for (int r = 0; r < k; r++) {
       double bs = ts[0];
       int32_t bd = td[0];
-      int32_t bt = tid;
+      int32_t bt = lane;
+#pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
-        double os = __shfl_xor(bs, o, 64);
-        int32_t od = __shfl_xor(bd, o, 64), ot = __shfl_xor(bt, o, 64);
-        if (better(os, od, bs, bd)) {
+        const double os = __shfl_xor(bs, o, 64);
+        const int32_t od = __shfl_xor(bd, o, 64), ot = __shfl_xor(bt, o, 64);
+        if (better(os, od, bs, bd) || (os == bs && od == bd && ot < bt)) {
           bs = os;
           bd = od;
           bt = ot;
         }
       }
-      if (lane == 0) {
-        red_s[wave] = bs;
-        red_d[wave] = bd;
-        red_t[wave] = bt;
-      }
-      __syncthreads();
-      bs = red_s[0];
-      bd = red_d[0];
-      bt = red_t[0];
-      for (int x = 1; x < kQNT / 64; x++)
-        if (better(red_s[x], red_d[x], bs, bd)) {
-          bs = red_s[x];
-          bd = red_d[x];
-          bt = red_t[x];
-        }
-      if (tid == bt) {  // pop the head: shift the winner's list left
+      if (lane == bt) {
 #pragma unroll
         for (int j = 0; j < KMAX - 1; j++) {
           ts[j] = ts[j + 1];
@@ -214,12 +439,11 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
         ts[KMAX - 1] = -INFINITY;
         td[KMAX - 1] = 0x7FFFFFFF;
       }
-      if (tid == 0) {
+      if (lane == 0) {
         const bool valid = bs != -INFINITY;
         out_d[(int64_t)q * k + r] = valid ? bd : -1;
         out_s[(int64_t)q * k + r] = valid ? bs : 0.0;
       }
-      __syncthreads();
     }
   }
 }
@@ -227,28 +451,90 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k, int32_t *d_out_docno,
                 double *d_out_score, hipStream_t st) {
   if (k < 1) throw Error(SME_EINVAL, "k must be >= 1");
+  if (k > 32) throw Error(SME_ENOTIMPL, "top-k with k > 32 is not built yet");
   if (nq <= 0) return;
-  int *err = ix->ctx->ws[63].as<int>(4);
-  SME_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
+  auto &W = ix->ctx->ws;
+  int *err = W[63].as<int>(4);
+  SME_HIP(hipMemsetAsync(err, 0, 4 * sizeof(int), st));
   const int64_t *off = (const int64_t *)ix->d_off.p;
   const int32_t *dn = (const int32_t *)ix->d_docno_d.p;
   const int32_t *tf = (const int32_t *)ix->d_tf_d.p;
   const double *lut = (const double *)ix->d_lut.p;
   const double *idf = (const double *)ix->d_idf.p;
+  const int64_t V = ix->V;
   unsigned grid = (unsigned)std::min(nq, 1 << 20);
+  // Tiled path unless a query is longer than kTMaxTerms, tf does not pack, or the
+  // batch's skip table would be unreasonably large; SME_QUERY_KERNEL=stream forces
+  // the streaming kernel (tests run both).
+  const char *force = getenv("SME_QUERY_KERNEL");
+  bool tiled = V > 0 && ix->P > 0 && ix->dmax >= ix->dmin &&
+               !(force && strcmp(force, "stream") == 0);
+  const int64_t T = tiled ? ((ix->dmax - ix->dmin) >> kWBits) + 1 : 0;
+  const int32_t *row_of = nullptr, *sk = nullptr;
+  if (tiled) {
+    hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
+    int h_mx = 0;
+    SME_HIP(hipMemcpyAsync(&h_mx, err + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+    int64_t nterm = 0;
+    SME_HIP(hipMemcpyAsync(&nterm, d_qoff + nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    tiled = h_mx <= kTMaxTerms;
+    if (tiled) {
+      // distinct batch terms -> rows of the skip table
+      int32_t *mark = W[55].as<int32_t>(V + 1), *rowo = W[56].as<int32_t>(V + 1);
+      SME_HIP(hipMemsetAsync(mark, 0, (V + 1) * sizeof(int32_t), st));
+      if (nterm > 0)
+        hipLaunchKernelGGL(k_mark_terms, dim3((unsigned)std::min<int64_t>((nterm + 255) / 256, 8192)), dim3(256), 0, st,
+                           d_terms, nterm, V, mark);
+      size_t tbb = 0;
+      SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, mark, rowo, (int)V + 1, st));
+      SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, mark, rowo, (int)V + 1, st));
+      int32_t nrows32 = 0;
+      SME_HIP(hipMemcpyAsync(&nrows32, rowo + V, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+      SME_HIP(hipStreamSynchronize(st));
+      const int64_t nrows = nrows32;
+      if ((double)nrows * (double)(T + 1) * 4.0 > 8.0e9) {
+        tiled = false;
+      } else if (nrows > 0) {
+        int32_t *tor = W[57].as<int32_t>(nrows + 1);
+        int64_t *rdf = W[58].as<int64_t>(nrows + 1), *rpre = W[59].as<int64_t>(nrows + 1);
+        const unsigned gV = (unsigned)std::min<int64_t>((V + 255) / 256, 8192);
+        hipLaunchKernelGGL(k_term_rows, dim3(gV), dim3(256), 0, st, mark, rowo, V, off, tor, rdf);
+        SME_HIP(hipMemsetAsync(rdf + nrows, 0, sizeof(int64_t), st));
+        SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, rdf, rpre, (int)nrows + 1, st));
+        SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, rdf, rpre, (int)nrows + 1, st));
+        int32_t *skw = W[60].as<int32_t>(nrows * (T + 1));
+        hipLaunchKernelGGL(k_skip_zero_rows, dim3((unsigned)std::min<int64_t>(nrows, 4096)), dim3(256), 0, st, rdf,
+                           nrows, T, skw);
+        hipLaunchKernelGGL(k_skip_fill, dim3(8192), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T, skw);
+        SME_CHECK_LAUNCH();
+        row_of = rowo;
+        sk = skw;
+      } else {
+        row_of = rowo;
+        sk = W[60].as<int32_t>(T + 1);
+      }
+    }
+  }
   // events on the launch stream bracket the scoring kernel (bench.py roofline)
   hipEvent_t e0, e1;
   SME_HIP(hipEventCreate(&e0));
   SME_HIP(hipEventCreate(&e1));
   SME_HIP(hipEventRecord(e0, st));
-  if (k <= 16) {
-    hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff, nq, k,
-                       d_out_docno, d_out_score, err);
-  } else if (k <= 32) {
-    hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff, nq, k,
-                       d_out_docno, d_out_score, err);
+  if (tiled) {
+    const unsigned wgrid = (unsigned)std::min(nq, 1 << 22);
+    if (k <= 16)
+      hipLaunchKernelGGL(k_query_wave<16>, dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf, row_of, sk,
+                         ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score);
+    else
+      hipLaunchKernelGGL(k_query_wave<32>, dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf, row_of, sk,
+                         ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score);
+  } else if (k <= 16) {
+    hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff,
+                       nq, k, d_out_docno, d_out_score, err);
   } else {
-    throw Error(SME_ENOTIMPL, "top-k with k > 32 is not built yet");
+    hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff,
+                       nq, k, d_out_docno, d_out_score, err);
   }
   SME_CHECK_LAUNCH();
   SME_HIP(hipEventRecord(e1, st));
@@ -258,6 +544,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   float ms = 0;
   SME_HIP(hipEventElapsedTime(&ms, e0, e1));
   ix->ctx->last_query_ms = ms;
+  ix->ctx->last_query_tiled = tiled;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   if (h_err) throw Error(SME_ELIMIT, "a query has more than 128 terms");

@@ -144,6 +144,48 @@ def test_queries_vs_oracle(sme, synth, idf_mode):
         assert (dn[q, k:] == -1).all()
 
 
+def _query_both_kernels(ix, terms, qoff, k):
+    """Default (tiled) scoring and the streaming kernel: identical bits."""
+    dn, sc = ix.query_topk(terms, qoff, k)
+    os.environ["SME_QUERY_KERNEL"] = "stream"
+    try:
+        dn2, sc2 = ix.query_topk(terms, qoff, k)
+    finally:
+        del os.environ["SME_QUERY_KERNEL"]
+    assert np.array_equal(dn, dn2) and np.array_equal(sc, sc2)
+    return dn, sc
+
+
+def test_queries_multi_tile(sme, synth):
+    """Docnos spanning several 4096-document tiles, negative docnos (unmapped
+    docids, T14) below the mapped ones, unknown terms, a query longer than the
+    tiled kernel takes (falls back to the streaming kernel)."""
+    n = 9000
+    c = synth.gen_corpus(n, V=3000, seed=13, len_lo=8, len_hi=30)
+    ids = synth.docids(n)
+    mapped = [d for i, d in enumerate(ids) if i % 7 != 3]  # every 7th docid unmapped -> negative docno
+    ix, ref = _check_build(sme, c, mapped, R=1)
+    _, _, _, df = ix.csr()
+    names = [ix.term(i) for i in range(ix.V)]
+    tu, ou = synth.queries_by_df(df, 60, seed=5, uniform=True)
+    td_, od = synth.queries_by_df(df, 8, seed=6)
+    tu[::11] = -1
+    for terms, qoff in ((tu, ou), (td_, od)):
+        dn, sc = _query_both_kernels(ix, terms, qoff, 10)
+        for q in range(len(qoff) - 1):
+            tl = [names[t] for t in terms[qoff[q]:qoff[q + 1]] if t >= 0]
+            rd, rs = ref.query(tl, 10, 0, 0)
+            assert dn[q, :len(rd)].tolist() == rd, q
+            assert np.array_equal(sc[q, :len(rd)], np.array(rs)), q
+    # a 20-term query in the batch: whole batch through the streaming kernel
+    long_terms = np.concatenate([tu[:ou[3]], np.arange(20, dtype=np.int32)])
+    long_off = np.concatenate([ou[:4], [ou[3] + 20]]).astype(np.int64)
+    dn, sc = ix.query_topk(long_terms, long_off, 10)
+    tl = [names[t] for t in range(20)]
+    rd, rs = ref.query(tl, 10, 0, 0)
+    assert dn[3, :len(rd)].tolist() == rd and np.array_equal(sc[3, :len(rd)], np.array(rs))
+
+
 def test_single_term_queries_match_reference_sort(sme, synth):
     """For single-term queries the reference's Collections.sort on DocScore
     leaves the stored (tf desc, docno asc) order: equal to the docno tie-break."""
