@@ -212,15 +212,24 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     qstep()
     barrier()
     steps = max(1, a.steps // 2)
-    kms = []
+    kms, pms, kname = [], [], "k_query"
     t0 = time.perf_counter()
     for _ in range(steps):
+        tq = time.perf_counter()
         qstep()
-        kms.append(ix.ctx.last_build_profile().get("query_kernel"))
+        if os.environ.get("SME_BENCH_VERBOSE"):
+            torch.cuda.synchronize()
+            print("query step wall %.3f ms" % ((time.perf_counter() - tq) * 1e3), file=sys.stderr)
+        qp = ix.ctx.last_build_profile()
+        kms.append(qp.get("query_kernel"))
+        pms.append(qp.get("query_prep"))
+        kname = qp.get("query_kernel_name", kname)
     barrier()
     dt = (time.perf_counter() - t0) / steps
     kms = [x for x in kms if x is not None]
     qk_ms = sum(kms) / len(kms) if kms else None
+    pms = [x for x in pms if x is not None]
+    qp_ms = sum(pms) / len(pms) if pms else None
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -236,9 +245,11 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     t_k = (qk_ms * 1e-3) if qk_ms else dt
     return {"metric": "top-10 queries/sec", "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
             "terms_per_query": "U{2..8} drawn by df (seed 7)", "ms_per_batch": round(dt * 1e3, 3),
-            "roofline": {"bound": "hbm", "kernel": "k_query", "kernel_ms": qk_ms,
+            "prep_ms": qp_ms,
+            "prep_what": "per-batch skip table (distinct batch terms x 1024-doc tiles), inside ms_per_batch",
+            "roofline": {"bound": "hbm", "kernel": kname, "kernel_ms": qk_ms,
                          "achieved": round(alg / t_k / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(alg / t_k / 1e9 / HBM_PEAK_GBS, 6), "traffic": pmc_traffic("k_query", a),
+                         "frac": round(alg / t_k / 1e9 / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname, a),
                          "what": "A_q = 8*sum(df of distinct batch terms) + 4*sum|q| + 12*k*Q per launch / "
                                  "mean launch time (HIP events)"},
             "postings_touched_GBps": round(touched / t_k / 1e9, 2),

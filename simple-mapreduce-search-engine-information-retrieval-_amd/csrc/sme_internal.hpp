@@ -25,6 +25,7 @@ struct sme_ctx {
   std::vector<std::pair<std::string, float>> last_profile;
   std::vector<uint8_t> mapping_out;  // last sme_number_documents result
   float last_query_ms = -1.0f;  // device time of the last query kernel launch
+  float last_query_prep_ms = -1.0f;  // skip-table preparation before it (wave kernel only)
   bool last_query_tiled = false;  // which scoring kernel it was (k_query_tiled / k_query)
   // indexes borrow the context (its pool, workspace, stream): sme_destroy defers
   // the delete until the last index is freed, whatever order a host frees them in

@@ -68,6 +68,13 @@ __device__ __forceinline__ void topk_insert(double (&ts)[K], int32_t (&td)[K], d
   }
 }
 
+// 64-bit value of lane l (l wave-uniform) as a scalar
+__device__ __forceinline__ int64_t rl64(int64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // merge the per-lane lists: k rounds of block arg-max over list heads; thread 0
 // writes query q's k results (docno -1 / score 0 padding)
 template <int KMAX>
@@ -250,7 +257,7 @@ constexpr int kTMaxTerms = 16;  // queries with more terms go through k_query
 constexpr int kWBits = 10;      // tile = 1024 documents: 8 KiB of fp64 accumulators per wave
 constexpr int kWTile = 1 << kWBits;
 constexpr int kWLut = 128;      // 1 + ln(tf) for tf < 128 from LDS
-constexpr int kWBatch = 8;      // 64-posting chunks in flight per wave
+constexpr int kWBatchDefault = 8;  // 64-posting chunks in flight per wave
 
 __global__ void k_mark_terms(const int32_t *terms, int64_t n, int64_t V, int32_t *mark) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -274,26 +281,59 @@ __global__ void k_max_qlen(const int64_t *qoff, int nq, int *mx) {
   for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
   if ((threadIdx.x & 63) == 0) atomicMax(mx, m);
 }
-// sk[row * (T + 1) + j] = first posting (term-relative) with tile >= j; every
-// entry is written exactly once: posting p covers tiles (tile(p-1), tile(p)],
-// the last posting also (tile(last), T].
-__global__ void k_skip_fill(const int64_t *rpre, int64_t nrows, const int32_t *term_of_row, const int64_t *off,
-                            const int32_t *docno, int64_t dmin, int64_t T, int32_t *sk) {
+// sk[row * (T + 1) + j] = first posting (term-relative) with tile >= j.  The
+// table starts as "infinity" with sk[row][T] = df; every posting that opens a
+// tile writes its index there (a change point), and a backward min-scan per
+// row fills the gaps (k_skip_suffix).
+constexpr int kSkipChunk = 2048;  // postings per block in k_skip_fill
+__global__ __launch_bounds__(256) void k_skip_fill(const int64_t *rpre, int64_t nrows, const int32_t *term_of_row,
+                                                   const int64_t *off, const int32_t *docno, int64_t dmin, int64_t T,
+                                                   int32_t *sk) {
   const int64_t total = rpre[nrows];
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total; x += (int64_t)gridDim.x * blockDim.x) {
-    int64_t lo = 0, hi = nrows;  // rpre[lo] <= x < rpre[hi]
+  for (int64_t x0 = (int64_t)blockIdx.x * kSkipChunk; x0 < total; x0 += (int64_t)gridDim.x * kSkipChunk) {
+    const int64_t x1 = x0 + kSkipChunk < total ? x0 + kSkipChunk : total;
+    int64_t lo = 0, hi = nrows;  // row of x0: rpre[lo] <= x0 < rpre[hi] (same in every thread)
     while (hi - lo > 1) {
       const int64_t m = (lo + hi) >> 1;
-      if (rpre[m] <= x) lo = m;
+      if (rpre[m] <= x0) lo = m;
       else hi = m;
     }
-    const int64_t b = off[term_of_row[lo]], i = x - rpre[lo], n = rpre[lo + 1] - rpre[lo];
-    int32_t *row = sk + lo * (T + 1);
-    const int64_t j = ((int64_t)docno[b + i] - dmin) >> kWBits;
-    const int64_t jp = i == 0 ? -1 : (((int64_t)docno[b + i - 1] - dmin) >> kWBits);
-    for (int64_t jj = jp + 1; jj <= j; jj++) row[jj] = (int32_t)i;
-    if (i == n - 1)
-      for (int64_t jj = j + 1; jj <= T; jj++) row[jj] = (int32_t)n;
+    int64_t row = lo, rb = rpre[row], re = rpre[row + 1], b = off[term_of_row[row]];
+    for (int64_t x = x0 + threadIdx.x; x < x1; x += blockDim.x) {
+      while (x >= re) {  // the chunk crosses into later rows
+        row++;
+        rb = re;
+        re = rpre[row + 1];
+        b = off[term_of_row[row]];
+      }
+      const int64_t i = x - rb, n = re - rb;
+      int32_t *r = sk + row * (T + 1);
+      const int64_t j = ((int64_t)docno[b + i] - dmin) >> kWBits;
+      const int64_t jp = i == 0 ? -1 : (((int64_t)docno[b + i - 1] - dmin) >> kWBits);
+      if (jp < j) r[j] = (int32_t)i;
+      if (i == n - 1) r[T] = (int32_t)n;
+    }
+  }
+}
+// one wave per row: suffix minimum from j = T down to 0, 64 entries at a time
+__global__ __launch_bounds__(256) void k_skip_suffix(int64_t nrows, int64_t T, int32_t *sk) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < nrows; r += nw) {
+    int32_t *row = sk + r * (T + 1);
+    int32_t carry = 0x7FFFFFFF;
+    for (int64_t j1 = T + 1; j1 > 0; j1 -= 64) {
+      const int64_t j = j1 - 1 - lane;  // lane 0 = highest index of the chunk
+      int32_t v = j >= 0 ? row[j] : 0x7FFFFFFF;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int32_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v = min(v, u);
+      }
+      v = min(v, carry);
+      if (j >= 0) row[j] = v;
+      carry = __shfl(v, 63, 64);
+    }
   }
 }
 // rows with df = 0 (possible only for empty terms) never get a posting: all zeros
@@ -312,7 +352,7 @@ __global__ void k_skip_zero_rows(const int64_t *rdf, int64_t nrows, int64_t T, i
 // kWBatch 64-posting chunks (all loads of a batch in flight together), applies
 // them in query-token order, and folds the tile into per-lane register top-k
 // lists; the next tile is the smallest tile holding a remaining posting.
-template <int KMAX>
+template <int KMAX, int kWBatch>
 __global__ __launch_bounds__(64) void k_query_wave(const int64_t *__restrict__ off, const int32_t *__restrict__ docno,
                                                    const int32_t *__restrict__ tf, const double *__restrict__ lut,
                                                    int max_tf, const double *__restrict__ idf,
@@ -354,15 +394,22 @@ __global__ __launch_bounds__(64) void k_query_wave(const int64_t *__restrict__ o
     int32_t tile = nx;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) tile = min(tile, __shfl_xor(tile, o, 64));
+    int32_t mc = 0, me = 0;
+    if (tile != 0x7FFFFFFF && lane < nt && mdf > 0) {
+      mc = mrow[tile];
+      me = mrow[tile + 1];
+    }
     while (tile != 0x7FFFFFFF) {  // wave-uniform
-      int32_t mc = 0, me = 0;
-      if (lane < nt && mdf > 0) {
-        mc = mrow[tile];
-        me = mrow[tile + 1];
-      }
-      // next tile of this term (load overlaps the batch loads below)
+      // loads for the next step overlap this tile's batch loads: the next tile
+      // of this term, and (for the common case that it is tile + 1) its range end
       nx = 0x7FFFFFFF;
-      if (lane < nt && me < mdf) nx = (int32_t)(((int64_t)docno[mb + me] - dmin) >> kWBits);
+      int32_t me1 = 0;
+      if (lane < nt && me < mdf) {
+        nx = (int32_t)(((int64_t)docno[mb + me] - dmin) >> kWBits);
+        me1 = tile + 2 <= T ? mrow[tile + 2] : mdf;
+      } else if (lane < nt) {
+        me1 = mdf;
+      }
       const int64_t dbase = dmin + ((int64_t)tile << kWBits);
       // walk (term i, position s) over all chunks of the tile, kWBatch at a time
       int i = 0;
@@ -411,9 +458,17 @@ __global__ __launch_bounds__(64) void k_query_wave(const int64_t *__restrict__ o
         acc[j] = -1.0;
         topk_insert<KMAX>(ts, td, sc, (int32_t)(dbase + j));
       }
-      tile = nx;
+      int32_t nt_ = nx;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) tile = min(tile, __shfl_xor(tile, o, 64));
+      for (int o = 32; o > 0; o >>= 1) nt_ = min(nt_, __shfl_xor(nt_, o, 64));
+      if (nt_ == tile + 1) {
+        mc = me;
+        me = me1;
+      } else if (nt_ != 0x7FFFFFFF && lane < nt && mdf > 0) {
+        mc = mrow[nt_];
+        me = mrow[nt_ + 1];
+      }
+      tile = nt_;
     }
     // k rounds of wave arg-max over the lanes' list heads
     for (int r = 0; r < k; r++) {
@@ -463,6 +518,9 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   const double *idf = (const double *)ix->d_idf.p;
   const int64_t V = ix->V;
   unsigned grid = (unsigned)std::min(nq, 1 << 20);
+  hipEvent_t ep;
+  SME_HIP(hipEventCreate(&ep));
+  SME_HIP(hipEventRecord(ep, st));
   // Tiled path unless a query is longer than kTMaxTerms, tf does not pack, or the
   // batch's skip table would be unreasonably large; SME_QUERY_KERNEL=stream forces
   // the streaming kernel (tests run both).
@@ -504,9 +562,12 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
         SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, rdf, rpre, (int)nrows + 1, st));
         SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, rdf, rpre, (int)nrows + 1, st));
         int32_t *skw = W[60].as<int32_t>(nrows * (T + 1));
+        SME_HIP(hipMemsetAsync(skw, 0x7F, (size_t)nrows * (T + 1) * sizeof(int32_t), st));
         hipLaunchKernelGGL(k_skip_zero_rows, dim3((unsigned)std::min<int64_t>(nrows, 4096)), dim3(256), 0, st, rdf,
                            nrows, T, skw);
-        hipLaunchKernelGGL(k_skip_fill, dim3(8192), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T, skw);
+        hipLaunchKernelGGL(k_skip_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T, skw);
+        hipLaunchKernelGGL(k_skip_suffix, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 16384)), dim3(256), 0, st,
+                           nrows, T, skw);
         SME_CHECK_LAUNCH();
         row_of = rowo;
         sk = skw;
@@ -523,12 +584,19 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   SME_HIP(hipEventRecord(e0, st));
   if (tiled) {
     const unsigned wgrid = (unsigned)std::min(nq, 1 << 22);
-    if (k <= 16)
-      hipLaunchKernelGGL(k_query_wave<16>, dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf, row_of, sk,
-                         ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score);
-    else
-      hipLaunchKernelGGL(k_query_wave<32>, dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf, row_of, sk,
-                         ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score);
+    const char *eb = getenv("SME_QBATCH");
+    const int bsel = eb ? atoi(eb) : kWBatchDefault;
+#define SME_QW(KM, BT)                                                                                                \
+  hipLaunchKernelGGL((k_query_wave<KM, BT>), dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf, row_of, sk, \
+                     ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score)
+    if (k <= 16) {
+      if (bsel == 16) SME_QW(16, 16);
+      else if (bsel == 4) SME_QW(16, 4);
+      else SME_QW(16, 8);
+    } else {
+      SME_QW(32, 8);
+    }
+#undef SME_QW
   } else if (k <= 16) {
     hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff,
                        nq, k, d_out_docno, d_out_score, err);
@@ -541,9 +609,12 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   int h_err = 0;
   SME_HIP(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, st));
   SME_HIP(hipStreamSynchronize(st));
-  float ms = 0;
+  float ms = 0, pms = 0;
   SME_HIP(hipEventElapsedTime(&ms, e0, e1));
+  SME_HIP(hipEventElapsedTime(&pms, ep, e0));
   ix->ctx->last_query_ms = ms;
+  ix->ctx->last_query_prep_ms = pms;
+  (void)hipEventDestroy(ep);
   ix->ctx->last_query_tiled = tiled;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
