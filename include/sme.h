@@ -91,6 +91,21 @@ int sme_build_index(sme_ctx *ctx, const uint8_t *corpus, size_t nbytes, sme_inde
 int sme_build_index_device(sme_ctx *ctx, const void *d_corpus, size_t nbytes, void *stream,
                            sme_index **out);
 
+/* CharKGramTermIndexer (C/sa/edu/kaust/indexing/CharKGramTermIndexer.java:74-211, the
+ * other PA2-3 job): k = cfg.k (1..5) character k-grams of every '$'+token+'$', each
+ * mapped to the set of tokens containing it (JDK 6 HashSet iteration order), written
+ * as TextOutputFormat lines "gram\t[t1, t2, ...]\n" into cfg.num_partitions
+ * HashPartitioner partitions in Text key order.  One split (one map task); no docno
+ * mapping is needed (the job's mapper never reads docids).  The result is an
+ * sme_index whose only accessors are the two below and sme_index_free. */
+int sme_build_chargram(sme_ctx *ctx, const uint8_t *corpus, size_t nbytes, sme_index **out);
+int sme_build_chargram_device(sme_ctx *ctx, const void *d_corpus, size_t nbytes, void *stream,
+                              sme_index **out);
+/* part-NNNNN text bytes of reduce partition `part` (host buffer owned by the index) */
+int sme_chargram_partition_text(sme_index *ix, int part, const uint8_t **buf, size_t *n);
+/* distinct k-grams (output lines) and (k-gram, token) set entries */
+int sme_chargram_stats(const sme_index *ix, uint64_t *ngrams, uint64_t *npairs);
+
 void sme_index_free(sme_index *ix);
 
 /* N = records mapped (= df of the " " doc-counter key), V = distinct terms

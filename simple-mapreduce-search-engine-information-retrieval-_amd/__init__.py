@@ -43,6 +43,7 @@ EXPORTS = [
     "sme_build_index_device", "sme_index_free", "sme_index_stats", "sme_index_partition_records", "sme_index_csr",
     "sme_index_device_arrays", "sme_index_term", "sme_tokenize", "sme_lookup_terms", "sme_query_topk",
     "sme_query_topk_device", "sme_last_build_profile", "sme_index_reweight", "sme_number_documents",
+    "sme_build_chargram", "sme_build_chargram_device", "sme_chargram_partition_text", "sme_chargram_stats",
 ]
 
 
@@ -77,6 +78,10 @@ def lib():
     L.sme_last_build_profile.argtypes = [vp, C.POINTER(C.c_char_p)]
     L.sme_index_reweight.argtypes = [vp, C.c_int64, vp, vp]
     L.sme_number_documents.argtypes = [vp, C.c_char_p, sz, C.POINTER(vp), C.POINTER(sz)]
+    L.sme_build_chargram.argtypes = [vp, C.c_char_p, sz, C.POINTER(vp)]
+    L.sme_build_chargram_device.argtypes = [vp, vp, sz, vp, C.POINTER(vp)]
+    L.sme_chargram_partition_text.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
+    L.sme_chargram_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     _lib = L
     return L
 
@@ -156,6 +161,18 @@ class Context:
         _check(lib().sme_build_index_device(self._h, C.c_void_p(d_ptr), nbytes, C.c_void_p(stream or 0),
                                             C.byref(h)))
         return Index(h, self)
+
+    def build_chargram(self, corpus):
+        """CharKGramTermIndexer over host bytes (k = this context's k, R = num_partitions)."""
+        h = C.c_void_p()
+        _check(lib().sme_build_chargram(self._h, corpus, len(corpus), C.byref(h)))
+        return CharGramOutput(h, self)
+
+    def build_chargram_device(self, d_ptr, nbytes, stream=None):
+        h = C.c_void_p()
+        _check(lib().sme_build_chargram_device(self._h, C.c_void_p(d_ptr), nbytes, C.c_void_p(stream or 0),
+                                               C.byref(h)))
+        return CharGramOutput(h, self)
 
     def last_build_profile(self):
         import json
@@ -252,6 +269,29 @@ class Index:
 
 
 # ---------------------------------------------------------------------------
+class CharGramOutput:
+    """Output of the CharKGramTermIndexer job: the text of every reduce partition."""
+
+    def __init__(self, h, ctx):
+        self._h, self.ctx = h, ctx
+        a, b = C.c_uint64(), C.c_uint64()
+        _check(lib().sme_chargram_stats(h, C.byref(a), C.byref(b)))
+        self.ngrams, self.npairs = a.value, b.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().sme_index_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def partition_text(self, part):
+        p, n = C.c_void_p(), C.c_size_t()
+        _check(lib().sme_chargram_partition_text(self._h, part, C.byref(p), C.byref(n)))
+        return C.string_at(p, n.value) if n.value else b""
+
+
 # reference-shaped facades
 class GalagoTokenizer:
     """GalagoTokenizer.processContent, evaluated by the device tokenizer."""
@@ -298,6 +338,24 @@ class TermKGramDocIndexer:
             from . import seqfile
             seqfile.write_index_dir(ix, output_dir)
         return ix
+
+
+class CharKGramTermIndexer:
+    """CharKGramTermIndexer.run(K, input, output) as one device call (R = 10 reducers
+    as the reference's run() sets); writes part-NNNNN text files if output_dir is given."""
+
+    def __init__(self, k=2, num_reduce_tasks=10, device=0):
+        self.ctx = Context(k, num_reduce_tasks, SME_IDF_REFERENCE, device)
+
+    def run(self, corpus, output_dir=None):
+        corpus = open(corpus, "rb").read() if isinstance(corpus, str) else corpus
+        out = self.ctx.build_chargram(corpus)
+        if output_dir is not None:
+            os.makedirs(output_dir, exist_ok=True)
+            for p in range(self.ctx.num_partitions):
+                with open(os.path.join(output_dir, "part-%05d" % p), "wb") as f:
+                    f.write(out.partition_text(p))
+        return out
 
 
 class IntDocVectorsForwardIndex:

@@ -228,6 +228,46 @@ int sme_build_index_device(sme_ctx *cx, const void *d_corpus, size_t nbytes, voi
   });
 }
 
+int sme_build_chargram_device(sme_ctx *cx, const void *d_corpus, size_t nbytes, void *stream, sme_index **out) {
+  return guard([&] {
+    if (!cx || !out || (!d_corpus && nbytes)) throw sme::Error(SME_EINVAL, "null argument");
+    set_device(cx);
+    hipStream_t st = stream_of(cx, stream);
+    sme_index *ix = sme::build_index(cx, (const uint8_t *)d_corpus, nbytes, st, 1);
+    cx->last_profile = ix->profile;
+    *out = ix;
+  });
+}
+
+int sme_build_chargram(sme_ctx *cx, const uint8_t *corpus, size_t nbytes, sme_index **out) {
+  return guard([&] {
+    if (!cx || !out || (!corpus && nbytes)) throw sme::Error(SME_EINVAL, "null argument");
+    set_device(cx);
+    hipStream_t st = cx->own_stream;
+    sme::DevBuf buf;
+    uint8_t *d = buf.as<uint8_t>(nbytes + 16);
+    if (nbytes) SME_HIP(hipMemcpyAsync(d, corpus, nbytes, hipMemcpyHostToDevice, st));
+    sme_index *ix = sme::build_index(cx, d, nbytes, st, 1);
+    SME_HIP(hipStreamSynchronize(st));
+    cx->last_profile = ix->profile;
+    *out = ix;
+  });
+}
+
+int sme_chargram_stats(const sme_index *ix, uint64_t *ngrams, uint64_t *npairs) {
+  return guard([&] {
+    if (!ix || !ngrams || !npairs) throw sme::Error(SME_EINVAL, "null argument");
+    if (ix->job != 1) throw sme::Error(SME_EINVAL, "not a CharKGramTermIndexer output");
+    *ngrams = (uint64_t)ix->cg_ngrams;
+    *npairs = (uint64_t)ix->cg_pairs;
+  });
+}
+
+int sme_chargram_partition_text(sme_index *ix, int part, const uint8_t **buf, size_t *n) {
+  if (ix && ix->job != 1) return fail(SME_EINVAL, "not a CharKGramTermIndexer output");
+  return sme_index_partition_records(ix, part, buf, n);
+}
+
 int sme_build_index(sme_ctx *cx, const uint8_t *corpus, size_t nbytes, sme_index **out) {
   return guard([&] {
     if (!cx || !out || (!corpus && nbytes)) throw sme::Error(SME_EINVAL, "null argument");

@@ -2047,33 +2047,6 @@ __global__ __launch_bounds__(256) void k_tf_tile_place(const int64_t *__restrict
 // ============================================================================
 // host orchestration
 // ============================================================================
-struct Prof {
-  hipStream_t st;
-  std::vector<std::pair<std::string, hipEvent_t>> ev;
-  explicit Prof(hipStream_t s) : st(s) { mark("start"); }
-  void mark(const char *name) {
-    hipEvent_t e;
-    SME_HIP(hipEventCreate(&e));
-    SME_HIP(hipEventRecord(e, st));
-    ev.emplace_back(name, e);
-  }
-  std::vector<std::pair<std::string, float>> finish() {
-    SME_HIP(hipEventSynchronize(ev.back().second));
-    std::vector<std::pair<std::string, float>> out;
-    for (size_t i = 1; i < ev.size(); i++) {
-      float ms = 0;
-      SME_HIP(hipEventElapsedTime(&ms, ev[i - 1].second, ev[i].second));
-      out.emplace_back(ev[i].first, ms);
-    }
-    float tot = 0;
-    SME_HIP(hipEventElapsedTime(&tot, ev.front().second, ev.back().second));
-    out.emplace_back("total", tot);
-    for (auto &p : ev) (void)hipEventDestroy(p.second);
-    ev.clear();
-    return out;
-  }
-};
-
 static int grid_for(int64_t n, int nt = 256, int cap = 8192) {
   int64_t g = (n + nt - 1) / nt;
   if (g < 1) g = 1;
@@ -2194,8 +2167,15 @@ RecordSpans find_records(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t 
   return RecordSpans{rs, re, nR, C, nC};
 }
 
-sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st) {
-  if (!cx->has_map) throw Error(SME_ENOMAP, "no docno mapping loaded (sme_load_docno_mapping)");
+__global__ void k_iota_docno(int32_t *d, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = (int32_t)(i + 1);
+}
+
+sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st, int job) {
+  // job 0: TermKGramDocIndexer; job 1: CharKGramTermIndexer (no docnos: its mapper
+  // never calls getDocid, and records stay in file order = the map task's order)
+  if (job == 0 && !cx->has_map) throw Error(SME_ENOMAP, "no docno mapping loaded (sme_load_docno_mapping)");
   DevBuf *W = cx->ws + kBuildWs;
   Prof prof(st);
   auto cub_tmp = [&](size_t bytes) { return cx->cub_tmp.get(bytes); };
@@ -2208,10 +2188,12 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   // ---------------- K2 docno ----------------
   int32_t *docno = W[W_DOCNO].as<int32_t>(nR + 1);
   SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
-  if (nR > 0) {
+  if (nR > 0 && job == 0) {
     hipLaunchKernelGGL(k_docno, dim3(grid_for(nR)), dim3(256), 0, st, t, rs, re, nR,
                        (const uint16_t *)cx->map_chars.p, (const int64_t *)cx->map_off.p, cx->map_n, docno, cnt);
     SME_CHECK_LAUNCH();
+  } else if (nR > 0) {
+    hipLaunchKernelGGL(k_iota_docno, dim3(grid_for(nR)), dim3(256), 0, st, docno, nR);
   }
   uint8_t *slow = W[W_SLOW].as<uint8_t>(nR + 1);
   if (nR > 0) {
@@ -2478,6 +2460,37 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   }
   SME_CHECK_LAUNCH();
   prof.mark("vocabulary");
+  if (job == 1) {
+    // CharKGramTermIndexer: term stream in file order, then the char k-gram stage
+    AggIn ai;
+    ai.rs = rs;
+    ai.tokstream = tok;
+    ai.ntok = ntok;
+    ai.raw_term = raw_term;
+    ai.raw_nout = co.raw_nout;
+    ai.multi_term = multi;
+    ai.perm = perm;  // identity (docno = record index + 1)
+    ai.docno = docno;
+    const unsigned g_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
+    int64_t *tcnt = W[W_T2].as<int64_t>(nR + 1), *toff = W[W_T3].as<int64_t>(nR + 1);
+    if (nR > 0) hipLaunchKernelGGL(k_tcount, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, tcnt);
+    SME_HIP(hipMemsetAsync(tcnt + nR, 0, sizeof(int64_t), st));
+    size_t tbb = 0;
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, tcnt, toff, (int)nR + 1, st));
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, tcnt, toff, (int)nR + 1, st));
+    const int64_t M = d2h(toff + nR, st);
+    int32_t *tstream = W[W_U16].as<int32_t>(M + 1);
+    if (nR > 0) hipLaunchKernelGGL(k_twrite, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, toff, tstream);
+    SME_CHECK_LAUNCH();
+    prof.mark("term_stream");
+    chargram_stage(cx, ix, tstream, M, V, term_off, (const uint16_t *)ix->d_term_chars.p, st, &prof);
+    ix->N = nR;
+    ix->V = V;
+    ix->Vt = V;
+    ix->profile = prof.finish();
+    ix_guard.release();
+    return ix;
+  }
 
   // ---------------- K5 aggregation ----------------
   const int K = cx->cfg.k;

@@ -36,6 +36,8 @@ struct sme_ctx {
 struct sme_index {
   sme_ctx *ctx = nullptr;
   int K = 1, R = 1, idf_mode = 0;
+  int job = 0;               // 0 TermKGramDocIndexer index, 1 CharKGramTermIndexer output
+  int64_t cg_ngrams = 0, cg_pairs = 0;  // job 1: distinct char k-grams, (gram, term) set entries
   int64_t N = 0, V = 0, P = 0;
   int64_t Vt = 0;  // term vocabulary size (V counts k-grams when K > 1)
   int32_t max_tf = 0;
@@ -83,7 +85,34 @@ struct sme_index {
 };
 
 namespace sme {
-struct Prof;  // per-stage device-event timer (sme_build.hip)
+// per-stage device-event timer of a build
+struct Prof {
+  hipStream_t st;
+  std::vector<std::pair<std::string, hipEvent_t>> ev;
+  explicit Prof(hipStream_t s) : st(s) { mark("start"); }
+  void mark(const char *name) {
+    hipEvent_t e;
+    SME_HIP(hipEventCreate(&e));
+    SME_HIP(hipEventRecord(e, st));
+    ev.emplace_back(name, e);
+  }
+  std::vector<std::pair<std::string, float>> finish() {
+    SME_HIP(hipEventSynchronize(ev.back().second));
+    std::vector<std::pair<std::string, float>> out;
+    for (size_t i = 1; i < ev.size(); i++) {
+      float ms = 0;
+      SME_HIP(hipEventElapsedTime(&ms, ev[i - 1].second, ev[i].second));
+      out.emplace_back(ev[i].first, ms);
+    }
+    float tot = 0;
+    SME_HIP(hipEventElapsedTime(&tot, ev.front().second, ev.back().second));
+    out.emplace_back("total", tot);
+    for (auto &p : ev) (void)hipEventDestroy(p.second);
+    ev.clear();
+    return out;
+  }
+};
+
 struct RecordSpans {
   uint64_t *rs, *re;  // record [rs, re) byte spans, in reader order
   int64_t nR;
@@ -92,7 +121,10 @@ struct RecordSpans {
 };
 RecordSpans find_records(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, Prof *prof);
 void number_documents(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, std::vector<uint8_t> &out);
-sme_index *build_index(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st);
+sme_index *build_index(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, int job = 0);
+// CharKGramTermIndexer stage over the file-order term stream (sme_chargram.hip)
+void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t M, int64_t V, const int64_t *term_off,
+                    const uint16_t *term_chars, hipStream_t st, Prof *prof);
 void serialize_index(sme_index *ix, hipStream_t st);
 void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t st);
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k,

@@ -41,6 +41,16 @@ def lib():
                                     C.c_void_p, C.c_void_p]
         L.or_last_error.restype = C.c_char_p
         L.or_split_records.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]
+        L.or_chargram.restype = C.c_void_p
+        L.or_chargram.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int]
+        L.or_chargram_ngrams.argtypes = [C.c_void_p]
+        L.or_chargram_npairs.argtypes = [C.c_void_p]
+        L.or_chargram_npairs.restype = C.c_longlong
+        L.or_chargram_part_len.argtypes = [C.c_void_p, C.c_int]
+        L.or_chargram_part_len.restype = C.c_size_t
+        L.or_chargram_part_bytes.argtypes = [C.c_void_p, C.c_int]
+        L.or_chargram_part_bytes.restype = C.c_void_p
+        L.or_chargram_free.argtypes = [C.c_void_p]
         _lib = L
     return _lib
 
@@ -171,6 +181,28 @@ class OracleIndex:
         sc = (C.c_double * max(k, 1))()
         r = lib().or_query_utf8(self._h, blob, o, len(terms), k, idf_mode, order, dn, sc)
         return [dn[i] for i in range(r)], [sc[i] for i in range(r)]
+
+
+class OracleCharGram:
+    """CharKGramTermIndexer restated on the CPU (oracle/oracle_chargram.c): the
+    TextOutputFormat bytes of every reduce partition."""
+
+    def __init__(self, corpus, k, R):
+        self.R = R
+        self._h = lib().or_chargram(corpus, len(corpus), k, R)
+        if not self._h:
+            raise ValueError("bad k/R")
+        self.ngrams = lib().or_chargram_ngrams(self._h)
+        self.npairs = lib().or_chargram_npairs(self._h)
+
+    def part_bytes(self, p):
+        n = lib().or_chargram_part_len(self._h, p)
+        return C.string_at(lib().or_chargram_part_bytes(self._h, p), n) if n else b""
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().or_chargram_free(self._h)
+            self._h = None
 
 
 def write_mapping(docids):

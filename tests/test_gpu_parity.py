@@ -299,3 +299,41 @@ def test_number_documents(sme, synth):
     ctx.load_docno_mapping(ctx.number_documents(fz))
     ix = ctx.build(fz)
     assert ix.N == O.OracleIndex(fz, ctx.number_documents(fz), 1, 1).N
+
+
+# ---- CharKGramTermIndexer on the device (C/sa/edu/kaust/indexing/CharKGramTermIndexer.java:74-211) ----
+def _check_chargram(sme, corpus, k, R):
+    ref = O.OracleCharGram(corpus, k, R)
+    ctx = sme.Context(k, R)
+    out = ctx.build_chargram(corpus)
+    assert (out.ngrams, out.npairs) == (ref.ngrams, ref.npairs)
+    for p in range(R):
+        assert out.partition_text(p) == ref.part_bytes(p), p
+    return out
+
+
+def test_chargram_kat(sme):
+    corpus = b"<DOC><DOCNO>A</DOCNO> bats cats dog </DOC>\n<DOC><DOCNO>B</DOCNO> cat bat </DOC>"
+    out = _check_chargram(sme, corpus, 2, 1)
+    assert b"at\t[cat, bat]\n" in out.partition_text(0)
+
+
+@pytest.mark.parametrize("k,R", [(1, 1), (2, 10), (3, 3), (5, 2)])
+def test_chargram_fuzz(sme, k, R):
+    corpus, _ = common.fuzz_corpus(20 + k, 120)
+    _check_chargram(sme, corpus, k, R)
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_chargram_synthetic(sme, synth, k):
+    """Zipfian vocabulary: sets of thousands of terms (many JDK 6 resizes)."""
+    c = synth.gen_corpus(300, V=4000, seed=31, len_lo=40, len_hi=120)
+    _check_chargram(sme, c, k, 10)
+
+
+def test_chargram_empty(sme):
+    ctx = sme.Context(2, 3)
+    out = ctx.build_chargram(b"no records")
+    assert (out.ngrams, out.npairs) == (0, 0) and out.partition_text(2) == b""
+    out = ctx.build_chargram(b"<DOC><DOCNO>A</DOCNO> the of </DOC>")  # stopwords only
+    assert out.ngrams == 0

@@ -109,3 +109,29 @@ def test_duplicate_docids_merge():
     ix = O.OracleIndex(corpus, O.write_mapping(["A", "B"]), 1, 1)
     w = [p for g, _, _, p in ix.terms() if g == ("wolf",)][0]
     assert w == [(1, 3), (2, 1)]
+
+
+# ---- CharKGramTermIndexer (C/sa/edu/kaust/indexing/CharKGramTermIndexer.java:74-211) ----
+def test_chargram_kat():
+    """Hand-derived: "bats cats dog" then "cat bat", k=2, R=1.  The set of "at" is
+    inserted bat-then-cat, but JDK 6 HashSet iteration puts cat (bucket 2 of 16:
+    spread("cat".hashCode()=98262) & 15) before bat (bucket 10: spread(97301) & 15)."""
+    corpus = b"<DOC><DOCNO>A</DOCNO> bats cats dog </DOC>\n<DOC><DOCNO>B</DOCNO> cat bat </DOC>"
+    o = O.OracleCharGram(corpus, 2, 1)
+    assert o.part_bytes(0) == (b"$b\t[bat]\n$c\t[cat]\n$d\t[dog]\nat\t[cat, bat]\nba\t[bat]\nca\t[cat]\n"
+                               b"do\t[dog]\ng$\t[dog]\nog\t[dog]\nt$\t[cat, bat]\n")
+    assert (o.ngrams, o.npairs) == (10, 12)
+
+
+@pytest.mark.parametrize("k,R", [(1, 1), (2, 10), (3, 3), (4, 1)])
+def test_chargram_oracle_vs_python(k, R):
+    """The C oracle (direct JDK 6 HashMap simulation) against the pure-Python
+    restatement on fuzzed corpora: sets > 12 and > 24 members (resizes), non-ASCII,
+    surrogate pairs cut by a gram, markup."""
+    import common
+    import pyref_chargram as P
+    corpus, _ = common.fuzz_corpus(7 + k, 60)
+    o = O.OracleCharGram(corpus, k, R)
+    exp = P.chargram_parts(corpus, k, R)
+    for p in range(R):
+        assert o.part_bytes(p) == exp[p], p
