@@ -211,7 +211,7 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
 
     qstep()
     barrier()
-    steps = max(1, a.steps // 2)
+    steps = max(3, a.steps // 2)
     kms, pms, kname = [], [], "k_query"
     t0 = time.perf_counter()
     for _ in range(steps):

@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+#include <algorithm>
+
 #include "sme_internal.hpp"
 
 namespace {
@@ -200,6 +202,12 @@ int sme_load_docno_mapping(sme_ctx *cx, const uint8_t *m, size_t n) {
     SME_HIP(hipStreamSynchronize(st));
     cx->map_n = (int64_t)off.size() - 1;
     cx->has_map = true;
+    // distinct docids (the file is sorted): the hash lookup equals binarySearch
+    bool distinct = true;
+    for (size_t i = 1; i + 1 < off.size() && distinct; i++)
+      distinct = !(off[i + 1] - off[i] == off[i] - off[i - 1] &&
+                   std::equal(chars.begin() + off[i - 1], chars.begin() + off[i], chars.begin() + off[i]));
+    sme::build_docid_hash(cx, distinct, st);
   });
 }
 

@@ -380,9 +380,34 @@ __device__ int cmp_u16_utf8(const uint16_t *m, int64_t mn, const uint8_t *b, int
   return k < mn ? 1 : 0;
 }
 
+// Docid hash table over the mapping (built once when the mapping is loaded, as
+// MyMapper.configure loads it once per task): slots hold entry index + 1; a record
+// whose docid hashes to an equal entry takes that index, and only a miss (docid not
+// in the mapping: the negative insertion point of Arrays.binarySearch) or a mapping
+// with duplicate docids falls back to the binary search.
+__device__ __forceinline__ uint64_t docid_hash_step(uint64_t h, uint16_t u) { return (h ^ u) * 0x100000001B3ull; }
+__device__ __forceinline__ uint64_t docid_hash_fin(uint64_t h) { return fmix64(h) | 1ull; }
+
+__global__ void k_map_hash(const uint16_t *mchars, const int64_t *moff, int64_t mn, uint32_t *slots, uint64_t mask,
+                           unsigned int *ovf) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < mn; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (int64_t x = moff[i]; x < moff[i + 1]; x++) h = docid_hash_step(h, mchars[x]);
+    uint64_t sl = docid_hash_fin(h) & mask;
+    for (uint64_t probe = 0;; probe++) {
+      if (probe > mask) {
+        atomicOr(ovf, 1u);
+        break;
+      }
+      if (atomicCAS(&slots[sl], 0u, (uint32_t)(i + 1)) == 0u) break;
+      sl = (sl + 1) & mask;
+    }
+  }
+}
+
 __global__ void k_docno(const uint8_t *t, const uint64_t *rs, const uint64_t *re, int64_t nR,
-                        const uint16_t *mchars, const int64_t *moff, int64_t mn, int32_t *docno,
-                        unsigned long long *err) {
+                        const uint16_t *mchars, const int64_t *moff, int64_t mn, const uint32_t *mslots,
+                        uint64_t mmask, int32_t *docno, unsigned long long *err) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nR; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = (int64_t)rs[r], e = (int64_t)re[r];
     int64_t ib, ie;
@@ -390,6 +415,28 @@ __global__ void k_docno(const uint8_t *t, const uint64_t *rs, const uint64_t *re
       atomicAdd(err, 1ull);
       docno[r] = 0;
       continue;
+    }
+    if (mslots) {
+      uint64_t h = 0xCBF29CE484222325ull;
+      for (int64_t p = ib; p < ie;) {
+        uint16_t u[2];
+        int nu;
+        p += utf8_step(t, p, ie, u, &nu);
+        for (int x = 0; x < nu; x++) h = docid_hash_step(h, u[x]);
+      }
+      uint64_t sl = docid_hash_fin(h) & mmask;
+      int64_t found = -1;
+      for (uint32_t v; (v = mslots[sl]) != 0u; sl = (sl + 1) & mmask) {
+        const int64_t m = (int64_t)v - 1;
+        if (cmp_u16_utf8(mchars + moff[m], moff[m + 1] - moff[m], t + ib, ie - ib) == 0) {
+          found = m;
+          break;
+        }
+      }
+      if (found >= 0) {
+        docno[r] = (int32_t)found;
+        continue;
+      }
     }
     // Arrays.binarySearch over {"", docids...}
     int64_t lo = 0, hi = mn - 1;
@@ -2172,6 +2219,21 @@ __global__ void k_iota_docno(int32_t *d, int64_t n) {
     d[i] = (int32_t)(i + 1);
 }
 
+void build_docid_hash(sme_ctx *cx, bool distinct, hipStream_t st) {
+  cx->map_hash_ok = false;
+  if (!distinct || cx->map_n < 2) return;
+  const uint64_t cap = next_pow2(std::max<uint64_t>(1024, 2 * (uint64_t)cx->map_n));
+  uint32_t *slots = cx->map_slots.as<uint32_t>(cap);
+  unsigned int *ovf = cx->ws[63].as<unsigned int>(4);
+  SME_HIP(hipMemsetAsync(slots, 0, cap * sizeof(uint32_t), st));
+  SME_HIP(hipMemsetAsync(ovf, 0, sizeof(unsigned int), st));
+  hipLaunchKernelGGL(k_map_hash, dim3(grid_for(cx->map_n)), dim3(256), 0, st, (const uint16_t *)cx->map_chars.p,
+                     (const int64_t *)cx->map_off.p, cx->map_n, slots, cap - 1, ovf);
+  SME_CHECK_LAUNCH();
+  cx->map_mask = cap - 1;
+  cx->map_hash_ok = d2h(ovf, st) == 0;
+}
+
 sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st, int job) {
   // job 0: TermKGramDocIndexer; job 1: CharKGramTermIndexer (no docnos: its mapper
   // never calls getDocid, and records stay in file order = the map task's order)
@@ -2190,7 +2252,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
   if (nR > 0 && job == 0) {
     hipLaunchKernelGGL(k_docno, dim3(grid_for(nR)), dim3(256), 0, st, t, rs, re, nR,
-                       (const uint16_t *)cx->map_chars.p, (const int64_t *)cx->map_off.p, cx->map_n, docno, cnt);
+                       (const uint16_t *)cx->map_chars.p, (const int64_t *)cx->map_off.p, cx->map_n,
+                       cx->map_hash_ok ? (const uint32_t *)cx->map_slots.p : nullptr, cx->map_mask, docno, cnt);
     SME_CHECK_LAUNCH();
   } else if (nR > 0) {
     hipLaunchKernelGGL(k_iota_docno, dim3(grid_for(nR)), dim3(256), 0, st, docno, nR);

@@ -17,6 +17,9 @@ struct sme_ctx {
   sme::DevBuf map_chars, map_off;
   int64_t map_n = 0;  // entries including the "" sentinel
   bool has_map = false;
+  sme::DevBuf map_slots;  // docid hash table (entry index + 1), see k_docno
+  uint64_t map_mask = 0;
+  bool map_hash_ok = false;  // built, and the mapping's docids are distinct
   // build workspace, reused across builds (see DevBuf)
   sme::DevBuf ws[128];  // 48..63 query / serializer / tokenizer / reweight, 64..127 build
   sme::DevBuf cub_tmp;
@@ -119,6 +122,7 @@ struct RecordSpans {
   uint64_t *C;        // sorted positions of '<' whose markup is not "simple"
   int64_t nC;
 };
+void build_docid_hash(sme_ctx *cx, bool distinct, hipStream_t st);
 RecordSpans find_records(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, Prof *prof);
 void number_documents(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, std::vector<uint8_t> &out);
 sme_index *build_index(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, int job = 0);
