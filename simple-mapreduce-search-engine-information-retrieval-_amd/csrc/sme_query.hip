@@ -257,7 +257,7 @@ constexpr int kTMaxTerms = 16;  // queries with more terms go through k_query
 constexpr int kWBits = 10;      // tile = 1024 documents: 8 KiB of fp64 accumulators per wave
 constexpr int kWTile = 1 << kWBits;
 constexpr int kWLut = 128;      // 1 + ln(tf) for tf < 128 from LDS
-constexpr int kWBatchDefault = 8;  // 64-posting chunks in flight per wave
+constexpr int kWBatchDefault = 4;  // 64-posting chunks in flight per wave (8 spills at 128 VGPRs)
 
 __global__ void k_mark_terms(const int32_t *terms, int64_t n, int64_t V, int32_t *mark) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -343,6 +343,52 @@ __global__ void k_skip_zero_rows(const int64_t *rdf, int64_t nrows, int64_t T, i
       for (int64_t j = threadIdx.x; j <= T; j += blockDim.x) sk[r * (T + 1) + j] = 0;
 }
 
+// Dense tf rows for the batch's hot terms.  A term whose postings cover at
+// least 1/div of the docno span costs >= 8 B x span / div as (docno, tf)
+// postings but span bytes as a u8 tf-per-document row, so for div = 8 the row
+// is never more traffic -- and for the Zipf head (df ~ N) it is 8x less, one
+// coalesced 16-byte load per lane per tile instead of 32 scattered 4-byte loads.
+// Default div = 4 (measured on c3: 1/4 beats 1/2, 1/8 and 1/32: below ~N/4 a
+// tile's few postings are cheaper to apply than 1024 tf bytes).
+// drow[row] = dense row of skip row `row` or -1.  A term with any tf > 255 has
+// its dense row withdrawn (k_dense_drop) and stays on the posting path.
+constexpr int kDMax = 4;  // dense terms per query (query positions 0..3)
+__global__ void k_dense_mark(const int64_t *rdf, int64_t nrows, int64_t span, int64_t div, int32_t *flag) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
+    flag[r] = (div > 0 && rdf[r] > 0 && rdf[r] * div >= span) ? 1 : 0;
+}
+__global__ void k_dense_rows(const int32_t *flag, const int32_t *scan, int64_t nrows, int64_t cap, int32_t *drow) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
+    drow[r] = (flag[r] && scan[r] < cap) ? scan[r] : -1;
+}
+// one block per dense row (grid-stride): tf bytes at docno - dmin
+__global__ __launch_bounds__(256) void k_dense_fill(const int32_t *drow, int64_t nrows, const int32_t *term_of_row,
+                                                    const int64_t *off, const int32_t *docno, const int32_t *tf,
+                                                    int64_t dmin, int64_t stride, uint8_t *dense, int32_t *bad) {
+  for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const int32_t d = drow[r];
+    if (d < 0) continue;
+    const int64_t b = off[term_of_row[r]], e = off[term_of_row[r] + 1];
+    uint8_t *row = dense + (int64_t)d * stride;
+    for (int64_t p = b + threadIdx.x; p < e; p += blockDim.x) {
+      const int32_t f = tf[p];
+      const int64_t x = (int64_t)docno[p] - dmin, r = x & (kWTile - 1);
+      row[(x - r) + 16 * (r & 63) + (r >> 6)] = (uint8_t)(f > 255 ? 0 : f);
+      if (f > 255) bad[d] = 1;
+    }
+  }
+}
+__global__ void k_dense_drop(int32_t *drow, int64_t nrows, const int32_t *bad) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
+    if (drow[r] >= 0 && bad[drow[r]]) drow[r] = -1;
+}
+
+// Within a tile a dense row is stored lane-major: byte 16 l + b holds document
+// 64 b + l, so lane l's 16-byte load carries documents l, l + 64, ..., and the
+// apply of byte b touches 64 consecutive accumulators (no LDS bank conflicts,
+// while the posting path keeps the natural acc[d] layout that consecutive
+// docnos hit conflict-free).
+
 // One WAVE per query (no block barriers at all): the wave's fp64 accumulators
 // for a tile of kWTile documents live in its own LDS slice, and a wave's LDS
 // operations execute in program order, so applying term i's postings before
@@ -353,13 +399,14 @@ __global__ void k_skip_zero_rows(const int64_t *rdf, int64_t nrows, int64_t T, i
 // them in query-token order, and folds the tile into per-lane register top-k
 // lists; the next tile is the smallest tile holding a remaining posting.
 template <int KMAX, int kWBatch>
-__global__ __launch_bounds__(64) void k_query_wave(const int64_t *__restrict__ off, const int32_t *__restrict__ docno,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ? 4 : 1))) void k_query_wave(const int64_t *__restrict__ off, const int32_t *__restrict__ docno,
                                                    const int32_t *__restrict__ tf, const double *__restrict__ lut,
                                                    int max_tf, const double *__restrict__ idf,
                                                    const int32_t *__restrict__ row_of, const int32_t *__restrict__ sk,
                                                    int64_t dmin, int64_t T, const int32_t *__restrict__ terms,
                                                    const int64_t *__restrict__ qoff, int nq, int k, int32_t *out_d,
-                                                   double *out_s) {
+                                                   double *out_s, const uint8_t *__restrict__ dense,
+                                                   const int32_t *__restrict__ drow, int64_t dstride) {
   __shared__ double acc[kWTile];
   __shared__ double s_lut[kWLut];
   const int lane = threadIdx.x;
@@ -368,12 +415,13 @@ __global__ __launch_bounds__(64) void k_query_wave(const int64_t *__restrict__ o
   for (int q = blockIdx.x; q < nq; q += gridDim.x) {
     const int64_t q0 = qoff[q];
     const int nt = (int)(qoff[q + 1] - q0);  // <= kTMaxTerms (host checked)
-    // lane i < nt holds term i: postings base, df, idf, skip row
+    // lane i < nt holds term i: postings base, df, idf, skip row, dense row
     int64_t mb = 0;
     int32_t mdf = 0;
     double midf = 0.0;
     const int32_t *mrow = sk;
     int32_t nx = 0x7FFFFFFF;
+    int64_t mdr = -1;
     if (lane < nt) {
       const int32_t t = terms[q0 + lane];
       if (t >= 0) {
@@ -382,8 +430,12 @@ __global__ __launch_bounds__(64) void k_query_wave(const int64_t *__restrict__ o
         midf = idf[t];
         mrow = sk + (int64_t)row_of[t] * (T + 1);
         if (mdf > 0) nx = (int32_t)(((int64_t)docno[mb] - dmin) >> kWBits);
+        if (drow != nullptr && lane < kDMax && mdf > 0) mdr = drow[row_of[t]];
       }
     }
+    const bool isd = mdr >= 0;
+    const uint64_t dmask = (uint64_t)__ballot(isd);  // wave-uniform: query positions read from dense rows
+    const uint8_t *mdp = dense + (isd ? mdr * dstride : 0);  // row base (read lane-uniformly per term)
     double ts[KMAX];
     int32_t td[KMAX];
 #pragma unroll
@@ -411,45 +463,99 @@ __global__ __launch_bounds__(64) void k_query_wave(const int64_t *__restrict__ o
         me1 = mdf;
       }
       const int64_t dbase = dmin + ((int64_t)tile << kWBits);
-      // walk (term i, position s) over all chunks of the tile, kWBatch at a time
+      // dense terms with postings in this tile: their 16 tf bytes per lane, all
+      // loads issued before the posting batches
+      const uint64_t tmask = dmask & (uint64_t)__ballot(isd && me > mc);
+      uint4 dz[kDMax];
+#pragma unroll
+      for (int j = 0; j < kDMax; j++) {
+        if ((tmask >> j) & 1) {
+          const uint8_t *pj = reinterpret_cast<const uint8_t *>(rl64((int64_t)mdp, j));
+          dz[j] = *reinterpret_cast<const uint4 *>(pj + ((int64_t)tile << kWBits) + 16 * lane);
+        } else {
+          dz[j] = make_uint4(0, 0, 0, 0);
+        }
+      }
+      int da = 0;  // dense terms at positions < da are applied (wave-uniform)
+      // apply dense terms at positions [da, lim) in query order
+      auto dense_upto = [&](int lim) {
+#pragma unroll
+        for (int j = 0; j < kDMax; j++) {
+          if (j >= da && j < lim && ((tmask >> j) & 1)) {
+            const double widf = __shfl(midf, j, 64);
+#pragma unroll 1
+            for (int u = 0; u < 4; u++) {
+              const uint32_t wd = u == 0 ? dz[j].x : u == 1 ? dz[j].y : u == 2 ? dz[j].z : dz[j].w;
+#pragma unroll
+              for (int b = 0; b < 4; b++) {
+                const int f = (int)((wd >> (8 * b)) & 0xFF);
+                if (f == 0) continue;
+                const double l = f < kWLut ? s_lut[f] : lut[f];
+                const double w = __dmul_rn(l, widf);
+                const int x = (((u << 2) | b) << 6) | lane;
+                const double a = acc[x];
+                acc[x] = a < 0.0 ? w : __dadd_rn(a, w);
+              }
+            }
+          }
+        }
+        da = lim > da ? lim : da;
+      };
+      // walk (term i, position s) over all chunks of the tile, kWBatch at a time;
+      // dense terms have empty posting ranges here
+      // bar = query position of the next dense term still to apply (nt if none):
+      // a batch never holds postings of a term at or past it, so every
+      // document's adds stay in query-token order
+      auto next_bar = [&]() {
+        const uint64_t r = tmask >> da;
+        const int b = r ? da + (int)__builtin_ctzll(r) : nt;
+        return b < nt ? b : nt;
+      };
+      int bar = next_bar();
       int i = 0;
-      int64_t s = __shfl(mb + mc, 0, 64), e = __shfl(mb + me, 0, 64);
-      while (i < nt) {
+      int64_t s = __shfl(mb + (isd ? me : mc), 0, 64), e = __shfl(mb + me, 0, 64);
+      for (;;) {
+        while (i < bar && s >= e) {  // advance to the next term with postings left in this tile
+          i++;
+          if (i < nt) {
+            s = __shfl(mb + (isd ? me : mc), i, 64);
+            e = __shfl(mb + me, i, 64);
+          }
+        }
+        if (i >= bar) {
+          if (bar >= nt) break;
+          dense_upto(bar + 1);  // the dense term at position bar
+          bar = next_bar();
+          continue;  // its posting range is empty: the advance moves past it
+        }
         int32_t dv[kWBatch], fv[kWBatch];
         int ti[kWBatch];
 #pragma unroll
         for (int m = 0; m < kWBatch; m++) {
-          while (i < nt && s >= e) {  // advance to the next term with postings left in this tile
+          while (i < bar && s >= e) {
             i++;
             if (i < nt) {
-              s = __shfl(mb + mc, i, 64);
+              s = __shfl(mb + (isd ? me : mc), i, 64);
               e = __shfl(mb + me, i, 64);
             }
           }
           ti[m] = i;
           const int64_t p = s + lane;
-          const bool v = i < nt && p < e;
+          const bool v = i < bar && p < e;
           dv[m] = v ? docno[p] : -1;
           fv[m] = v ? tf[p] : 0;
           s += 64;
         }
 #pragma unroll
         for (int m = 0; m < kWBatch; m++) {
-          const double widf = __shfl(midf, ti[m], 64);  // all lanes: ti[m] is wave-uniform
-          if (fv[m] == 0) continue;                       // tf >= 1 on every posting
+          const double widf = __shfl(midf, ti[m] < nt ? ti[m] : 0, 64);  // ti[m] is wave-uniform
+          if (fv[m] == 0) continue;                                        // tf >= 1 on every posting
           const int d = (int)((int64_t)dv[m] - dbase);
           const int f = fv[m];
           const double l = f < kWLut ? s_lut[f] : lut[f];
           const double w = __dmul_rn(l, widf);
           const double a = acc[d];
           acc[d] = a < 0.0 ? w : __dadd_rn(a, w);
-        }
-        while (i < nt && s >= e) {
-          i++;
-          if (i < nt) {
-            s = __shfl(mb + mc, i, 64);
-            e = __shfl(mb + me, i, 64);
-          }
         }
       }
       for (int j = lane; j < kWTile; j += 64) {
@@ -528,7 +634,9 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   bool tiled = V > 0 && ix->P > 0 && ix->dmax >= ix->dmin &&
                !(force && strcmp(force, "stream") == 0);
   const int64_t T = tiled ? ((ix->dmax - ix->dmin) >> kWBits) + 1 : 0;
-  const int32_t *row_of = nullptr, *sk = nullptr;
+  const int32_t *row_of = nullptr, *sk = nullptr, *drow = nullptr;
+  const uint8_t *dense = nullptr;
+  int64_t dstride = 0;
   if (tiled) {
     hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
     int h_mx = 0;
@@ -571,6 +679,38 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
         SME_CHECK_LAUNCH();
         row_of = rowo;
         sk = skw;
+        // dense tf rows for terms covering >= 1/div of the docno span
+        // (SME_QDENSE=div, 0 = posting path only; tests run several)
+        const char *ed = getenv("SME_QDENSE");
+        const int64_t ddiv = ed ? atoll(ed) : 4;
+        const int64_t span = ix->dmax - ix->dmin + 1, stride = T << kWBits;
+        if (ddiv > 0) {
+          const int64_t cap = std::max<int64_t>(1, (int64_t)4e9 / stride);
+          int32_t *flag = W[53].as<int32_t>(nrows + 1), *dscan = W[54].as<int32_t>(nrows + 1);
+          const unsigned gR = (unsigned)std::min<int64_t>((nrows + 256) / 256, 8192);
+          hipLaunchKernelGGL(k_dense_mark, dim3(gR), dim3(256), 0, st, rdf, nrows + 1, span, ddiv, flag);
+          SME_HIP(hipMemsetAsync(flag + nrows, 0, sizeof(int32_t), st));
+          SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, flag, dscan, (int)nrows + 1, st));
+          SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, flag, dscan, (int)nrows + 1, st));
+          int32_t ndense = 0;
+          SME_HIP(hipMemcpyAsync(&ndense, dscan + nrows, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+          SME_HIP(hipStreamSynchronize(st));
+          const int64_t nd = std::min<int64_t>(ndense, cap);
+          if (nd > 0) {
+            int32_t *drw = W[62].as<int32_t>(nrows), *bad = W[52].as<int32_t>(nd);
+            uint8_t *dns = W[61].as<uint8_t>(nd * stride);
+            SME_HIP(hipMemsetAsync(dns, 0, (size_t)(nd * stride), st));
+            SME_HIP(hipMemsetAsync(bad, 0, (size_t)nd * sizeof(int32_t), st));
+            hipLaunchKernelGGL(k_dense_rows, dim3(gR), dim3(256), 0, st, flag, dscan, nrows, cap, drw);
+            hipLaunchKernelGGL(k_dense_fill, dim3((unsigned)std::min<int64_t>(nrows, 8192)), dim3(256), 0, st, drw,
+                               nrows, tor, off, dn, tf, ix->dmin, stride, dns, bad);
+            hipLaunchKernelGGL(k_dense_drop, dim3(gR), dim3(256), 0, st, drw, nrows, bad);
+            SME_CHECK_LAUNCH();
+            dense = dns;
+            drow = drw;
+            dstride = stride;
+          }
+        }
       } else {
         row_of = rowo;
         sk = W[60].as<int32_t>(T + 1);
@@ -588,11 +728,13 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     const int bsel = eb ? atoi(eb) : kWBatchDefault;
 #define SME_QW(KM, BT)                                                                                                \
   hipLaunchKernelGGL((k_query_wave<KM, BT>), dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf, row_of, sk, \
-                     ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score)
-    if (k <= 16) {
-      if (bsel == 16) SME_QW(16, 16);
-      else if (bsel == 4) SME_QW(16, 4);
-      else SME_QW(16, 8);
+                     ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score, dense, drow, dstride)
+    if (k <= 10) {
+      if (bsel == 16) SME_QW(10, 16);
+      else if (bsel == 4) SME_QW(10, 4);
+      else SME_QW(10, 8);
+    } else if (k <= 16) {
+      SME_QW(16, 8);
     } else {
       SME_QW(32, 8);
     }

@@ -144,15 +144,28 @@ def test_queries_vs_oracle(sme, synth, idf_mode):
         assert (dn[q, k:] == -1).all()
 
 
-def _query_both_kernels(ix, terms, qoff, k):
-    """Default (tiled) scoring and the streaming kernel: identical bits."""
-    dn, sc = ix.query_topk(terms, qoff, k)
-    os.environ["SME_QUERY_KERNEL"] = "stream"
+def _query_env(ix, terms, qoff, k, **env):
+    old = {n: os.environ.get(n) for n in env}
+    os.environ.update({n: str(v) for n, v in env.items()})
     try:
-        dn2, sc2 = ix.query_topk(terms, qoff, k)
+        return ix.query_topk(terms, qoff, k)
     finally:
-        del os.environ["SME_QUERY_KERNEL"]
-    assert np.array_equal(dn, dn2) and np.array_equal(sc, sc2)
+        for n, v in old.items():
+            if v is None:
+                del os.environ[n]
+            else:
+                os.environ[n] = v
+
+
+def _query_both_kernels(ix, terms, qoff, k):
+    """Default (tiled, dense rows for hot terms) scoring, the tiled kernel on
+    postings only, every term on dense rows, and the streaming kernel: all
+    identical bits."""
+    dn, sc = ix.query_topk(terms, qoff, k)
+    for env in ({"SME_QUERY_KERNEL": "stream"}, {"SME_QDENSE": 0}, {"SME_QDENSE": 1 << 30},
+                {"SME_QDENSE": 1 << 30, "SME_QBATCH": 4}):
+        dn2, sc2 = _query_env(ix, terms, qoff, k, **env)
+        assert np.array_equal(dn, dn2) and np.array_equal(sc, sc2), env
     return dn, sc
 
 
@@ -184,6 +197,32 @@ def test_queries_multi_tile(sme, synth):
     tl = [names[t] for t in range(20)]
     rd, rs = ref.query(tl, 10, 0, 0)
     assert dn[3, :len(rd)].tolist() == rd and np.array_equal(sc[3, :len(rd)], np.array(rs))
+
+
+def test_queries_dense_rows(sme, synth):
+    """Hot terms read from per-batch dense tf rows: a small vocabulary makes most
+    terms dense, a few documents push one hot term's tf past 255 (its row is
+    withdrawn, posting path), queries repeat terms and hold more dense terms
+    than the kernel's dense slots; k = 10 and k = 16 instantiations."""
+    n = 5000
+    c = synth.gen_corpus(n, V=60, seed=21, len_lo=10, len_hi=50)
+    blob, offs = synth.make_vocab(60, 21)
+    hot = blob[offs[0]:offs[1]].decode()
+    extra = b"".join(b"<DOC>\n<DOCNO>Z%04d</DOCNO>\n<TEXT>\n" % i + (hot + " ").encode() * (250 + 7 * i) +
+                     b"\n</TEXT>\n</DOC>\n" for i in range(4))
+    ix, ref = _check_build(sme, c + extra, synth.docids(n) + ["Z%04d" % i for i in range(4)], R=1)
+    assert int(ix.csr()[2].max()) > 255
+    _, _, _, df = ix.csr()
+    names = [ix.term(i) for i in range(ix.V)]
+    terms, qoff = synth.queries_by_df(df, 40, seed=3, qlen_lo=1, qlen_hi=12)
+    terms[5] = terms[4]  # a repeated term
+    for k in (10, 16):
+        dn, sc = _query_both_kernels(ix, terms, qoff, k)
+        for q in range(len(qoff) - 1):
+            tl = [names[t] for t in terms[qoff[q]:qoff[q + 1]] if t >= 0]
+            rd, rs = ref.query(tl, k, 0, 0)
+            assert dn[q, :len(rd)].tolist() == rd, (k, q)
+            assert np.array_equal(sc[q, :len(rd)], np.array(rs)), (k, q)
 
 
 def test_single_term_queries_match_reference_sort(sme, synth):
