@@ -246,7 +246,7 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     return {"metric": "top-10 queries/sec", "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
             "terms_per_query": "U{2..8} drawn by df (seed 7)", "ms_per_batch": round(dt * 1e3, 3),
             "prep_ms": qp_ms,
-            "prep_what": "per-batch skip table (distinct batch terms x 1024-doc tiles), inside ms_per_batch",
+            "prep_what": "per-batch skip table (distinct batch terms x 1024-doc tiles) + dense u8 tf rows of terms with df >= span/4, inside ms_per_batch",
             "roofline": {"bound": "hbm", "kernel": kname, "kernel_ms": qk_ms,
                          "achieved": round(alg / t_k / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(alg / t_k / 1e9 / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname, a),

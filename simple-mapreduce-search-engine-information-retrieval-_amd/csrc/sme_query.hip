@@ -256,7 +256,7 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
 constexpr int kTMaxTerms = 16;  // queries with more terms go through k_query
 constexpr int kWBits = 10;      // tile = 1024 documents: 8 KiB of fp64 accumulators per wave
 constexpr int kWTile = 1 << kWBits;
-constexpr int kWLut = 128;      // 1 + ln(tf) for tf < 128 from LDS
+constexpr int kWLut = 256;      // 1 + ln(tf) for tf < 256 from LDS (entry 0 = 0: the register path's absent term)
 constexpr int kWBatchDefault = 4;  // 64-posting chunks in flight per wave (8 spills at 128 VGPRs)
 
 __global__ void k_mark_terms(const int32_t *terms, int64_t n, int64_t V, int32_t *mark) {
@@ -353,6 +353,7 @@ __global__ void k_skip_zero_rows(const int64_t *rdf, int64_t nrows, int64_t T, i
 // drow[row] = dense row of skip row `row` or -1.  A term with any tf > 255 has
 // its dense row withdrawn (k_dense_drop) and stays on the posting path.
 constexpr int kDMax = 4;  // dense terms per query (query positions 0..3)
+constexpr int kRMax = 8;  // register path: terms per query (8 tf-byte rows in the 8 KiB of acc)
 __global__ void k_dense_mark(const int64_t *rdf, int64_t nrows, int64_t span, int64_t div, int32_t *flag) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
     flag[r] = (div > 0 && rdf[r] > 0 && rdf[r] * div >= span) ? 1 : 0;
@@ -398,7 +399,10 @@ __global__ void k_dense_drop(int32_t *drow, int64_t nrows, const int32_t *bad) {
 // kWBatch 64-posting chunks (all loads of a batch in flight together), applies
 // them in query-token order, and folds the tile into per-lane register top-k
 // lists; the next tile is the smallest tile holding a remaining posting.
-template <int KMAX, int kWBatch>
+// kPath 1 = register path (queries that qualify, others skipped), 2 = LDS-
+// accumulator path (the rest): two launches, each kernel carrying only its own
+// registers.
+template <int KMAX, int kWBatch, int kPath>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ? 4 : 1))) void k_query_wave(const int64_t *__restrict__ off, const int32_t *__restrict__ docno,
                                                    const int32_t *__restrict__ tf, const double *__restrict__ lut,
                                                    int max_tf, const double *__restrict__ idf,
@@ -406,12 +410,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
                                                    int64_t dmin, int64_t T, const int32_t *__restrict__ terms,
                                                    const int64_t *__restrict__ qoff, int nq, int k, int32_t *out_d,
                                                    double *out_s, const uint8_t *__restrict__ dense,
-                                                   const int32_t *__restrict__ drow, int64_t dstride) {
-  __shared__ double acc[kWTile];
+                                                   const int32_t *__restrict__ drow, int64_t dstride, int fast) {
+  __shared__ double acc[kWTile];  // LDS-accumulator path; the register path reuses it as 8 tf-byte rows
   __shared__ double s_lut[kWLut];
   const int lane = threadIdx.x;
   for (int j = lane; j < kWTile; j += 64) acc[j] = -1.0;  // untouched (weights are >= 0)
-  for (int j = lane; j < kWLut; j += 64) s_lut[j] = j <= max_tf ? lut[j] : 0.0;
+  for (int j = lane; j < kWLut; j += 64) s_lut[j] = (j >= 1 && j <= max_tf) ? lut[j] : 0.0;
   for (int q = blockIdx.x; q < nq; q += gridDim.x) {
     const int64_t q0 = qoff[q];
     const int nt = (int)(qoff[q + 1] - q0);  // <= kTMaxTerms (host checked)
@@ -435,6 +439,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
     }
     const bool isd = mdr >= 0;
     const uint64_t dmask = (uint64_t)__ballot(isd);  // wave-uniform: query positions read from dense rows
+    // register path: <= kRMax terms, every known term's idf > 0 (a touched
+    // document then has a positive score, so "untouched" = 0), all tf <= 255
+    const bool fastq = fast && nt <= kRMax && __ballot(lane < nt && mdf > 0 && !(midf > 0.0)) == 0;
+    if (fastq != (kPath == 1)) continue;  // wave-uniform: the other launch takes it
     const uint8_t *mdp = dense + (isd ? mdr * dstride : 0);  // row base (read lane-uniformly per term)
     double ts[KMAX];
     int32_t td[KMAX];
@@ -463,6 +471,100 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
         me1 = mdf;
       }
       const int64_t dbase = dmin + ((int64_t)tile << kWBits);
+      if constexpr (kPath == 1) {
+        // Register path.  Every term with postings in the tile gets a row of
+        // 1024 tf bytes in LDS (lane-major: byte 16 l + b = document 64 b + l):
+        // dense terms copy their HBM row, posting terms are zeroed and their
+        // tf bytes scattered (one byte per (term, document): order-free).  Then
+        // lane l accumulates documents l + 64 b in 16 fp64 registers, term by
+        // term in query order: r = r + lut[tf] * idf with lut[0] = 0 adds an
+        // exact 0 for absent terms, so r is the reference's left-to-right sum.
+        uint8_t *rows = reinterpret_cast<uint8_t *>(acc);
+        const uint64_t amask = (uint64_t)__ballot(lane < nt && me > mc);
+        const uint64_t dm = dmask & amask, sm = amask & ~dmask;
+#pragma unroll
+        for (int j = 0; j < kDMax; j++) {
+          if ((dm >> j) & 1) {
+            const uint8_t *pj = reinterpret_cast<const uint8_t *>(rl64((int64_t)mdp, j));
+            *reinterpret_cast<uint4 *>(rows + (j << kWBits) + 16 * lane) =
+                *reinterpret_cast<const uint4 *>(pj + ((int64_t)tile << kWBits) + 16 * lane);
+          }
+        }
+        for (uint64_t m = sm; m; m &= m - 1)
+          *reinterpret_cast<uint4 *>(rows + ((int)__builtin_ctzll(m) << kWBits) + 16 * lane) = make_uint4(0, 0, 0, 0);
+        int i = 0;
+        int64_t s = __shfl(mb + (isd ? me : mc), 0, 64), e = __shfl(mb + me, 0, 64);
+        for (;;) {
+          while (i < nt && s >= e) {
+            i++;
+            if (i < nt) {
+              s = __shfl(mb + (isd ? me : mc), i, 64);
+              e = __shfl(mb + me, i, 64);
+            }
+          }
+          if (i >= nt) break;
+          int32_t dv[kWBatch], fv[kWBatch];
+          int ti[kWBatch];
+#pragma unroll
+          for (int m = 0; m < kWBatch; m++) {
+            while (i < nt && s >= e) {
+              i++;
+              if (i < nt) {
+                s = __shfl(mb + (isd ? me : mc), i, 64);
+                e = __shfl(mb + me, i, 64);
+              }
+            }
+            ti[m] = i;
+            const int64_t p = s + lane;
+            const bool v = i < nt && p < e;
+            dv[m] = v ? docno[p] : 0;
+            fv[m] = v ? tf[p] : 0;
+            s += 64;
+          }
+#pragma unroll
+          for (int m = 0; m < kWBatch; m++) {
+            if (fv[m] == 0) continue;
+            const int d = (int)((int64_t)dv[m] - dbase);
+            rows[(ti[m] << kWBits) + 16 * (d & 63) + (d >> 6)] = (uint8_t)fv[m];
+          }
+        }
+        // two halves of 8 documents per lane keep the live registers low
+        double r0[8];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          double r[8];
+#pragma unroll
+          for (int b = 0; b < 8; b++) r[b] = 0.0;
+          for (uint64_t m = amask; m; m &= m - 1) {
+            const int j = (int)__builtin_ctzll(m);  // ascending position = query-token order
+            const double widf = __shfl(midf, j, 64);
+            const uint2 v = *reinterpret_cast<const uint2 *>(rows + (j << kWBits) + 16 * lane + 8 * h);
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+              const int f = (int)(((b < 4 ? v.x : v.y) >> (8 * (b & 3))) & 0xFF);
+              r[b] = __dadd_rn(r[b], __dmul_rn(s_lut[f], widf));
+            }
+          }
+          // the rows live in acc: the first half's sums wait in registers
+          // until the second half has read its bytes
+          if (h == 0) {
+#pragma unroll
+            for (int b = 0; b < 8; b++) r0[b] = r[b];
+          } else {
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+              acc[(b << 6) | lane] = r0[b];
+              acc[((b + 8) << 6) | lane] = r[b];
+            }
+          }
+        }
+        // fold through LDS (one topk_insert site keeps the register budget):
+        // document 64 b + lane at acc[64 b + lane]
+        for (int j = lane; j < kWTile; j += 64) {
+          const double sc = acc[j];
+          if (sc > 0.0) topk_insert<KMAX>(ts, td, sc, (int32_t)(dbase + j));
+        }
+      } else {
       // dense terms with postings in this tile: their 16 tf bytes per lane, all
       // loads issued before the posting batches
       const uint64_t tmask = dmask & (uint64_t)__ballot(isd && me > mc);
@@ -564,6 +666,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
         acc[j] = -1.0;
         topk_insert<KMAX>(ts, td, sc, (int32_t)(dbase + j));
       }
+      }  // LDS-accumulator path
       int32_t nt_ = nx;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) nt_ = min(nt_, __shfl_xor(nt_, o, 64));
@@ -725,10 +828,18 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   if (tiled) {
     const unsigned wgrid = (unsigned)std::min(nq, 1 << 22);
     const char *eb = getenv("SME_QBATCH");
+    const char *ef = getenv("SME_QREG");  // 0 = LDS-accumulator path only (tests run both)
+    const int fast = (ix->max_tf <= 255 && !(ef && atoi(ef) == 0)) ? 1 : 0;
     const int bsel = eb ? atoi(eb) : kWBatchDefault;
-#define SME_QW(KM, BT)                                                                                                \
-  hipLaunchKernelGGL((k_query_wave<KM, BT>), dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf, row_of, sk, \
-                     ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score, dense, drow, dstride)
+#define SME_QW1(KM, BT, PATH)                                                                                  \
+  hipLaunchKernelGGL((k_query_wave<KM, BT, PATH>), dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf,  \
+                     row_of, sk, ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score, dense, drow, dstride, \
+                     fast)
+#define SME_QW(KM, BT)          \
+  do {                          \
+    if (fast) SME_QW1(KM, 8, 1);  \
+    SME_QW1(KM, BT, 2);         \
+  } while (0)
     if (k <= 10) {
       if (bsel == 16) SME_QW(10, 16);
       else if (bsel == 4) SME_QW(10, 4);
@@ -739,6 +850,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       SME_QW(32, 8);
     }
 #undef SME_QW
+#undef SME_QW1
   } else if (k <= 16) {
     hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff,
                        nq, k, d_out_docno, d_out_score, err);

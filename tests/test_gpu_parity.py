@@ -158,12 +158,13 @@ def _query_env(ix, terms, qoff, k, **env):
 
 
 def _query_both_kernels(ix, terms, qoff, k):
-    """Default (tiled, dense rows for hot terms) scoring, the tiled kernel on
-    postings only, every term on dense rows, and the streaming kernel: all
-    identical bits."""
+    """Default (tiled: register path for queries of <= 8 terms with idf > 0,
+    dense rows for hot terms) scoring, the tiled kernel on postings only, every
+    term on dense rows, the LDS-accumulator path only, and the streaming kernel:
+    all identical bits."""
     dn, sc = ix.query_topk(terms, qoff, k)
     for env in ({"SME_QUERY_KERNEL": "stream"}, {"SME_QDENSE": 0}, {"SME_QDENSE": 1 << 30},
-                {"SME_QDENSE": 1 << 30, "SME_QBATCH": 4}):
+                {"SME_QDENSE": 1 << 30, "SME_QBATCH": 4}, {"SME_QREG": 0}, {"SME_QREG": 0, "SME_QDENSE": 0}):
         dn2, sc2 = _query_env(ix, terms, qoff, k, **env)
         assert np.array_equal(dn, dn2) and np.array_equal(sc, sc2), env
     return dn, sc
