@@ -637,6 +637,7 @@ constexpr int kTokBytes = 16 * kTokWords;         // 64 bytes per lane
 constexpr int kChunk = kTokNT * kTokBytes;        // 16 KiB of text per block step
 constexpr int kStageV = kTokNT * kTokWords + 64;  // staged 16-byte words: chunk + 1 KiB lookahead
 constexpr int kRecWin = 384;  // records overlapping one chunk: fast-path records are >= kMinFastRec bytes
+constexpr int kTokBuf = 1536;  // chunk tokens staged in LDS for coalesced stores (a 16 KiB chunk holds ~1950)
 
 // entity span end: '&' [a-z0-9#]* ';'  (TagTokenizer.onAmpersand 644-662); p if none
 template <typename B>
@@ -676,11 +677,12 @@ constexpr int32_t kFar = 1 << 30;
 struct TokLds {
   uint4 st4[kStageV];
   int32_t rs[kRecWin], re[kRecWin];  // chunk-relative, clamped
-  int64_t tbase[kRecWin];            // tokstream offset of the record (rs >> 1)
+  int64_t tbase0;                    // tokstream offset (rs >> 1) of window record 0 (others: from rs)
   int32_t c0[kRecWin];
   int32_t rid[kRecWin];               // record index
   uint64_t smask[kTokNT];             // split-byte mask of every lane's 64 bytes
   int32_t sc32[kTokNT / 64 + 1];
+  uint32_t tokbuf[kTokBuf];           // raw slots of chunk tokens 0 .. kTokBuf-1
 };
 
 // byte at chunk-relative position p (stage, or global beyond the lookahead)
@@ -766,7 +768,7 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
       const int64_t b = ok ? (int64_t)re_g[r] : INT64_MAX;
       L.rs[i] = ok ? (int32_t)max<int64_t>(a - c_lo, -1) : kFar;
       L.re[i] = ok ? (int32_t)min<int64_t>(b - c_lo, kFar) : kFar;
-      L.tbase[i] = ok ? (a >> 1) : 0;
+      if (i == 0) L.tbase0 = ok ? (a >> 1) : 0;
       L.rid[i] = ok ? r : -1;
       L.c0[i] = 0;
     }
@@ -899,8 +901,13 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
       const bool hit = len <= 16 && v.key == g.h && v.rep != 0 && (v.rep & 0xFFFFFFull) == (uint64_t)len &&
                        v.w0 == g.w0 && v.w1 == g.w1;
       const uint32_t slot = hit ? (uint32_t)(g.h & tb.mask) : raw_insert(tb, g, (uint64_t)(c_lo + x), (uint64_t)len, v);
-      const int32_t r0k = jt == 0 ? L.c0[0] - carry0 : L.c0[jt];
-      tokstream[L.tbase[jt] + (idx - r0k)] = slot;
+      if (idx < kTokBuf) {
+        L.tokbuf[idx] = slot;  // stored coalesced after the chunk
+      } else {
+        const int32_t r0k = jt == 0 ? L.c0[0] - carry0 : L.c0[jt];
+        const int64_t tb = jt == 0 ? L.tbase0 : ((c_lo + L.rs[jt]) >> 1);
+        tokstream[tb + (idx - r0k)] = slot;
+      }
       idx++;
     }
     // ntok of every record whose last byte is in this lane (no token starts at its '>')
@@ -925,6 +932,39 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
     if (blk_max >= 0) mask_carry = max<int64_t>(mask_carry, c_lo + blk_max);
     prev_chunk_byte = stg[kChunk - 1];
     __syncthreads();
+    // coalesced stores of the staged tokens: chunk token i belongs to the last
+    // window record whose first chunk token is <= i (records without tokens
+    // share that rank with their successor, so they are skipped)
+    {
+      const int nbuf = blk_cnt < kTokBuf ? blk_cnt : kTokBuf;
+      int nk;  // window records starting before the chunk end
+      {
+        int lo = 0, hi = kRecWin;
+        while (lo < hi) {
+          const int m = (lo + hi) >> 1;
+          if (L.rs[m] < kChunk) lo = m + 1;
+          else hi = m;
+        }
+        nk = lo;
+      }
+      auto fr = [&](int k) { return (k == 0 && L.rs[0] < 0) ? 0 : L.c0[k]; };
+      int k = 0;
+      if (tid < nbuf) {
+        int lo = 0, hi = nk;  // last k with fr(k) <= tid
+        while (hi - lo > 1) {
+          const int m = (lo + hi) >> 1;
+          if (fr(m) <= tid) lo = m;
+          else hi = m;
+        }
+        k = lo;
+      }
+      for (int i = tid; i < nbuf; i += kTokNT) {
+        while (k + 1 < nk && fr(k + 1) <= i) k++;
+        const int32_t r0k = k == 0 ? L.c0[0] - carry0 : L.c0[k];
+        const int64_t tb = k == 0 ? L.tbase0 : ((c_lo + L.rs[k]) >> 1);
+        tokstream[tb + (i - r0k)] = L.tokbuf[i];
+      }
+    }
     fcur += s_adv;
     tok_carry = L.sc32[0];
     __syncthreads();  // LDS is overwritten by the next chunk
