@@ -41,10 +41,12 @@ def main():
         wk = [v for n, v in write.items() if k in n]
         if not fk or not wk:
             continue
-        f = sum(fk[0]) / len(fk[0]) * 1024
-        w = sum(wk[0]) / len(wk[0]) * 1024
+        # template instantiations of one kernel (e.g. the query kernel's register
+        # and LDS paths) are launched together: a "launch" is the sum of their means
+        f = sum(sum(v) / len(v) for v in fk) * 1024
+        w = sum(sum(v) / len(v) for v in wk) * 1024
         res["kernels"][k] = {"fetch_bytes_raw": round(f), "write_bytes": round(w), "dispatches": len(fk[0]),
-                             "hbm_bytes_per_launch": round(2 * f + w)}
+                             "instantiations": len(fk), "hbm_bytes_per_launch": round(2 * f + w)}
     os.makedirs("profiles", exist_ok=True)
     json.dump(res, open("profiles/pmc_traffic.json", "w"), indent=1)
     print(json.dumps(res, indent=1))
