@@ -529,7 +529,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
           }
         }
         // two halves of 8 documents per lane keep the live registers low
-        double r0[8];
+        double r0[8], fth = 0.0;
+        bool fold = false;
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           double r[8];
@@ -551,18 +552,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
 #pragma unroll
             for (int b = 0; b < 8; b++) r0[b] = r[b];
           } else {
+            // th = the best KMAX-th score over the lanes' lists: that lane holds
+            // KMAX documents scoring >= th, so a document below th cannot reach
+            // the final top-k.  Most tiles then skip the fold entirely.
+            double th = ts[KMAX - 1], mx = 0.0;
 #pragma unroll
-            for (int b = 0; b < 8; b++) {
-              acc[(b << 6) | lane] = r0[b];
-              acc[((b + 8) << 6) | lane] = r[b];
+            for (int o = 32; o > 0; o >>= 1) th = fmax(th, __shfl_xor(th, o, 64));
+#pragma unroll
+            for (int b = 0; b < 8; b++) mx = fmax(mx, fmax(r0[b], r[b]));
+            fold = __ballot(mx > 0.0 && mx >= th) != 0;
+            if (fold) {
+#pragma unroll
+              for (int b = 0; b < 8; b++) {
+                acc[(b << 6) | lane] = r0[b];
+                acc[((b + 8) << 6) | lane] = r[b];
+              }
             }
+            fth = th;
           }
         }
         // fold through LDS (one topk_insert site keeps the register budget):
         // document 64 b + lane at acc[64 b + lane]
-        for (int j = lane; j < kWTile; j += 64) {
-          const double sc = acc[j];
-          if (sc > 0.0) topk_insert<KMAX>(ts, td, sc, (int32_t)(dbase + j));
+        if (fold) {
+          for (int j = lane; j < kWTile; j += 64) {
+            const double sc = acc[j];
+            if (sc > 0.0 && sc >= fth) topk_insert<KMAX>(ts, td, sc, (int32_t)(dbase + j));
+          }
         }
       } else {
       // dense terms with postings in this tile: their 16 tf bytes per lane, all
