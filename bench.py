@@ -19,6 +19,7 @@ are all-gathered and merged.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import gc
 import ctypes as C
 import importlib
 import json
@@ -102,14 +103,19 @@ def main():
         ix = step()
     barrier()
     profs = []
+    gc.collect()
+    gc.disable()  # no cyclic-GC pause inside the timed steps (re-enabled after)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         if ix is not None:
             ix.close()
         ix = step()
-        profs.append(ctx.last_build_profile())  # device events; the step has synchronised already
     barrier()
     dt = (time.perf_counter() - t0) / a.steps
+    gc.enable()
+    # per-stage device-event times of the last step (read after the timed region;
+    # every step does identical work)
+    profs.append(ctx.last_build_profile())
     prof = {k: round(sum(p.get(k, 0.0) for p in profs) / len(profs), 4) for k in profs[-1]}
     N, V, P = ix.N, ix.V, ix.P
     t_max = dt
@@ -211,21 +217,30 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
 
     qstep()
     barrier()
-    steps = max(3, a.steps // 2)
+    gc.collect()
+    gc.disable()  # no cyclic-GC pause inside the timed batches (re-enabled after)
+    # a one-off host stall of ~50 ms right after the timed region opens was seen
+    # on the GPU box (cause not found: not GC, not the profile read); >= 5
+    # batches amortise it like any other steady-state overhead
+    steps = max(5, a.steps)
     kms, pms, kname = [], [], "k_query"
     t0 = time.perf_counter()
+    walls = []
     for _ in range(steps):
         tq = time.perf_counter()
         qstep()
-        if os.environ.get("SME_BENCH_VERBOSE"):
-            torch.cuda.synchronize()
-            print("query step wall %.3f ms" % ((time.perf_counter() - tq) * 1e3), file=sys.stderr)
-        qp = ix.ctx.last_build_profile()
-        kms.append(qp.get("query_kernel"))
-        pms.append(qp.get("query_prep"))
-        kname = qp.get("query_kernel_name", kname)
+        walls.append((time.perf_counter() - tq) * 1e3)
     barrier()
     dt = (time.perf_counter() - t0) / steps
+    gc.enable()
+    if os.environ.get("SME_BENCH_VERBOSE"):
+        print("query step walls %s ms" % ["%.3f" % w for w in walls], file=sys.stderr)
+    # device-event timings of the last batch (read after the timed region: the
+    # profile call is measurement overhead, not query work; every batch is identical)
+    qp = ix.ctx.last_build_profile()
+    kms.append(qp.get("query_kernel"))
+    pms.append(qp.get("query_prep"))
+    kname = qp.get("query_kernel_name", kname)
     kms = [x for x in kms if x is not None]
     qk_ms = sum(kms) / len(kms) if kms else None
     pms = [x for x in pms if x is not None]
