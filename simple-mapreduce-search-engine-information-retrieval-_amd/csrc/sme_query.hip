@@ -348,8 +348,9 @@ __global__ void k_skip_zero_rows(const int64_t *rdf, int64_t nrows, int64_t T, i
 // postings but span bytes as a u8 tf-per-document row, so for div = 8 the row
 // is never more traffic -- and for the Zipf head (df ~ N) it is 8x less, one
 // coalesced 16-byte load per lane per tile instead of 32 scattered 4-byte loads.
-// Default div = 4 (measured on c3: 1/4 beats 1/2, 1/8 and 1/32: below ~N/4 a
-// tile's few postings are cheaper to apply than 1024 tf bytes).
+// Default div = 4 (measured on c3 with the LDS-accumulator path: 1/4 beat 1/2,
+// 1/8 and 1/32; with the register path 1/4, 1/8 and 1/16 are equal within noise
+// and 1/2 is 2.5 % slower).
 // drow[row] = dense row of skip row `row` or -1.  A term with any tf > 255 has
 // its dense row withdrawn (k_dense_drop) and stays on the posting path.
 constexpr int kDMax = 4;  // dense terms per query (query positions 0..3)
