@@ -286,6 +286,8 @@ typedef struct or_index {
   int nterms;
   uint8_t **part_bytes;
   size_t *part_len;
+  int *lk;           /* lazily built: open-addressed table of the forward-index lookup (find_term) */
+  int lk_cap;
 } or_index;
 
 static void stable_sort_postings(posting *a, posting *tmp, int n, int by_tf) {
@@ -380,6 +382,7 @@ void or_index_free(or_index *ix) {
     for (int r = 0; r < ix->R; r++) free(ix->part_bytes[r]);
   free(ix->part_bytes);
   free(ix->part_len);
+  free(ix->lk);
   free(ix);
 }
 
@@ -571,7 +574,7 @@ static int term_key_cmp(const term_rec *a, const term_rec *b) {
   return a->k - b->k;
 }
 
-static int find_term(const or_index *ix, const uint16_t *w, int n) {
+static int find_term_scan(const or_index *ix, const uint16_t *w, int n) {
   /* IntDocVectorsForwardIndex keys the forward index by k_gram[0] (T11): the
    * forward file lists every record in global TermDF order
    * (BuildIntDocVectorsForwardIndex.java:139-153) and the ctor's Hashtable.put
@@ -583,6 +586,48 @@ static int find_term(const or_index *ix, const uint16_t *w, int n) {
       if (best < 0 || term_key_cmp(&ix->terms[t], &ix->terms[best]) > 0) best = t;
   }
   return best;
+}
+
+static uint32_t js_fnv(const uint16_t *w, int n) {
+  uint32_t h = 2166136261u;
+  for (int i = 0; i < n; i++) h = (h ^ w[i]) * 16777619u;
+  return h;
+}
+
+/* The same result as find_term_scan, through a table of the best term per
+ * first element (built once per index: the scan is O(V) per query term). */
+static int find_term(const or_index *cix, const uint16_t *w, int n) {
+  or_index *ix = (or_index *)cix;
+  if (!ix->lk) {
+    int cap = 16;
+    while (cap < 2 * ix->nterms + 16) cap <<= 1;
+    ix->lk = (int *)malloc(sizeof(int) * (size_t)cap);
+    for (int i = 0; i < cap; i++) ix->lk[i] = -1;
+    ix->lk_cap = cap;
+    for (int t = 0; t < ix->nterms; t++) {
+      const jstr *g = &ix->terms[t].gram[0];
+      uint32_t s = js_fnv(g->p, g->n) & (uint32_t)(cap - 1);
+      for (;; s = (s + 1) & (uint32_t)(cap - 1)) {
+        int o = ix->lk[s];
+        if (o < 0) {
+          ix->lk[s] = t;
+          break;
+        }
+        const jstr *h = &ix->terms[o].gram[0];
+        if (h->n == g->n && (g->n == 0 || memcmp(h->p, g->p, (size_t)g->n * 2) == 0)) {
+          if (term_key_cmp(&ix->terms[t], &ix->terms[o]) > 0) ix->lk[s] = t;
+          break;
+        }
+      }
+    }
+  }
+  uint32_t s = js_fnv(w, n) & (uint32_t)(ix->lk_cap - 1);
+  for (;; s = (s + 1) & (uint32_t)(ix->lk_cap - 1)) {
+    int o = ix->lk[s];
+    if (o < 0) return -1;
+    const jstr *h = &ix->terms[o].gram[0];
+    if (h->n == n && (n == 0 || memcmp(h->p, w, (size_t)n * 2) == 0)) return o;
+  }
 }
 
 typedef struct {
@@ -655,6 +700,12 @@ int or_query(const or_index *ix, const uint16_t *const *terms, const int *lens, 
              int idf_mode, int order, int32_t *out_docno, double *out_score) {
   int cap = 1024, n = 0;
   docscore *sc = (docscore *)malloc(sizeof(docscore) * cap);
+  /* scores.indexOf(new DocScore(d)) (T6) finds the one entry with docId d, or
+   * none: a docno -> entry table gives the same index without the O(n) scan,
+   * and entries are appended in first-encounter order exactly as scores.add */
+  int hcap = 1024;
+  int *ht = (int *)malloc(sizeof(int) * hcap);
+  for (int i = 0; i < hcap; i++) ht[i] = -1;
   int N = ix->N;
   for (int qi = 0; qi < nterms; qi++) {
     int t = find_term(ix, terms[qi], lens[qi]);
@@ -664,12 +715,9 @@ int or_query(const or_index *ix, const uint16_t *const *terms, const int *lens, 
     double idf = log10((double)(N / df));
     for (int p = 0; p < tr->npost; p++) {
       int d = tr->post[p].docno;
-      int idx = -1;
-      for (int s = 0; s < n; s++) /* scores.indexOf (T6) */
-        if (sc[s].docId == d) {
-          idx = s;
-          break;
-        }
+      uint32_t h = ((uint32_t)d * 2654435761u) & (uint32_t)(hcap - 1);
+      while (ht[h] >= 0 && sc[ht[h]].docId != d) h = (h + 1) & (uint32_t)(hcap - 1);
+      int idx = ht[h];
       if (idx < 0) {
         if (n == cap) {
           cap *= 2;
@@ -679,11 +727,24 @@ int or_query(const or_index *ix, const uint16_t *const *terms, const int *lens, 
         sc[n].score = 0.0;
         sc[n].first = n;
         idx = n++;
+        ht[h] = idx;
+        if (2 * n > hcap) { /* grow and rehash */
+          free(ht);
+          hcap *= 4;
+          ht = (int *)malloc(sizeof(int) * hcap);
+          for (int i = 0; i < hcap; i++) ht[i] = -1;
+          for (int i = 0; i < n; i++) {
+            uint32_t g = ((uint32_t)sc[i].docId * 2654435761u) & (uint32_t)(hcap - 1);
+            while (ht[g] >= 0) g = (g + 1) & (uint32_t)(hcap - 1);
+            ht[g] = i;
+          }
+        }
       }
       double w = (1.0 + log((double)tr->post[p].tf)) * idf;
       sc[idx].score += w;
     }
   }
+  free(ht);
   if (order == 1) {
     docscore *aux = (docscore *)malloc(sizeof(docscore) * (n ? n : 1));
     memcpy(aux, sc, sizeof(docscore) * n);
@@ -811,4 +872,15 @@ int or_split_records(const uint8_t *b, size_t n, uint64_t *off, uint64_t *len, i
   }
   free(r);
   return nr;
+}
+
+/* self-check for tests: the table lookup and the O(V) scan agree on every
+ * index term's first element; returns the number of disagreements */
+int or_lookup_selfcheck(const or_index *ix) {
+  int bad = 0;
+  for (int t = 0; t < ix->nterms; t++) {
+    const jstr *g = &ix->terms[t].gram[0];
+    if (find_term(ix, g->p, g->n) != find_term_scan(ix, g->p, g->n)) bad++;
+  }
+  return bad;
 }

@@ -82,6 +82,10 @@ def lib():
     L.sme_build_chargram_device.argtypes = [vp, vp, sz, vp, C.POINTER(vp)]
     L.sme_chargram_partition_text.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
     L.sme_chargram_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.sme_synth_corpus.argtypes = [C.c_int, C.c_char_p, vp, C.c_int64, vp, C.c_int64, C.c_int64, C.c_uint64, C.c_int,
+                                   C.c_int, C.POINTER(vp), C.POINTER(sz)]
+    L.sme_synth_free.argtypes = [vp]
+    L.sme_synth_free.restype = None
     _lib = L
     return L
 
@@ -266,6 +270,38 @@ class Index:
     def query_topk_device(self, d_terms, d_qoff, nq, k, d_out_docno, d_out_score, stream=None):
         _check(lib().sme_query_topk_device(self._h, C.c_void_p(d_terms), C.c_void_p(d_qoff), nq, k,
                                            C.c_void_p(d_out_docno), C.c_void_p(d_out_score), C.c_void_p(stream or 0)))
+
+
+class DeviceCorpus:
+    """A synthetic Zipfian TREC corpus generated directly in HBM (sme_synth_corpus;
+    the same bytes as synth.gen_corpus): docs d0 .. d0+n_docs-1."""
+
+    def __init__(self, n_docs, V=1 << 20, seed=42, len_lo=400, len_hi=600, d0=0, device=0):
+        from . import synth
+        blob, voff = synth.make_vocab(V, seed)
+        cdf = synth.zipf_cdf(V, 1.0)
+        p, n = C.c_void_p(), C.c_size_t()
+        _check(lib().sme_synth_corpus(device, blob, voff.ctypes.data, V, cdf.ctypes.data, n_docs, d0, seed, len_lo,
+                                      len_hi, C.byref(p), C.byref(n)))
+        self.ptr, self.nbytes = p.value, n.value
+
+    def to_host(self):
+        """Copy the corpus bytes back (hipMemcpy device -> host)."""
+        hip = C.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        out = (C.c_ubyte * max(self.nbytes, 1))()
+        rc = hip.hipMemcpy(out, C.c_void_p(self.ptr), self.nbytes, 2)  # hipMemcpyDeviceToHost
+        if rc != 0:
+            raise SmeError(-2, "hipMemcpy failed: %d" % rc)
+        return bytes(out)[:self.nbytes]
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            lib().sme_synth_free(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        self.close()
 
 
 # ---------------------------------------------------------------------------

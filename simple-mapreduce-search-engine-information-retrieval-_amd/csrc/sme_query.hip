@@ -5,26 +5,22 @@
 //
 // Scoring semantics: for each query token in order (unknown ones skipped,
 // duplicates twice), for each posting of that term, score[d] += w where
-// w = (1 + ln tf) * idf was precomputed in fp64 by the build's weight pass.
-// A document's score is therefore the left-to-right fp64 sum of its weights in
-// query-token order, exactly as the JVM accumulates `score.score += ...`.
-// Output order: score desc, docno asc (north-star tie-break; equals the
-// reference's stable Collections.sort for single-term queries).
+// w = (1 + ln tf) * idf, evaluated as __dmul_rn(lut[tf], idf[term]) -- the same
+// fp64 product the build's weight pass (k_weights) stores, recomputed here
+// from 8-byte (docno, tf) postings.  A document's score is therefore the
+// left-to-right fp64 sum of its weights in query-token order, exactly as the
+// JVM accumulates `score.score += ...`.  Output order: score desc, docno asc
+// (north-star tie-break; equals the reference's stable Collections.sort for
+// single-term queries).
 //
-// Kernel shape: one 256-lane workgroup per query, sweeping the docno axis in
-// tiles of kTile documents whose fp64 accumulators live in LDS (32 KiB, so four
-// workgroups share a CU).  Postings are docno-sorted per term; for each tile the
-// workgroup streams every query term's postings that fall in it, 1024 per step
-// (4 per lane, coalesced), in query-token order -- one barrier per step, and
-// postings of one term have distinct docnos, so a document's adds happen in
-// token order and the fp64 sum is the reference's.  The weight of a posting is
-// lut[tf] * idf[term] (fp64, no contraction: bit-identical to the build's
-// TF-IDF pass), so a posting costs 8 bytes of HBM (docno, tf), not 12.  Each
-// lane keeps its best KMAX (score, docno) in registers; the lists are merged by
-// k rounds of block arg-max at the end.
+// Two kernels: k_query_imp (tiled, impact-gated; queries of <= 64 terms, any
+// k <= 448), described below, and k_query (streaming; one 256-lane workgroup
+// per query with fp64 LDS accumulators over 4096-document tiles, k <= 32),
+// which takes batches holding a longer query.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -130,7 +126,7 @@ __device__ __forceinline__ void emit_topk(double (&ts)[KMAX], int32_t (&td)[KMAX
 template <int KMAX>
 __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off, const int32_t *__restrict__ docno,
                                                 const int32_t *__restrict__ tf, const double *__restrict__ lut,
-                                                int max_tf, const double *__restrict__ idf,
+                                                int max_tf, const double *__restrict__ idf, int64_t V,
                                                 const int32_t *__restrict__ terms, const int64_t *__restrict__ qoff,
                                                 int nq, int k, int32_t *out_d, double *out_s, int *err) {
   __shared__ double acc[kTile];
@@ -154,7 +150,8 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
     if (tid == 0) s_next = 0x7FFFFFFF;
     __syncthreads();
     for (int i = tid; i < nt; i += kQNT) {
-      const int32_t t = terms[q0 + i];
+      const int32_t t0 = terms[q0 + i];
+      const int32_t t = t0 < V ? t0 : -1;  // out-of-range ids are skipped like unknown ones
       const int64_t b = t >= 0 ? off[t] : 0, e = t >= 0 ? off[t + 1] : 0;
       cur[i] = b;
       endp[i] = e;
@@ -243,21 +240,53 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
 }
 
 
+
 // ---------------------------------------------------------------------------
-// Tiled scoring (default path).  The docno axis is cut into fixed tiles of
-// kTile documents starting at the index's smallest docno.  A per-batch skip
-// table gives, for every DISTINCT term of the batch and every tile, the offset
-// of the term's first posting in that tile, so a workgroup knows every term's
-// range in a tile up front: it gathers all of them with one round of coalesced
-// loads into an LDS stage (docno-in-tile | tf << 12), then applies them term by
-// term in query-token order (one LDS barrier per term, no global latency in the
-// ordered part).  Same fp64 operation sequence as k_query: bit-identical scores.
+// Tiled, impact-gated scoring (default path).
+//
+// The docno axis is cut into tiles of kWTile documents from the index's
+// smallest docno.  Per batch: a skip table gives, for every DISTINCT batch term
+// and every tile, the term's first posting in the tile; terms covering >= 1/div
+// of the docno span (the Zipf head) also get two dense byte rows, the tf of
+// every document and its IMPACT q = floor(w * alpha) + 1 (w = lut[tf] * idf, the
+// exact fp64 weight; 0 where absent), alpha = 253.5 / (largest weight of any
+// batch term), so q <= 255 and q >= 1 exactly where the term occurs.
+//
+// One wave per query sweeps the tiles.  Per tile it sums the impacts of its
+// terms into packed u16 lanes (A(d) = sum_j q_j(d) is an integer, order-free:
+// dense terms by two byte permutes + adds per dword of four documents, posting
+// terms by LDS atomic adds).  Since q_j > w_j * alpha, A(d) > alpha * R(d) where
+// R is the real sum of d's weights, so a document whose fp64 score S(d) can
+// reach the current k-th best score th has A(d) >= gate = floor(alpha * th *
+// (1 - 2^-40)) (the factor absorbs every rounding).  Only
+// those candidates are scored exactly: S(d) = the left-to-right fp64 sum of
+// lut[tf] * idf over the query's terms in token order (tf from the dense tf row
+// or a binary search of the tile's postings), bit-identical to the reference's
+// `score += (1 + Math.log(tf)) * idf` (IntDocVectorsForwardIndex.java:197-213).
+// Candidates that beat th go to a per-wave LDS buffer of C entries; when it
+// fills, a bitonic sort (score desc, docno asc) keeps the best k and raises th.
 // ---------------------------------------------------------------------------
-constexpr int kTMaxTerms = 16;  // queries with more terms go through k_query
-constexpr int kWBits = 10;      // tile = 1024 documents: 8 KiB of fp64 accumulators per wave
+#ifndef SME_QTB
+#define SME_QTB 10
+#endif
+constexpr int kWBits = SME_QTB;     // tile = 2^kWBits documents
 constexpr int kWTile = 1 << kWBits;
-constexpr int kWLut = 256;      // 1 + ln(tf) for tf < 256 from LDS (entry 0 = 0: the register path's absent term)
-constexpr int kWBatchDefault = 4;  // 64-posting chunks in flight per wave (8 spills at 128 VGPRs)
+constexpr int kDPL = kWTile / 64;   // documents per lane in a tile (16 at 1024)
+constexpr int kIMaxTerms = 64;      // lane j holds query term j
+constexpr int kWLut = 256;          // 1 + ln(tf) for tf < 256 from LDS
+static_assert(kDPL % 16 == 0 && kDPL <= 32, "tile must be 1024 or 2048 documents");
+
+__device__ __forceinline__ uint32_t impact(double l, double widf, double alpha) {
+  return (uint32_t)floor(__dmul_rn(__dmul_rn(l, widf), alpha)) + 1u;
+}
+__device__ __forceinline__ double rld(double v, int l) { return __longlong_as_double(rl64(__double_as_longlong(v), l)); }
+__device__ __forceinline__ uint32_t pkmax_u16(uint32_t a, uint32_t b) {
+  const uint32_t lo = max(a & 0xFFFFu, b & 0xFFFFu), hi = max(a >> 16, b >> 16);
+  return lo | (hi << 16);
+}
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 __global__ void k_mark_terms(const int32_t *terms, int64_t n, int64_t V, int32_t *mark) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -343,84 +372,147 @@ __global__ void k_skip_zero_rows(const int64_t *rdf, int64_t nrows, int64_t T, i
       for (int64_t j = threadIdx.x; j <= T; j += blockDim.x) sk[r * (T + 1) + j] = 0;
 }
 
-// Dense tf rows for the batch's hot terms.  A term whose postings cover at
-// least 1/div of the docno span costs >= 8 B x span / div as (docno, tf)
-// postings but span bytes as a u8 tf-per-document row, so for div = 8 the row
-// is never more traffic -- and for the Zipf head (df ~ N) it is 8x less, one
-// coalesced 16-byte load per lane per tile instead of 32 scattered 4-byte loads.
-// Default div = 4 (measured on c3 with the LDS-accumulator path: 1/4 beat 1/2,
-// 1/8 and 1/32; with the register path 1/4, 1/8 and 1/16 are equal within noise
-// and 1/2 is 2.5 % slower).
-// drow[row] = dense row of skip row `row` or -1.  A term with any tf > 255 has
-// its dense row withdrawn (k_dense_drop) and stays on the posting path.
-constexpr int kDMax = 4;  // dense terms per query (query positions 0..3)
-constexpr int kRMax = 8;  // register path: terms per query (8 tf-byte rows in the 8 KiB of acc)
-__global__ void k_dense_mark(const int64_t *rdf, int64_t nrows, int64_t span, int64_t div, int32_t *flag) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
-    flag[r] = (div > 0 && rdf[r] > 0 && rdf[r] * div >= span) ? 1 : 0;
+// Per batch row: the largest weight of the term (its max tf is the first
+// posting of the reduce-order CSR, tf desc) folded into wmax (non-negative
+// doubles order like their bit patterns), and whether the term gets dense rows:
+// postings covering >= 1/div of the docno span, every tf <= 255.  A row costs
+// span bytes against >= 8 B x span / div of (docno, tf) postings.
+__global__ void k_row_stats(const int32_t *term_of_row, const int64_t *rdf, int64_t nrows, const int64_t *off,
+                            const int32_t *tf_o, const double *lut, const double *idf, int64_t span, int64_t div,
+                            int32_t *flag, unsigned long long *wmax_bits) {
+  unsigned long long wm = 0;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows + 1; r += (int64_t)gridDim.x * blockDim.x) {
+    int32_t fl = 0;
+    if (r < nrows && rdf[r] > 0) {
+      const int32_t t = term_of_row[r];
+      const int32_t mt = tf_o[off[t]];
+      const unsigned long long wb = (unsigned long long)__double_as_longlong(__dmul_rn(lut[mt], idf[t]));
+      wm = wb > wm ? wb : wm;
+      fl = (div > 0 && rdf[r] * div >= span && mt <= 255) ? 1 : 0;
+    }
+    flag[r] = fl;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long u = __shfl_xor(wm, o, 64);
+    wm = u > wm ? u : wm;
+  }
+  if ((threadIdx.x & 63) == 0 && wm) atomicMax(wmax_bits, wm);
 }
 __global__ void k_dense_rows(const int32_t *flag, const int32_t *scan, int64_t nrows, int64_t cap, int32_t *drow) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
     drow[r] = (flag[r] && scan[r] < cap) ? scan[r] : -1;
 }
-// one block per dense row (grid-stride): tf bytes at docno - dmin
+// Within a tile a dense row is stored lane-major: byte kDPL * l + b holds
+// document 64 b + l, so lane l's kDPL-byte load carries the documents it owns.
+__device__ __forceinline__ int64_t dense_pos(int64_t x) {
+  const int64_t r = x & (kWTile - 1);
+  return (x - r) + kDPL * (r & 63) + (r >> 6);
+}
+// one block per dense row (grid-stride): tf and impact bytes at docno - dmin
 __global__ __launch_bounds__(256) void k_dense_fill(const int32_t *drow, int64_t nrows, const int32_t *term_of_row,
                                                     const int64_t *off, const int32_t *docno, const int32_t *tf,
-                                                    int64_t dmin, int64_t stride, uint8_t *dense, int32_t *bad) {
+                                                    const double *lut, const double *idf,
+                                                    const unsigned long long *wmax_bits, int64_t dmin, int64_t stride,
+                                                    uint8_t *dtf, uint8_t *dq) {
+  const double wmax = __longlong_as_double((long long)*wmax_bits);
+  const double alpha = wmax > 0.0 ? 253.5 / wmax : 1.0;
   for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     const int32_t d = drow[r];
     if (d < 0) continue;
-    const int64_t b = off[term_of_row[r]], e = off[term_of_row[r] + 1];
-    uint8_t *row = dense + (int64_t)d * stride;
+    const int32_t t = term_of_row[r];
+    const int64_t b = off[t], e = off[t + 1];
+    const double widf = idf[t];
+    uint8_t *rt = dtf + (int64_t)d * stride, *rq = dq + (int64_t)d * stride;
     for (int64_t p = b + threadIdx.x; p < e; p += blockDim.x) {
-      const int32_t f = tf[p];
-      const int64_t x = (int64_t)docno[p] - dmin, r = x & (kWTile - 1);
-      row[(x - r) + 16 * (r & 63) + (r >> 6)] = (uint8_t)(f > 255 ? 0 : f);
-      if (f > 255) bad[d] = 1;
+      const int32_t f = tf[p];  // <= 255 (k_row_stats)
+      const int64_t pos = dense_pos((int64_t)docno[p] - dmin);
+      rt[pos] = (uint8_t)f;
+      rq[pos] = (uint8_t)impact(lut[f], widf, alpha);
     }
   }
 }
-__global__ void k_dense_drop(int32_t *drow, int64_t nrows, const int32_t *bad) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
-    if (drow[r] >= 0 && bad[drow[r]]) drow[r] = -1;
+
+// Query order for cache sharing: queries sorted by their heaviest term (largest
+// df, then smaller id) and second heaviest, so concurrent waves on one XCD read
+// the same rows / posting ranges.
+__global__ void k_query_keys(const int32_t *terms, const int64_t *qoff, int nq, const int64_t *off, int64_t V,
+                             uint64_t *keys, int32_t *idx) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+    int64_t d1 = -1, d2 = -1;
+    uint32_t t1 = 0xFFFFFFFFu, t2 = 0xFFFFFFFFu;
+    for (int64_t i = qoff[q]; i < qoff[q + 1]; i++) {
+      const int32_t t = terms[i];
+      if (t < 0 || t >= V) continue;
+      const int64_t d = off[t + 1] - off[t];
+      if (d > d1 || (d == d1 && (uint32_t)t < t1)) {
+        d2 = d1;
+        t2 = t1;
+        d1 = d;
+        t1 = (uint32_t)t;
+      } else if ((uint32_t)t != t1 && (d > d2 || (d == d2 && (uint32_t)t < t2))) {
+        d2 = d;
+        t2 = (uint32_t)t;
+      }
+    }
+    keys[q] = ((uint64_t)t1 << 32) | t2;
+    idx[q] = q;
+  }
 }
 
-// Within a tile a dense row is stored lane-major: byte 16 l + b holds document
-// 64 b + l, so lane l's 16-byte load carries documents l, l + 64, ..., and the
-// apply of byte b touches 64 consecutive accumulators (no LDS bank conflicts,
-// while the posting path keeps the natural acc[d] layout that consecutive
-// docnos hit conflict-free).
+// Bitonic sort of n (power of two) entries of one wave's LDS buffer, best
+// first (score desc, docno asc).  The workgroup is one wave, so the barriers
+// only order the LDS traffic.
+__device__ __forceinline__ void wave_sort(double *s, int32_t *d, int n) {
+  const int lane = threadIdx.x;
+  for (int size = 2; size <= n; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < (n >> 1); i += 64) {
+        const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1)), hi = lo + stride;
+        const double as = s[lo], bs = s[hi];
+        const int32_t ad = d[lo], bd = d[hi];
+        const bool sw = (lo & size) == 0 ? better(bs, bd, as, ad) : better(as, ad, bs, bd);
+        if (sw) {
+          s[lo] = bs;
+          d[lo] = bd;
+          s[hi] = as;
+          d[hi] = ad;
+        }
+      }
+      __syncthreads();
+    }
+}
 
-// One WAVE per query (no block barriers at all): the wave's fp64 accumulators
-// for a tile of kWTile documents live in its own LDS slice, and a wave's LDS
-// operations execute in program order, so applying term i's postings before
-// term i+1's reproduces the reference's left-to-right sum without any
-// synchronisation.  Per tile: lanes < nt read the term's skip-table entries,
-// then the wave streams the tile's postings of all its terms in batches of
-// kWBatch 64-posting chunks (all loads of a batch in flight together), applies
-// them in query-token order, and folds the tile into per-lane register top-k
-// lists; the next tile is the smallest tile holding a remaining posting.
-// kPath 1 = register path (queries that qualify, others skipped), 2 = LDS-
-// accumulator path (the rest): two launches, each kernel carrying only its own
-// registers.
-template <int KMAX, int kWBatch, int kPath>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ? 4 : 1))) void k_query_wave(const int64_t *__restrict__ off, const int32_t *__restrict__ docno,
-                                                   const int32_t *__restrict__ tf, const double *__restrict__ lut,
-                                                   int max_tf, const double *__restrict__ idf,
-                                                   const int32_t *__restrict__ row_of, const int32_t *__restrict__ sk,
-                                                   int64_t dmin, int64_t T, const int32_t *__restrict__ terms,
-                                                   const int64_t *__restrict__ qoff, int nq, int k, int32_t *out_d,
-                                                   double *out_s, const uint8_t *__restrict__ dense,
-                                                   const int32_t *__restrict__ drow, int64_t dstride, int fast) {
-  __shared__ double acc[kWTile];  // LDS-accumulator path; the register path reuses it as 8 tf-byte rows
+template <int C>
+__global__ __launch_bounds__(64) void k_query_imp(
+    const int64_t *__restrict__ off, const int32_t *__restrict__ docno, const int32_t *__restrict__ tf,
+    const double *__restrict__ lut, int max_tf, const double *__restrict__ idf, int64_t V,
+    const int32_t *__restrict__ row_of, const int32_t *__restrict__ sk, int64_t dmin, int64_t T,
+    const int32_t *__restrict__ terms, const int64_t *__restrict__ qoff, const int32_t *__restrict__ qorder, int nq,
+    int k, int32_t *out_d, double *out_s, const uint8_t *__restrict__ dtf, const uint8_t *__restrict__ dq,
+    const int32_t *__restrict__ drow, int64_t dstride, const unsigned long long *__restrict__ wmax_bits, int sh,
+    unsigned long long *stats, int exper) {
+  __shared__ uint32_t lacc[kDPL / 2 * 64];  // posting terms' impact sums, u16 pairs (documents 128 m + l, + 64)
+  __shared__ double bs[C];
+  __shared__ int32_t bd[C];
   __shared__ double s_lut[kWLut];
   const int lane = threadIdx.x;
-  for (int j = lane; j < kWTile; j += 64) acc[j] = -1.0;  // untouched (weights are >= 0)
   for (int j = lane; j < kWLut; j += 64) s_lut[j] = (j >= 1 && j <= max_tf) ? lut[j] : 0.0;
-  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+  const double wmax = __longlong_as_double((long long)*wmax_bits);
+  // dense impacts are bytes at scale alpha; posting terms' impacts and the
+  // gate use alpha * 2^sh (the dense sums are shifted by sh before the gate)
+  const double alpha = wmax > 0.0 ? 253.5 / wmax : 1.0;
+  const double alpha_s = __dmul_rn(alpha, (double)(1 << sh));
+  __syncthreads();
+  // queries in `qorder` (heaviest terms first) are dealt in 8 contiguous slices,
+  // slice x to the blocks b with b % 8 == x, which share an XCD and its L2
+  const int slice = (nq + 7) >> 3;
+  for (int qi = blockIdx.x; qi < 8 * slice; qi += gridDim.x) {
+    const int pos = (qi & 7) * slice + (qi >> 3);
+    if (pos >= nq) continue;
+    const int q = qorder ? qorder[pos] : pos;
     const int64_t q0 = qoff[q];
-    const int nt = (int)(qoff[q + 1] - q0);  // <= kTMaxTerms (host checked)
-    // lane i < nt holds term i: postings base, df, idf, skip row, dense row
+    const int nt = (int)(qoff[q + 1] - q0);  // <= kIMaxTerms (host checked)
+    // lane j < nt holds term j: postings base, df, idf, skip row, dense rows
     int64_t mb = 0;
     int32_t mdf = 0;
     double midf = 0.0;
@@ -429,29 +521,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
     int64_t mdr = -1;
     if (lane < nt) {
       const int32_t t = terms[q0 + lane];
-      if (t >= 0) {
+      if (t >= 0 && t < V) {  // unknown (-1) and out-of-range ids are skipped
         mb = off[t];
         mdf = (int32_t)(off[t + 1] - mb);
         midf = idf[t];
         mrow = sk + (int64_t)row_of[t] * (T + 1);
-        if (mdf > 0) nx = (int32_t)(((int64_t)docno[mb] - dmin) >> kWBits);
-        if (drow != nullptr && lane < kDMax && mdf > 0) mdr = drow[row_of[t]];
+        if (mdf > 0) {
+          nx = (int32_t)(((int64_t)docno[mb] - dmin) >> kWBits);
+          if (drow != nullptr) mdr = drow[row_of[t]];
+        }
       }
     }
     const bool isd = mdr >= 0;
-    const uint64_t dmask = (uint64_t)__ballot(isd);  // wave-uniform: query positions read from dense rows
-    // register path: <= kRMax terms, every known term's idf > 0 (a touched
-    // document then has a positive score, so "untouched" = 0), all tf <= 255
-    const bool fastq = fast && nt <= kRMax && __ballot(lane < nt && mdf > 0 && !(midf > 0.0)) == 0;
-    if (fastq != (kPath == 1)) continue;  // wave-uniform: the other launch takes it
-    const uint8_t *mdp = dense + (isd ? mdr * dstride : 0);  // row base (read lane-uniformly per term)
-    double ts[KMAX];
-    int32_t td[KMAX];
-#pragma unroll
-    for (int j = 0; j < KMAX; j++) {
-      ts[j] = -INFINITY;
-      td[j] = 0x7FFFFFFF;
-    }
+    const uint64_t dmask = (uint64_t)__ballot(isd);
+    const uint8_t *mq = dq + (isd ? mdr * dstride : 0), *mt = dtf + (isd ? mdr * dstride : 0);
+    int cnt = 0;  // buffer fill (wave-uniform)
+    uint32_t st_tiles = 0, st_gated = 0, st_cand = 0, st_comp = 0, st_sparse = 0;  // SME_QSTATS
+    bool th_ok = false;
+    double th_s = 0.0;
+    int32_t th_d = 0;
+    uint32_t gate = 1;  // touched documents only until k of them are held
+    // sort the buffer, keep the best k, raise th and the gate
+    auto compact = [&]() {
+      st_comp++;
+      int n2 = 2;
+      while (n2 < cnt) n2 <<= 1;
+      for (int i = cnt + lane; i < n2; i += 64) {
+        bs[i] = -INFINITY;
+        bd[i] = 0x7FFFFFFF;
+      }
+      __syncthreads();
+      wave_sort(bs, bd, n2);
+      cnt = min(cnt, k);
+      if (cnt >= k) {
+        th_ok = true;
+        th_s = bs[k - 1];
+        th_d = bd[k - 1];
+        const double g = floor(__dmul_rn(__dmul_rn(th_s, alpha_s), 1.0 - 0x1p-40));
+        gate = g > 1.0 ? (uint32_t)g : 1u;
+      }
+    };
     int32_t tile = nx;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) tile = min(tile, __shfl_xor(tile, o, 64));
@@ -461,8 +570,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
       me = mrow[tile + 1];
     }
     while (tile != 0x7FFFFFFF) {  // wave-uniform
-      // loads for the next step overlap this tile's batch loads: the next tile
-      // of this term, and (for the common case that it is tile + 1) its range end
+      // loads for the next step overlap this tile's work: the next tile of this
+      // term, and (for the common case that it is tile + 1) its range end
       nx = 0x7FFFFFFF;
       int32_t me1 = 0;
       if (lane < nt && me < mdf) {
@@ -472,217 +581,151 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
         me1 = mdf;
       }
       const int64_t dbase = dmin + ((int64_t)tile << kWBits);
-      if constexpr (kPath == 1) {
-        // Register path.  Every term with postings in the tile gets a row of
-        // 1024 tf bytes in LDS (lane-major: byte 16 l + b = document 64 b + l):
-        // dense terms copy their HBM row, posting terms are zeroed and their
-        // tf bytes scattered (one byte per (term, document): order-free).  Then
-        // lane l accumulates documents l + 64 b in 16 fp64 registers, term by
-        // term in query order: r = r + lut[tf] * idf with lut[0] = 0 adds an
-        // exact 0 for absent terms, so r is the reference's left-to-right sum.
-        uint8_t *rows = reinterpret_cast<uint8_t *>(acc);
-        const uint64_t amask = (uint64_t)__ballot(lane < nt && me > mc);
-        const uint64_t dm = dmask & amask, sm = amask & ~dmask;
+      const int64_t tbyte = (int64_t)tile << kWBits;
+      const uint64_t amask = (uint64_t)__ballot(lane < nt && me > mc);  // terms with postings in the tile
+      const uint64_t dm = amask & dmask, sm = amask & ~dmask;
+      const int64_t plo = mb + mc, phi = mb + me;  // this lane's term: postings in the tile
+      uint32_t a[kDPL / 2];
+      st_tiles++;
+      // dense terms: kDPL impact bytes per lane, four terms' loads in flight;
+      // the first four are issued before the posting pass so both overlap
+      uint64_t dmr = dm;
+      auto dense_load = [&](uint4 (&v)[4][kDPL / 16]) {
 #pragma unroll
-        for (int j = 0; j < kDMax; j++) {
-          if ((dm >> j) & 1) {
-            const uint8_t *pj = reinterpret_cast<const uint8_t *>(rl64((int64_t)mdp, j));
-            *reinterpret_cast<uint4 *>(rows + (j << kWBits) + 16 * lane) =
-                *reinterpret_cast<const uint4 *>(pj + ((int64_t)tile << kWBits) + 16 * lane);
-          }
-        }
-        for (uint64_t m = sm; m; m &= m - 1)
-          *reinterpret_cast<uint4 *>(rows + ((int)__builtin_ctzll(m) << kWBits) + 16 * lane) = make_uint4(0, 0, 0, 0);
-        int i = 0;
-        int64_t s = __shfl(mb + (isd ? me : mc), 0, 64), e = __shfl(mb + me, 0, 64);
-        for (;;) {
-          while (i < nt && s >= e) {
-            i++;
-            if (i < nt) {
-              s = __shfl(mb + (isd ? me : mc), i, 64);
-              e = __shfl(mb + me, i, 64);
-            }
-          }
-          if (i >= nt) break;
-          int32_t dv[kWBatch], fv[kWBatch];
-          int ti[kWBatch];
+        for (int g = 0; g < 4; g++) {
+          if (dmr) {
+            const int j = (int)__builtin_ctzll(dmr);
+            dmr &= dmr - 1;
+            const uint8_t *pj = reinterpret_cast<const uint8_t *>(rl64((int64_t)mq, j)) + tbyte + kDPL * lane;
 #pragma unroll
-          for (int m = 0; m < kWBatch; m++) {
-            while (i < nt && s >= e) {
-              i++;
-              if (i < nt) {
-                s = __shfl(mb + (isd ? me : mc), i, 64);
-                e = __shfl(mb + me, i, 64);
-              }
-            }
-            ti[m] = i;
-            const int64_t p = s + lane;
-            const bool v = i < nt && p < e;
-            dv[m] = v ? docno[p] : 0;
-            fv[m] = v ? tf[p] : 0;
-            s += 64;
-          }
-#pragma unroll
-          for (int m = 0; m < kWBatch; m++) {
-            if (fv[m] == 0) continue;
-            const int d = (int)((int64_t)dv[m] - dbase);
-            rows[(ti[m] << kWBits) + 16 * (d & 63) + (d >> 6)] = (uint8_t)fv[m];
-          }
-        }
-        // two halves of 8 documents per lane keep the live registers low
-        double r0[8], fth = 0.0;
-        bool fold = false;
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          double r[8];
-#pragma unroll
-          for (int b = 0; b < 8; b++) r[b] = 0.0;
-          for (uint64_t m = amask; m; m &= m - 1) {
-            const int j = (int)__builtin_ctzll(m);  // ascending position = query-token order
-            const double widf = __shfl(midf, j, 64);
-            const uint2 v = *reinterpret_cast<const uint2 *>(rows + (j << kWBits) + 16 * lane + 8 * h);
-#pragma unroll
-            for (int b = 0; b < 8; b++) {
-              const int f = (int)(((b < 4 ? v.x : v.y) >> (8 * (b & 3))) & 0xFF);
-              r[b] = __dadd_rn(r[b], __dmul_rn(s_lut[f], widf));
-            }
-          }
-          // the rows live in acc: the first half's sums wait in registers
-          // until the second half has read its bytes
-          if (h == 0) {
-#pragma unroll
-            for (int b = 0; b < 8; b++) r0[b] = r[b];
+            for (int c = 0; c < kDPL / 16; c++) v[g][c] = *reinterpret_cast<const uint4 *>(pj + 16 * c);
           } else {
-            // th = the best KMAX-th score over the lanes' lists: that lane holds
-            // KMAX documents scoring >= th, so a document below th cannot reach
-            // the final top-k.  Most tiles then skip the fold entirely.
-            double th = ts[KMAX - 1], mx = 0.0;
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) th = fmax(th, __shfl_xor(th, o, 64));
-#pragma unroll
-            for (int b = 0; b < 8; b++) mx = fmax(mx, fmax(r0[b], r[b]));
-            fold = __ballot(mx > 0.0 && mx >= th) != 0;
-            if (fold) {
-#pragma unroll
-              for (int b = 0; b < 8; b++) {
-                acc[(b << 6) | lane] = r0[b];
-                acc[((b + 8) << 6) | lane] = r[b];
-              }
-            }
-            fth = th;
+            for (int c = 0; c < kDPL / 16; c++) v[g][c] = make_uint4(0, 0, 0, 0);
           }
         }
-        // fold through LDS (one topk_insert site keeps the register budget):
-        // document 64 b + lane at acc[64 b + lane]
-        if (fold) {
-          for (int j = lane; j < kWTile; j += 64) {
-            const double sc = acc[j];
-            if (sc > 0.0 && sc >= fth) topk_insert<KMAX>(ts, td, sc, (int32_t)(dbase + j));
-          }
-        }
-      } else {
-      // dense terms with postings in this tile: their 16 tf bytes per lane, all
-      // loads issued before the posting batches
-      const uint64_t tmask = dmask & (uint64_t)__ballot(isd && me > mc);
-      uint4 dz[kDMax];
+      };
+      auto dense_add = [&](const uint4 (&v)[4][kDPL / 16]) {
 #pragma unroll
-      for (int j = 0; j < kDMax; j++) {
-        if ((tmask >> j) & 1) {
-          const uint8_t *pj = reinterpret_cast<const uint8_t *>(rl64((int64_t)mdp, j));
-          dz[j] = *reinterpret_cast<const uint4 *>(pj + ((int64_t)tile << kWBits) + 16 * lane);
-        } else {
-          dz[j] = make_uint4(0, 0, 0, 0);
-        }
-      }
-      int da = 0;  // dense terms at positions < da are applied (wave-uniform)
-      // apply dense terms at positions [da, lim) in query order
-      auto dense_upto = [&](int lim) {
+        for (int g = 0; g < 4; g++)
 #pragma unroll
-        for (int j = 0; j < kDMax; j++) {
-          if (j >= da && j < lim && ((tmask >> j) & 1)) {
-            const double widf = __shfl(midf, j, 64);
-#pragma unroll 1
+          for (int c = 0; c < kDPL / 16; c++) {
+            const uint32_t w4[4] = {v[g][c].x, v[g][c].y, v[g][c].z, v[g][c].w};
+#pragma unroll
             for (int u = 0; u < 4; u++) {
-              const uint32_t wd = u == 0 ? dz[j].x : u == 1 ? dz[j].y : u == 2 ? dz[j].z : dz[j].w;
+              a[8 * c + 2 * u] += __builtin_amdgcn_perm(0u, w4[u], 0x0C010C00u);
+              a[8 * c + 2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
+            }
+          }
+      };
+      uint4 v0[4][kDPL / 16];
+      dense_load(v0);
+      if (sm && !(exper & 2)) {
+        st_sparse++;
+        // posting terms: impacts added into LDS (order-free integer sums)
 #pragma unroll
-              for (int b = 0; b < 4; b++) {
-                const int f = (int)((wd >> (8 * b)) & 0xFF);
-                if (f == 0) continue;
-                const double l = f < kWLut ? s_lut[f] : lut[f];
-                const double w = __dmul_rn(l, widf);
-                const int x = (((u << 2) | b) << 6) | lane;
-                const double a = acc[x];
-                acc[x] = a < 0.0 ? w : __dadd_rn(a, w);
+        for (int m = 0; m < kDPL / 2; m++) lacc[m * 64 + lane] = 0;
+        __syncthreads();
+        // the tile's postings of all posting terms as one list, 256 per step:
+        // entry x belongs to the last term j of sm with pre_j <= x
+        const int32_t cj = ((sm >> lane) & 1) ? me - mc : 0;
+        const int32_t incl = wave_incl_sum(cj), prej = incl - cj;
+        const int32_t total = __shfl(incl, 63, 64);
+        for (int32_t x0 = 0; x0 < total; x0 += 256) {
+          int32_t dv[4], fv[4];
+          double wv[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const int32_t x = x0 + 64 * u + lane;
+            int64_t pb = 0;
+            double wj = 0.0;
+            for (uint64_t m = sm; m; m &= m - 1) {
+              const int j = (int)__builtin_ctzll(m);
+              const int32_t pj = __builtin_amdgcn_readlane(prej, j);
+              if (x >= pj) {
+                pb = rl64(plo, j) - pj;
+                wj = rld(midf, j);
               }
             }
+            const bool v = x < total;
+            dv[u] = v ? docno[pb + x] : 0;
+            fv[u] = v ? tf[pb + x] : 0;
+            wv[u] = wj;
           }
-        }
-        da = lim > da ? lim : da;
-      };
-      // walk (term i, position s) over all chunks of the tile, kWBatch at a time;
-      // dense terms have empty posting ranges here
-      // bar = query position of the next dense term still to apply (nt if none):
-      // a batch never holds postings of a term at or past it, so every
-      // document's adds stay in query-token order
-      auto next_bar = [&]() {
-        const uint64_t r = tmask >> da;
-        const int b = r ? da + (int)__builtin_ctzll(r) : nt;
-        return b < nt ? b : nt;
-      };
-      int bar = next_bar();
-      int i = 0;
-      int64_t s = __shfl(mb + (isd ? me : mc), 0, 64), e = __shfl(mb + me, 0, 64);
-      for (;;) {
-        while (i < bar && s >= e) {  // advance to the next term with postings left in this tile
-          i++;
-          if (i < nt) {
-            s = __shfl(mb + (isd ? me : mc), i, 64);
-            e = __shfl(mb + me, i, 64);
-          }
-        }
-        if (i >= bar) {
-          if (bar >= nt) break;
-          dense_upto(bar + 1);  // the dense term at position bar
-          bar = next_bar();
-          continue;  // its posting range is empty: the advance moves past it
-        }
-        int32_t dv[kWBatch], fv[kWBatch];
-        int ti[kWBatch];
 #pragma unroll
-        for (int m = 0; m < kWBatch; m++) {
-          while (i < bar && s >= e) {
-            i++;
-            if (i < nt) {
-              s = __shfl(mb + (isd ? me : mc), i, 64);
-              e = __shfl(mb + me, i, 64);
+          for (int u = 0; u < 4; u++) {
+            if (fv[u] == 0) continue;
+            const int r = (int)((int64_t)dv[u] - dbase);
+            const double l = fv[u] < kWLut ? s_lut[fv[u]] : lut[fv[u]];
+            atomicAdd(&lacc[((r >> 7) << 6) | (r & 63)], impact(l, wv[u], alpha_s) << (((r >> 6) & 1) << 4));
+          }
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int m = 0; m < kDPL / 2; m++) a[m] = 0;
+      dense_add(v0);
+      while (dmr) {
+        uint4 v[4][kDPL / 16];
+        dense_load(v);
+        dense_add(v);
+      }
+      // A = (dense sums << sh) + posting-term sums: u16 fields never carry
+      // (host: 255 * 2^sh * terms <= 65535)
+#pragma unroll
+      for (int m = 0; m < kDPL / 2; m++) a[m] = (a[m] << sh) + (sm && !(exper & 2) ? lacc[m * 64 + lane] : 0u);
+      // gate: most tiles hold no document whose impact sum reaches it
+      uint32_t mx = a[0];
+#pragma unroll
+      for (int m = 1; m < kDPL / 2; m++) mx = pkmax_u16(mx, a[m]);
+      if (!(exper & 1) && __ballot(max(mx & 0xFFFFu, mx >> 16) >= gate) != 0) {
+        uint32_t cm = 0;
+#pragma unroll
+        for (int b = 0; b < kDPL; b++)
+          if (((a[b >> 1] >> ((b & 1) << 4)) & 0xFFFFu) >= gate) cm |= 1u << b;
+        st_gated++;
+        if (stats) st_cand += (uint32_t)__popc(cm);
+        for (;;) {
+          const bool have = cm != 0;
+          if (__ballot(have) == 0) break;  // wave-uniform
+          double S = 0.0;
+          int32_t d = 0x7FFFFFFF;
+          bool keep = false;
+          if (have) {
+            const int b = (int)__builtin_ctz(cm);
+            cm &= cm - 1;
+            d = (int32_t)(dbase + ((b << 6) | lane));
+            // exact score: query-token order, fp64, as rank() accumulates it
+            for (uint64_t m = amask; m; m &= m - 1) {
+              const int j = (int)__builtin_ctzll(m);
+              int f = 0;
+              if ((dmask >> j) & 1) {
+                f = reinterpret_cast<const uint8_t *>(rl64((int64_t)mt, j))[tbyte + kDPL * lane + b];
+              } else {
+                int64_t lo = rl64(plo, j);
+                const int64_t e = rl64(phi, j);
+                int64_t hi = e;
+                while (lo < hi) {
+                  const int64_t mid = (lo + hi) >> 1;
+                  if (docno[mid] < d) lo = mid + 1;
+                  else hi = mid;
+                }
+                if (lo < e && docno[lo] == d) f = tf[lo];
+              }
+              if (f != 0) S = __dadd_rn(S, __dmul_rn(f < kWLut ? s_lut[f] : lut[f], rld(midf, j)));
             }
+            keep = !th_ok || better(S, d, th_s, th_d);
           }
-          ti[m] = i;
-          const int64_t p = s + lane;
-          const bool v = i < bar && p < e;
-          dv[m] = v ? docno[p] : -1;
-          fv[m] = v ? tf[p] : 0;
-          s += 64;
-        }
-#pragma unroll
-        for (int m = 0; m < kWBatch; m++) {
-          const double widf = __shfl(midf, ti[m] < nt ? ti[m] : 0, 64);  // ti[m] is wave-uniform
-          if (fv[m] == 0) continue;                                        // tf >= 1 on every posting
-          const int d = (int)((int64_t)dv[m] - dbase);
-          const int f = fv[m];
-          const double l = f < kWLut ? s_lut[f] : lut[f];
-          const double w = __dmul_rn(l, widf);
-          const double a = acc[d];
-          acc[d] = a < 0.0 ? w : __dadd_rn(a, w);
+          const uint64_t km = (uint64_t)__ballot(keep);
+          if (keep) {
+            const int pos = cnt + (int)lane_prefix(km);
+            bs[pos] = S;
+            bd[pos] = d;
+          }
+          cnt += __popcll(km);
+          if (cnt > C - 64) compact();
         }
       }
-      for (int j = lane; j < kWTile; j += 64) {
-        const double sc = acc[j];
-        if (sc < 0.0) continue;
-        acc[j] = -1.0;
-        topk_insert<KMAX>(ts, td, sc, (int32_t)(dbase + j));
-      }
-      }  // LDS-accumulator path
       int32_t nt_ = nx;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) nt_ = min(nt_, __shfl_xor(nt_, o, 64));
@@ -695,46 +738,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMAX <= 10 ?
       }
       tile = nt_;
     }
-    // k rounds of wave arg-max over the lanes' list heads
-    for (int r = 0; r < k; r++) {
-      double bs = ts[0];
-      int32_t bd = td[0];
-      int32_t bt = lane;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double os = __shfl_xor(bs, o, 64);
-        const int32_t od = __shfl_xor(bd, o, 64), ot = __shfl_xor(bt, o, 64);
-        if (better(os, od, bs, bd) || (os == bs && od == bd && ot < bt)) {
-          bs = os;
-          bd = od;
-          bt = ot;
-        }
-      }
-      if (lane == bt) {
-#pragma unroll
-        for (int j = 0; j < KMAX - 1; j++) {
-          ts[j] = ts[j + 1];
-          td[j] = td[j + 1];
-        }
-        ts[KMAX - 1] = -INFINITY;
-        td[KMAX - 1] = 0x7FFFFFFF;
-      }
+    __syncthreads();
+    compact();
+    if (stats) {
+      uint32_t c = st_cand;
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
       if (lane == 0) {
-        const bool valid = bs != -INFINITY;
-        out_d[(int64_t)q * k + r] = valid ? bd : -1;
-        out_s[(int64_t)q * k + r] = valid ? bs : 0.0;
+        atomicAdd(stats + 0, (unsigned long long)st_tiles);
+        atomicAdd(stats + 1, (unsigned long long)st_gated);
+        atomicAdd(stats + 2, (unsigned long long)c);
+        atomicAdd(stats + 3, (unsigned long long)st_comp);
+        atomicAdd(stats + 4, (unsigned long long)st_sparse);
       }
     }
+    for (int r = lane; r < k; r += 64) {
+      out_d[(int64_t)q * k + r] = r < cnt ? bd[r] : -1;
+      out_s[(int64_t)q * k + r] = r < cnt ? bs[r] : 0.0;
+    }
+    __syncthreads();
   }
 }
 
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k, int32_t *d_out_docno,
                 double *d_out_score, hipStream_t st) {
   if (k < 1) throw Error(SME_EINVAL, "k must be >= 1");
-  if (k > 32) throw Error(SME_ENOTIMPL, "top-k with k > 32 is not built yet");
+  if (k > 448) throw Error(SME_ELIMIT, "top-k with k > 448");
   if (nq <= 0) return;
   auto &W = ix->ctx->ws;
   int *err = W[63].as<int>(4);
+  unsigned long long *wmax = reinterpret_cast<unsigned long long *>(err + 2);
   SME_HIP(hipMemsetAsync(err, 0, 4 * sizeof(int), st));
   const int64_t *off = (const int64_t *)ix->d_off.p;
   const int32_t *dn = (const int32_t *)ix->d_docno_d.p;
@@ -742,28 +774,26 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   const double *lut = (const double *)ix->d_lut.p;
   const double *idf = (const double *)ix->d_idf.p;
   const int64_t V = ix->V;
-  unsigned grid = (unsigned)std::min(nq, 1 << 20);
   hipEvent_t ep;
   SME_HIP(hipEventCreate(&ep));
   SME_HIP(hipEventRecord(ep, st));
-  // Tiled path unless a query is longer than kTMaxTerms, tf does not pack, or the
-  // batch's skip table would be unreasonably large; SME_QUERY_KERNEL=stream forces
-  // the streaming kernel (tests run both).
+  // Tiled path unless a query is longer than kIMaxTerms or the batch's skip
+  // table would be unreasonably large; SME_QUERY_KERNEL=stream forces the
+  // streaming kernel (tests run both).
   const char *force = getenv("SME_QUERY_KERNEL");
-  bool tiled = V > 0 && ix->P > 0 && ix->dmax >= ix->dmin &&
-               !(force && strcmp(force, "stream") == 0);
+  bool tiled = V > 0 && ix->P > 0 && ix->dmax >= ix->dmin && !(force && strcmp(force, "stream") == 0);
   const int64_t T = tiled ? ((ix->dmax - ix->dmin) >> kWBits) + 1 : 0;
   const int32_t *row_of = nullptr, *sk = nullptr, *drow = nullptr;
-  const uint8_t *dense = nullptr;
+  const uint8_t *dtf = nullptr, *dq = nullptr;
   int64_t dstride = 0;
+  int h_mx = 0;
   if (tiled) {
     hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
-    int h_mx = 0;
     SME_HIP(hipMemcpyAsync(&h_mx, err + 1, sizeof(int), hipMemcpyDeviceToHost, st));
     int64_t nterm = 0;
     SME_HIP(hipMemcpyAsync(&nterm, d_qoff + nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
-    tiled = h_mx <= kTMaxTerms;
+    tiled = h_mx <= kIMaxTerms;
     if (tiled) {
       // distinct batch terms -> rows of the skip table
       int32_t *mark = W[55].as<int32_t>(V + 1), *rowo = W[56].as<int32_t>(V + 1);
@@ -780,60 +810,79 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       const int64_t nrows = nrows32;
       if ((double)nrows * (double)(T + 1) * 4.0 > 8.0e9) {
         tiled = false;
-      } else if (nrows > 0) {
-        int32_t *tor = W[57].as<int32_t>(nrows + 1);
-        int64_t *rdf = W[58].as<int64_t>(nrows + 1), *rpre = W[59].as<int64_t>(nrows + 1);
-        const unsigned gV = (unsigned)std::min<int64_t>((V + 255) / 256, 8192);
-        hipLaunchKernelGGL(k_term_rows, dim3(gV), dim3(256), 0, st, mark, rowo, V, off, tor, rdf);
-        SME_HIP(hipMemsetAsync(rdf + nrows, 0, sizeof(int64_t), st));
-        SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, rdf, rpre, (int)nrows + 1, st));
-        SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, rdf, rpre, (int)nrows + 1, st));
-        int32_t *skw = W[60].as<int32_t>(nrows * (T + 1));
-        SME_HIP(hipMemsetAsync(skw, 0x7F, (size_t)nrows * (T + 1) * sizeof(int32_t), st));
-        hipLaunchKernelGGL(k_skip_zero_rows, dim3((unsigned)std::min<int64_t>(nrows, 4096)), dim3(256), 0, st, rdf,
-                           nrows, T, skw);
-        hipLaunchKernelGGL(k_skip_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T, skw);
-        hipLaunchKernelGGL(k_skip_suffix, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 16384)), dim3(256), 0, st,
-                           nrows, T, skw);
-        SME_CHECK_LAUNCH();
-        row_of = rowo;
-        sk = skw;
-        // dense tf rows for terms covering >= 1/div of the docno span
-        // (SME_QDENSE=div, 0 = posting path only; tests run several)
-        const char *ed = getenv("SME_QDENSE");
-        const int64_t ddiv = ed ? atoll(ed) : 4;
-        const int64_t span = ix->dmax - ix->dmin + 1, stride = T << kWBits;
-        if (ddiv > 0) {
-          const int64_t cap = std::max<int64_t>(1, (int64_t)4e9 / stride);
-          int32_t *flag = W[53].as<int32_t>(nrows + 1), *dscan = W[54].as<int32_t>(nrows + 1);
-          const unsigned gR = (unsigned)std::min<int64_t>((nrows + 256) / 256, 8192);
-          hipLaunchKernelGGL(k_dense_mark, dim3(gR), dim3(256), 0, st, rdf, nrows + 1, span, ddiv, flag);
-          SME_HIP(hipMemsetAsync(flag + nrows, 0, sizeof(int32_t), st));
-          SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, flag, dscan, (int)nrows + 1, st));
-          SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, flag, dscan, (int)nrows + 1, st));
-          int32_t ndense = 0;
-          SME_HIP(hipMemcpyAsync(&ndense, dscan + nrows, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-          SME_HIP(hipStreamSynchronize(st));
-          const int64_t nd = std::min<int64_t>(ndense, cap);
-          if (nd > 0) {
-            int32_t *drw = W[62].as<int32_t>(nrows), *bad = W[52].as<int32_t>(nd);
-            uint8_t *dns = W[61].as<uint8_t>(nd * stride);
-            SME_HIP(hipMemsetAsync(dns, 0, (size_t)(nd * stride), st));
-            SME_HIP(hipMemsetAsync(bad, 0, (size_t)nd * sizeof(int32_t), st));
-            hipLaunchKernelGGL(k_dense_rows, dim3(gR), dim3(256), 0, st, flag, dscan, nrows, cap, drw);
-            hipLaunchKernelGGL(k_dense_fill, dim3((unsigned)std::min<int64_t>(nrows, 8192)), dim3(256), 0, st, drw,
-                               nrows, tor, off, dn, tf, ix->dmin, stride, dns, bad);
-            hipLaunchKernelGGL(k_dense_drop, dim3(gR), dim3(256), 0, st, drw, nrows, bad);
-            SME_CHECK_LAUNCH();
-            dense = dns;
-            drow = drw;
-            dstride = stride;
-          }
-        }
       } else {
         row_of = rowo;
-        sk = W[60].as<int32_t>(T + 1);
+        int32_t *skw = W[60].as<int32_t>(std::max<int64_t>(nrows, 1) * (T + 1));
+        sk = skw;
+        if (nrows > 0) {
+          int32_t *tor = W[57].as<int32_t>(nrows + 1);
+          int64_t *rdf = W[58].as<int64_t>(nrows + 1), *rpre = W[59].as<int64_t>(nrows + 1);
+          const unsigned gV = (unsigned)std::min<int64_t>((V + 255) / 256, 8192);
+          hipLaunchKernelGGL(k_term_rows, dim3(gV), dim3(256), 0, st, mark, rowo, V, off, tor, rdf);
+          SME_HIP(hipMemsetAsync(rdf + nrows, 0, sizeof(int64_t), st));
+          SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, rdf, rpre, (int)nrows + 1, st));
+          SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, rdf, rpre, (int)nrows + 1, st));
+          SME_HIP(hipMemsetAsync(skw, 0x7F, (size_t)nrows * (T + 1) * sizeof(int32_t), st));
+          hipLaunchKernelGGL(k_skip_zero_rows, dim3((unsigned)std::min<int64_t>(nrows, 4096)), dim3(256), 0, st, rdf,
+                             nrows, T, skw);
+          hipLaunchKernelGGL(k_skip_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T, skw);
+          hipLaunchKernelGGL(k_skip_suffix, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 16384)), dim3(256), 0,
+                             st, nrows, T, skw);
+          // largest weight of the batch (impact scale) and the dense-row terms
+          // (SME_QDENSE=div, 0 = posting path only; tests run several)
+          const char *ed = getenv("SME_QDENSE");
+          const int64_t ddiv = ed ? atoll(ed) : 16;
+          const int64_t span = ix->dmax - ix->dmin + 1, stride = T << kWBits;
+          int32_t *flag = W[53].as<int32_t>(nrows + 1), *dscan = W[54].as<int32_t>(nrows + 1);
+          const unsigned gR = (unsigned)std::min<int64_t>((nrows + 256) / 256, 8192);
+          hipLaunchKernelGGL(k_row_stats, dim3(gR), dim3(256), 0, st, tor, rdf, nrows, off,
+                             (const int32_t *)ix->d_tf_o.p, lut, idf, span, ddiv, flag, wmax);
+          SME_CHECK_LAUNCH();
+          if (ddiv > 0) {
+            const int64_t cap = std::max<int64_t>(1, (int64_t)2e9 / stride);
+            SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, flag, dscan, (int)nrows + 1, st));
+            SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, flag, dscan, (int)nrows + 1, st));
+            int32_t ndense = 0;
+            SME_HIP(hipMemcpyAsync(&ndense, dscan + nrows, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            SME_HIP(hipStreamSynchronize(st));
+            const int64_t nd = std::min<int64_t>(ndense, cap);
+            if (nd > 0) {
+              int32_t *drw = W[62].as<int32_t>(nrows);
+              uint8_t *dns = W[61].as<uint8_t>(2 * nd * stride);
+              SME_HIP(hipMemsetAsync(dns, 0, (size_t)(2 * nd * stride), st));
+              hipLaunchKernelGGL(k_dense_rows, dim3(gR), dim3(256), 0, st, flag, dscan, nrows, cap, drw);
+              hipLaunchKernelGGL(k_dense_fill, dim3((unsigned)std::min<int64_t>(nrows, 8192)), dim3(256), 0, st, drw,
+                                 nrows, tor, off, dn, tf, lut, idf, wmax, ix->dmin, stride, dns, dns + nd * stride);
+              SME_CHECK_LAUNCH();
+              dtf = dns;
+              dq = dns + nd * stride;
+              drow = drw;
+              dstride = stride;
+            }
+          }
+        }
       }
+    }
+  }
+  if (!tiled && k > 32) throw Error(SME_ENOTIMPL, "top-k with k > 32 for queries of more than 64 terms");
+  int sh = 0;
+  const int32_t *qord = nullptr;
+  if (tiled) {
+    // impact shift: 255 * 2^sh * (terms per query) <= 65535 keeps the u16 sums exact
+    sh = 0;
+    while (sh < 5 && 255 * (2 << sh) * std::max(h_mx, 1) <= 65535) sh++;
+    // heaviest-term query order (SME_QORDER=0: batch order)
+    const char *eo = getenv("SME_QORDER");
+    if (!(eo && atoi(eo) == 0)) {
+      uint64_t *qk = W[46].as<uint64_t>(2 * (size_t)nq);
+      int32_t *qi = W[45].as<int32_t>(2 * (size_t)nq);
+      hipLaunchKernelGGL(k_query_keys, dim3(std::min((nq + 255) / 256, 4096)), dim3(256), 0, st, d_terms, d_qoff, nq, off,
+                         V, qk, qi);
+      size_t tbb = 0;
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, qk, qk + nq, qi, qi + nq, nq, 0, 64, st));
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(ix->ctx->cub_tmp.get(tbb), tbb, qk, qk + nq, qi, qi + nq, nq, 0, 64,
+                                                 st));
+      qord = qi + nq;
     }
   }
   // events on the launch stream bracket the scoring kernel (bench.py roofline)
@@ -841,38 +890,32 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   SME_HIP(hipEventCreate(&e0));
   SME_HIP(hipEventCreate(&e1));
   SME_HIP(hipEventRecord(e0, st));
+  const char *ex = getenv("SME_QEXP");  // timing experiments only (wrong results): 1 no candidates, 2 no postings
+  const int qexp = ex ? atoi(ex) : 0;
+  unsigned long long *qstats = nullptr;
+  const char *eq = getenv("SME_QSTATS");
+  if (eq && atoi(eq)) {
+    qstats = reinterpret_cast<unsigned long long *>(W[47].as<uint64_t>(8));
+    SME_HIP(hipMemsetAsync(qstats, 0, 8 * sizeof(uint64_t), st));
+  }
   if (tiled) {
-    const unsigned wgrid = (unsigned)std::min(nq, 1 << 22);
-    const char *eb = getenv("SME_QBATCH");
-    const char *ef = getenv("SME_QREG");  // 0 = LDS-accumulator path only (tests run both)
-    const int fast = (ix->max_tf <= 255 && !(ef && atoi(ef) == 0)) ? 1 : 0;
-    const int bsel = eb ? atoi(eb) : kWBatchDefault;
-#define SME_QW1(KM, BT, PATH)                                                                                  \
-  hipLaunchKernelGGL((k_query_wave<KM, BT, PATH>), dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf,  \
-                     row_of, sk, ix->dmin, T, d_terms, d_qoff, nq, k, d_out_docno, d_out_score, dense, drow, dstride, \
-                     fast)
-#define SME_QW(KM, BT)          \
-  do {                          \
-    if (fast) SME_QW1(KM, 8, 1);  \
-    SME_QW1(KM, BT, 2);         \
-  } while (0)
-    if (k <= 10) {
-      if (bsel == 16) SME_QW(10, 16);
-      else if (bsel == 4) SME_QW(10, 4);
-      else SME_QW(10, 8);
-    } else if (k <= 16) {
-      SME_QW(16, 8);
-    } else {
-      SME_QW(32, 8);
-    }
-#undef SME_QW
-#undef SME_QW1
+    const unsigned wgrid = (unsigned)std::min<int64_t>(8 * (((int64_t)nq + 7) / 8), 1 << 30);
+#define SME_QI(C)                                                                                                \
+  hipLaunchKernelGGL(k_query_imp<C>, dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, row_of, sk, \
+                     ix->dmin, T, d_terms, d_qoff, qord, nq, k, d_out_docno, d_out_score, dtf, dq, drow, dstride,    \
+                     (const unsigned long long *)wmax, sh, qstats, qexp)
+    if (k <= 64) SME_QI(128);
+    else if (k <= 192) SME_QI(256);
+    else SME_QI(512);
+#undef SME_QI
   } else if (k <= 16) {
-    hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff,
-                       nq, k, d_out_docno, d_out_score, err);
+    const unsigned grid = (unsigned)std::min(nq, 1 << 20);
+    hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
+                       d_qoff, nq, k, d_out_docno, d_out_score, err);
   } else {
-    hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, d_terms, d_qoff,
-                       nq, k, d_out_docno, d_out_score, err);
+    const unsigned grid = (unsigned)std::min(nq, 1 << 20);
+    hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
+                       d_qoff, nq, k, d_out_docno, d_out_score, err);
   }
   SME_CHECK_LAUNCH();
   SME_HIP(hipEventRecord(e1, st));
@@ -888,6 +931,13 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   ix->ctx->last_query_tiled = tiled;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  if (qstats) {
+    uint64_t h[8];
+    SME_HIP(hipMemcpy(h, qstats, sizeof h, hipMemcpyDeviceToHost));
+    fprintf(stderr, "SME_QSTATS tiles=%llu gated=%llu candidates=%llu compactions=%llu sparse_tiles=%llu\n",
+            (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
+            (unsigned long long)h[4]);
+  }
   if (h_err) throw Error(SME_ELIMIT, "a query has more than 128 terms");
 }
 

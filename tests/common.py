@@ -94,3 +94,29 @@ def fuzz_corpus(seed, n_docs, hard=True, extra_docids=0, with_quirks=True):
         body = "junk before <<DOC> x </DOC>\n" + body + "<DOC>\n<DOCNO>TAIL</DOCNO> unterminated"
     mapping = sorted(set(ids))
     return body.encode("utf-8"), mapping
+
+
+def canon_digest(buf):
+    """sha256 of a partition's record stream with the " " doc-counter record's
+    postings sorted (their order is Hadoop-defined): equal digests
+    <=> compare_partitions passes.  Only the " " record is parsed."""
+    import hashlib
+    import numpy as np
+    h = hashlib.sha256()
+    i, n = 0, len(buf)
+    while i < n:
+        rl, kl = struct.unpack_from(">ii", buf, i)
+        if kl == 11 and buf[i + 8:i + 15] == b"\x00\x00\x00\x01\x00\x01 ":
+            df = struct.unpack_from(">i", buf, i + 15)[0]
+            val = buf[i + 8 + kl:i + 8 + rl]
+            cnt = struct.unpack_from(">i", val, 0)[0]
+            h.update(b"SPACE%d:" % df)
+            if cnt > 0:
+                cl = struct.unpack_from(">H", val, 4)[0]
+                p = np.frombuffer(val, dtype=">i4", offset=6 + cl, count=2 * cnt).reshape(cnt, 2)
+                order = np.lexsort((p[:, 1], p[:, 0]))
+                h.update(p[order].astype(">i4").tobytes())
+        else:
+            h.update(buf[i:i + 8 + rl])
+        i += 8 + rl
+    return h.hexdigest()

@@ -40,6 +40,7 @@ def lib():
         L.or_query_utf8.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_void_p, C.c_void_p]
         L.or_last_error.restype = C.c_char_p
+        L.or_lookup_selfcheck.argtypes = [C.c_void_p]
         L.or_split_records.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]
         L.or_chargram.restype = C.c_void_p
         L.or_chargram.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int]
@@ -167,6 +168,10 @@ class OracleIndex:
             out.append((tuple(gram), L.or_index_term_part(self._h, t), L.or_index_term_df_field(self._h, t),
                         [(d[i], f[i]) for i in range(n)]))
         return out
+
+    def lookup_selfcheck(self):
+        """disagreements between the forward-index lookup table and the O(V) scan"""
+        return lib().or_lookup_selfcheck(self._h)
 
     def query(self, terms, k=10, idf_mode=0, order=0):
         """rank() over already-processed query terms; order 0 docno tie-break,

@@ -158,13 +158,15 @@ def _query_env(ix, terms, qoff, k, **env):
 
 
 def _query_both_kernels(ix, terms, qoff, k):
-    """Default (tiled: register path for queries of <= 8 terms with idf > 0,
-    dense rows for hot terms) scoring, the tiled kernel on postings only, every
-    term on dense rows, the LDS-accumulator path only, and the streaming kernel:
-    all identical bits."""
+    """Default tiled scoring (impact-gated, dense rows for terms covering >= 1/4
+    of the docno span), the tiled kernel on postings only, every term on dense
+    rows, only full-span terms dense, and the streaming kernel (k <= 32): all
+    identical bits."""
     dn, sc = ix.query_topk(terms, qoff, k)
-    for env in ({"SME_QUERY_KERNEL": "stream"}, {"SME_QDENSE": 0}, {"SME_QDENSE": 1 << 30},
-                {"SME_QDENSE": 1 << 30, "SME_QBATCH": 4}, {"SME_QREG": 0}, {"SME_QREG": 0, "SME_QDENSE": 0}):
+    envs = [{"SME_QDENSE": 0}, {"SME_QDENSE": 1 << 30}, {"SME_QDENSE": 1}]
+    if k <= 32:
+        envs.append({"SME_QUERY_KERNEL": "stream"})
+    for env in envs:
         dn2, sc2 = _query_env(ix, terms, qoff, k, **env)
         assert np.array_equal(dn, dn2) and np.array_equal(sc, sc2), env
     return dn, sc

@@ -135,3 +135,51 @@ def test_chargram_oracle_vs_python(k, R):
     exp = P.chargram_parts(corpus, k, R)
     for p in range(R):
         assert o.part_bytes(p) == exp[p], p
+
+
+def _py_rank(ix, terms, k, idf_mode):
+    """rank() restated in Python with the reference's list + indexOf accumulator
+    (IntDocVectorsForwardIndex.java:192-213), forward-index lookup by the LAST
+    term (global key order) whose first element matches (:107-120)."""
+    import math
+    recs = ix.terms()
+    recs_sorted = sorted(recs, key=lambda r: [g.encode("utf-16-be", "surrogatepass") for g in r[0]])
+    by_first = {}
+    for r in recs_sorted:
+        if r[0] != (" ",):
+            by_first[r[0][0]] = r
+    scores = []  # [docno, score]
+    for t in terms:
+        r = by_first.get(t)
+        if r is None:
+            continue
+        df = r[2] if idf_mode == 0 else len(r[3])
+        idf = math.log10(ix.N // df)
+        for d, tf in r[3]:
+            hit = [s for s in scores if s[0] == d]
+            w = (1.0 + math.log(tf)) * idf
+            if hit:
+                hit[0][1] += w
+            else:
+                scores.append([d, 0.0 + w])
+    scores.sort(key=lambda s: (-s[1], s[0]))
+    return [s[0] for s in scores[:k]], [s[1] for s in scores[:k]]
+
+
+@pytest.mark.parametrize("K", [1, 2])
+def test_oracle_query_tables_vs_scan(K):
+    """The oracle's hashed forward-index lookup and docno accumulator equal the
+    O(V) scan and the list-indexOf accumulator they replace."""
+    import common
+    import random
+    corpus, ids = common.fuzz_corpus(40 + K, 80)
+    ix = O.OracleIndex(corpus, O.write_mapping(ids), K, 1)
+    assert ix.lookup_selfcheck() == 0
+    firsts = sorted({g[0] for g, _, _, _ in ix.terms() if g != (" ",)})
+    rng = random.Random(K)
+    for _ in range(40):
+        tl = [rng.choice(firsts) for _ in range(rng.randint(1, 4))] + ["zz-absent"]
+        for mode in (0, 1):
+            d, s = ix.query(tl, 10, mode, 0)
+            pd, ps = _py_rank(ix, tl, 10, mode)
+            assert d == pd and s == ps, (tl, mode)
