@@ -82,6 +82,17 @@ int sme_load_docno_mapping(sme_ctx *ctx, const uint8_t *mapping_file, size_t n);
  * until its next call. */
 int sme_number_documents(sme_ctx *ctx, const uint8_t *corpus, size_t nbytes, const uint8_t **mapping, size_t *n);
 
+/* Doc-shard cut points for `world` shards: cuts[0] = 0, cuts[world] =
+ * nbytes, and cuts[g] = the first record start at or after nbytes * g / world,
+ * i.e. shard g holds the records a Hadoop split [n g/W, n (g+1)/W) owns
+ * (XMLInputFormat.java:110-143,173-198: a record belongs to the split its <DOC>
+ * match begins in), found by one record-reader pass over the whole input so a
+ * shard built from [cuts[g], cuts[g+1]) has exactly the single reader's records.
+ * cuts: world + 1 host entries. */
+int sme_split_points(sme_ctx *ctx, const uint8_t *corpus, size_t nbytes, int world, uint64_t *cuts);
+int sme_split_points_device(sme_ctx *ctx, const void *d_corpus, size_t nbytes, int world, void *stream,
+                            uint64_t *cuts);
+
 /* Build from a host corpus (TREC <DOC>..</DOC> records, one split). Copies to HBM. */
 int sme_build_index(sme_ctx *ctx, const uint8_t *corpus, size_t nbytes, sme_index **out);
 

@@ -19,7 +19,7 @@ import struct
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsme.so")
+LIB_PATH = os.environ.get("SME_LIB_PATH") or os.path.join(_HERE, "libsme.so")
 
 SME_IDF_REFERENCE = 0
 SME_IDF_TRUE_DF = 1
@@ -44,6 +44,7 @@ EXPORTS = [
     "sme_index_device_arrays", "sme_index_term", "sme_tokenize", "sme_lookup_terms", "sme_query_topk",
     "sme_query_topk_device", "sme_last_build_profile", "sme_index_reweight", "sme_number_documents",
     "sme_build_chargram", "sme_build_chargram_device", "sme_chargram_partition_text", "sme_chargram_stats",
+    "sme_split_points", "sme_split_points_device",
 ]
 
 
@@ -84,6 +85,8 @@ def lib():
     L.sme_chargram_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.sme_synth_corpus.argtypes = [C.c_int, C.c_char_p, vp, C.c_int64, vp, C.c_int64, C.c_int64, C.c_uint64, C.c_int,
                                    C.c_int, C.POINTER(vp), C.POINTER(sz)]
+    L.sme_split_points.argtypes = [vp, C.c_char_p, sz, C.c_int, C.POINTER(C.c_uint64)]
+    L.sme_split_points_device.argtypes = [vp, vp, sz, C.c_int, vp, C.POINTER(C.c_uint64)]
     L.sme_synth_free.argtypes = [vp]
     L.sme_synth_free.restype = None
     _lib = L

@@ -225,6 +225,27 @@ int sme_number_documents(sme_ctx *cx, const uint8_t *corpus, size_t nbytes, cons
   });
 }
 
+int sme_split_points(sme_ctx *cx, const uint8_t *corpus, size_t nbytes, int world, uint64_t *cuts) {
+  return guard([&] {
+    if (!cx || !cuts || world < 1 || (!corpus && nbytes)) throw sme::Error(SME_EINVAL, "bad argument");
+    set_device(cx);
+    hipStream_t st = cx->own_stream;
+    sme::DevBuf buf;
+    uint8_t *d = buf.as<uint8_t>(nbytes + 16);
+    if (nbytes) SME_HIP(hipMemcpyAsync(d, corpus, nbytes, hipMemcpyHostToDevice, st));
+    sme::split_points(cx, d, nbytes, world, cuts, st);
+  });
+}
+
+int sme_split_points_device(sme_ctx *cx, const void *d_corpus, size_t nbytes, int world, void *stream,
+                            uint64_t *cuts) {
+  return guard([&] {
+    if (!cx || !cuts || world < 1 || (!d_corpus && nbytes)) throw sme::Error(SME_EINVAL, "bad argument");
+    set_device(cx);
+    sme::split_points(cx, (const uint8_t *)d_corpus, nbytes, world, cuts, stream_of(cx, stream));
+  });
+}
+
 int sme_build_index_device(sme_ctx *cx, const void *d_corpus, size_t nbytes, void *stream, sme_index **out) {
   return guard([&] {
     if (!cx || !out || (!d_corpus && nbytes)) throw sme::Error(SME_EINVAL, "null argument");

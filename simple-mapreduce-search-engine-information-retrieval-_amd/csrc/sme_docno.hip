@@ -244,3 +244,38 @@ void number_documents(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st,
 }
 
 }  // namespace sme
+
+namespace sme {
+// cuts[g] = the first record start (XMLRecordReader match position of "<DOC>")
+// at or after n * g / world, n if none: the records a Hadoop split
+// [n g / W, n (g+1) / W) owns (XMLInputFormat.java:173-198, a record belongs to
+// the split its start tag's match begins in), taken from ONE reader pass over
+// the whole input so that a shard reader started at a cut sees exactly the
+// records the single reader does (no "<<DOC>" or nested "<DOC>" cut).
+__global__ void k_split_cuts(const uint64_t *rs, int64_t nR, uint64_t n, int world, uint64_t *cuts) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g > world) return;
+  if (g == 0 || g == world) {
+    cuts[g] = g == 0 ? 0 : n;
+    return;
+  }
+  const uint64_t target = n / (uint64_t)world * (uint64_t)g + n % (uint64_t)world * (uint64_t)g / (uint64_t)world;
+  int64_t lo = 0, hi = nR;  // first rs >= target
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (rs[m] < target) lo = m + 1;
+    else hi = m;
+  }
+  cuts[g] = lo < nR ? rs[lo] : n;
+}
+
+void split_points(sme_ctx *cx, const uint8_t *d_text, uint64_t n, int world, uint64_t *h_cuts, hipStream_t st) {
+  const RecordSpans rsp = find_records(cx, d_text, n, st, nullptr);
+  DevBuf out;
+  uint64_t *d = out.as<uint64_t>((size_t)world + 1);
+  hipLaunchKernelGGL(k_split_cuts, dim3((world + 64) / 64), dim3(64), 0, st, rsp.rs, rsp.nR, n, world, d);
+  SME_CHECK_LAUNCH();
+  SME_HIP(hipMemcpyAsync(h_cuts, d, ((size_t)world + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  SME_HIP(hipStreamSynchronize(st));
+}
+}  // namespace sme

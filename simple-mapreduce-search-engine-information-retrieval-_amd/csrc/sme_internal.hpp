@@ -124,6 +124,7 @@ struct RecordSpans {
 };
 void build_docid_hash(sme_ctx *cx, bool distinct, hipStream_t st);
 RecordSpans find_records(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, Prof *prof);
+void split_points(sme_ctx *cx, const uint8_t *d_text, uint64_t n, int world, uint64_t *h_cuts, hipStream_t st);
 void number_documents(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, std::vector<uint8_t> &out);
 sme_index *build_index(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream_t st, int job = 0);
 // CharKGramTermIndexer stage over the file-order term stream (sme_chargram.hip)

@@ -274,6 +274,7 @@ constexpr int kWTile = 1 << kWBits;
 constexpr int kDPL = kWTile / 64;   // documents per lane in a tile (16 at 1024)
 constexpr int kIMaxTerms = 64;      // lane j holds query term j
 constexpr int kWLut = 256;          // 1 + ln(tf) for tf < 256 from LDS
+constexpr int kTfRows = 4;          // LDS tf rows per tile (terms beyond: dense row bytes / binary search)
 static_assert(kDPL % 16 == 0 && kDPL <= 32, "tile must be 1024 or 2048 documents");
 
 __device__ __forceinline__ uint32_t impact(double l, double widf, double alpha) {
@@ -495,6 +496,10 @@ __global__ __launch_bounds__(64) void k_query_imp(
   __shared__ double bs[C];
   __shared__ int32_t bd[C];
   __shared__ double s_lut[kWLut];
+  // tf bytes of the tile for the first kTfRows query terms with postings in it
+  // (lane-major like the dense rows), read when candidates are scored exactly
+  __shared__ uint8_t trow[kTfRows * kWTile];
+  __shared__ uint32_t s_big;  // slots whose term has a tf > 255 in the tile
   const int lane = threadIdx.x;
   for (int j = lane; j < kWLut; j += 64) s_lut[j] = (j >= 1 && j <= max_tf) ? lut[j] : 0.0;
   const double wmax = __longlong_as_double((long long)*wmax_bits);
@@ -534,7 +539,7 @@ __global__ __launch_bounds__(64) void k_query_imp(
     }
     const bool isd = mdr >= 0;
     const uint64_t dmask = (uint64_t)__ballot(isd);
-    const uint8_t *mq = dq + (isd ? mdr * dstride : 0), *mt = dtf + (isd ? mdr * dstride : 0);
+    const int64_t mro = isd ? mdr * dstride : 0;  // this lane's dense row offset (impact / tf rows)
     int cnt = 0;  // buffer fill (wave-uniform)
     uint32_t st_tiles = 0, st_gated = 0, st_cand = 0, st_comp = 0, st_sparse = 0;  // SME_QSTATS
     bool th_ok = false;
@@ -584,6 +589,10 @@ __global__ __launch_bounds__(64) void k_query_imp(
       const int64_t tbyte = (int64_t)tile << kWBits;
       const uint64_t amask = (uint64_t)__ballot(lane < nt && me > mc);  // terms with postings in the tile
       const uint64_t dm = amask & dmask, sm = amask & ~dmask;
+      uint64_t rmask = amask;  // the first kTfRows terms of amask own an LDS tf row (slot = rank in amask)
+#pragma unroll
+      for (int x = 0; x < kTfRows; x++) rmask &= rmask - 1;
+      rmask = amask & ~rmask;
       const int64_t plo = mb + mc, phi = mb + me;  // this lane's term: postings in the tile
       uint32_t a[kDPL / 2];
       st_tiles++;
@@ -596,7 +605,7 @@ __global__ __launch_bounds__(64) void k_query_imp(
           if (dmr) {
             const int j = (int)__builtin_ctzll(dmr);
             dmr &= dmr - 1;
-            const uint8_t *pj = reinterpret_cast<const uint8_t *>(rl64((int64_t)mq, j)) + tbyte + kDPL * lane;
+            const uint8_t *pj = dq + rl64(mro, j) + tbyte + kDPL * lane;
 #pragma unroll
             for (int c = 0; c < kDPL / 16; c++) v[g][c] = *reinterpret_cast<const uint4 *>(pj + 16 * c);
           } else {
@@ -625,6 +634,15 @@ __global__ __launch_bounds__(64) void k_query_imp(
         // posting terms: impacts added into LDS (order-free integer sums)
 #pragma unroll
         for (int m = 0; m < kDPL / 2; m++) lacc[m * 64 + lane] = 0;
+        {
+          int sl = 0;
+          for (uint64_t m = rmask; m; m &= m - 1, sl++)
+            if ((sm >> __builtin_ctzll(m)) & 1)
+#pragma unroll
+              for (int c = 0; c < kDPL / 16; c++)
+                *reinterpret_cast<uint4 *>(trow + (sl << kWBits) + kDPL * lane + 16 * c) = make_uint4(0, 0, 0, 0);
+        }
+        if (lane == 0) s_big = 0;
         __syncthreads();
         // the tile's postings of all posting terms as one list, 256 per step:
         // entry x belongs to the last term j of sm with pre_j <= x
@@ -632,30 +650,45 @@ __global__ __launch_bounds__(64) void k_query_imp(
         const int32_t incl = wave_incl_sum(cj), prej = incl - cj;
         const int32_t total = __shfl(incl, 63, 64);
         for (int32_t x0 = 0; x0 < total; x0 += 256) {
-          int32_t dv[4], fv[4];
+          const int nu = min(4, (total - x0 + 63) >> 6);  // 64-entry chunks in this step (wave-uniform)
+          int32_t dv[4], fv[4], sv[4];
           double wv[4];
 #pragma unroll
           for (int u = 0; u < 4; u++) {
-            const int32_t x = x0 + 64 * u + lane;
-            int64_t pb = 0;
-            double wj = 0.0;
-            for (uint64_t m = sm; m; m &= m - 1) {
-              const int j = (int)__builtin_ctzll(m);
-              const int32_t pj = __builtin_amdgcn_readlane(prej, j);
-              if (x >= pj) {
-                pb = rl64(plo, j) - pj;
-                wj = rld(midf, j);
+            dv[u] = 0;
+            fv[u] = 0;
+            wv[u] = 0.0;
+            sv[u] = kTfRows;
+            if (u < nu) {
+              const int32_t x = x0 + 64 * u + lane;
+              int64_t pb = 0;
+              double wj = 0.0;
+              int sj = kTfRows;
+              for (uint64_t m = sm; m; m &= m - 1) {
+                const int j = (int)__builtin_ctzll(m);
+                const int32_t pj = __builtin_amdgcn_readlane(prej, j);
+                if (x >= pj) {
+                  pb = rl64(plo, j) - pj;
+                  wj = rld(midf, j);
+                  sj = ((rmask >> j) & 1) ? __popcll(amask & ((1ull << j) - 1)) : kTfRows;
+                }
               }
+              if (x < total) {
+                dv[u] = docno[pb + x];
+                fv[u] = tf[pb + x];
+              }
+              wv[u] = wj;
+              sv[u] = sj;
             }
-            const bool v = x < total;
-            dv[u] = v ? docno[pb + x] : 0;
-            fv[u] = v ? tf[pb + x] : 0;
-            wv[u] = wj;
           }
 #pragma unroll
           for (int u = 0; u < 4; u++) {
             if (fv[u] == 0) continue;
             const int r = (int)((int64_t)dv[u] - dbase);
+            if (sv[u] < kTfRows) {
+              trow[(sv[u] << kWBits) + kDPL * (r & 63) + (r >> 6)] = (uint8_t)(fv[u] > 255 ? 0 : fv[u]);
+              if (fv[u] > 255) atomicOr(&s_big, 1u << sv[u]);
+            }
             const double l = fv[u] < kWLut ? s_lut[fv[u]] : lut[fv[u]];
             atomicAdd(&lacc[((r >> 7) << 6) | (r & 63)], impact(l, wv[u], alpha_s) << (((r >> 6) & 1) << 4));
           }
@@ -685,6 +718,21 @@ __global__ __launch_bounds__(64) void k_query_imp(
           if (((a[b >> 1] >> ((b & 1) << 4)) & 0xFFFFu) >= gate) cm |= 1u << b;
         st_gated++;
         if (stats) st_cand += (uint32_t)__popc(cm);
+        // dense terms that own a tf row: copy the tile's tf bytes
+        {
+          int sl = 0;
+          for (uint64_t m = rmask; m; m &= m - 1, sl++) {
+            const int j = (int)__builtin_ctzll(m);
+            if (!((dmask >> j) & 1)) continue;
+            const uint8_t *pj = dtf + rl64(mro, j) + tbyte + kDPL * lane;
+#pragma unroll
+            for (int c = 0; c < kDPL / 16; c++)
+              *reinterpret_cast<uint4 *>(trow + (sl << kWBits) + kDPL * lane + 16 * c) =
+                  *reinterpret_cast<const uint4 *>(pj + 16 * c);
+          }
+        }
+        __syncthreads();
+        const uint32_t bigs = sm ? s_big : 0u;
         for (;;) {
           const bool have = cm != 0;
           if (__ballot(have) == 0) break;  // wave-uniform
@@ -696,11 +744,14 @@ __global__ __launch_bounds__(64) void k_query_imp(
             cm &= cm - 1;
             d = (int32_t)(dbase + ((b << 6) | lane));
             // exact score: query-token order, fp64, as rank() accumulates it
-            for (uint64_t m = amask; m; m &= m - 1) {
+            int sl = 0;
+            for (uint64_t m = amask; m; m &= m - 1, sl++) {
               const int j = (int)__builtin_ctzll(m);
               int f = 0;
-              if ((dmask >> j) & 1) {
-                f = reinterpret_cast<const uint8_t *>(rl64((int64_t)mt, j))[tbyte + kDPL * lane + b];
+              if (sl < kTfRows && !((bigs >> sl) & 1)) {
+                f = trow[(sl << kWBits) + kDPL * lane + b];
+              } else if ((dmask >> j) & 1) {
+                f = dtf[rl64(mro, j) + tbyte + kDPL * lane + b];
               } else {
                 int64_t lo = rl64(plo, j);
                 const int64_t e = rl64(phi, j);
@@ -831,7 +882,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           // largest weight of the batch (impact scale) and the dense-row terms
           // (SME_QDENSE=div, 0 = posting path only; tests run several)
           const char *ed = getenv("SME_QDENSE");
-          const int64_t ddiv = ed ? atoll(ed) : 16;
+          const int64_t ddiv = ed ? atoll(ed) : 32;
           const int64_t span = ix->dmax - ix->dmin + 1, stride = T << kWBits;
           int32_t *flag = W[53].as<int32_t>(nrows + 1), *dscan = W[54].as<int32_t>(nrows + 1);
           const unsigned gR = (unsigned)std::min<int64_t>((nrows + 256) / 256, 8192);

@@ -7,7 +7,8 @@ postings start with (0,0), TermKGramDocIndexer.java:84-90,126).  The exchanges a
 the small global statistics and the query results:
 
   split_points     Hadoop split ownership (XMLInputFormat.java:110-143): a record
-                   belongs to the split its <DOC> start tag begins in
+                   belongs to the split its <DOC> start tag begins in; cuts are
+                   record starts of one device reader pass (sme_split_points)
   global_count     N = sum of per-shard record counts        (all_reduce, 8 B)
   global_vocab     term strings of every shard -> global ids in TermDF.compareTo
                    order (all_gather of UTF-16BE bytes, local sort)
@@ -26,14 +27,41 @@ import torch
 import torch.distributed as dist
 
 
-def split_points(corpus, world):
-    """Byte offsets [0, s1, ..., n]: shard g = records whose '<DOC>' starts in
-    [n*g/world, n*(g+1)/world), realigned to the first '<DOC>' at or after each cut."""
-    n = len(corpus)
+def split_points(corpus, world, ctx=None):
+    """Byte offsets [0, s1, ..., n] of `world` doc shards (sme_split_points):
+    shard g = the records whose <DOC> match begins in [n*g/world, n*(g+1)/world)
+    (Hadoop split ownership, XMLInputFormat.java:110-143,173-198), with the record
+    starts taken from ONE record-reader pass on the device, so a shard never starts
+    inside '<<DOC>' or at a nested <DOC>.  `corpus` is host bytes, or a
+    sme.DeviceCorpus / (device pointer, nbytes) pair."""
+    import ctypes as C
+    import importlib
+    sme = importlib.import_module(__package__)
+    own = ctx is None
+    ctx = ctx or sme.Context()
+    try:
+        cuts = (C.c_uint64 * (world + 1))()
+        L = sme.lib()
+        if isinstance(corpus, (bytes, bytearray)):
+            rc = L.sme_split_points(ctx._h, bytes(corpus), len(corpus), world, cuts)
+        else:
+            ptr, n = (corpus.ptr, corpus.nbytes) if hasattr(corpus, "ptr") else corpus
+            rc = L.sme_split_points_device(ctx._h, C.c_void_p(ptr), n, world, None, cuts)
+        sme._check(rc)
+        return [int(c) for c in cuts]
+    finally:
+        if own:
+            ctx.close()
+
+
+def cuts_from_starts(starts, n, world):
+    """The same cut rule over a known list of record start offsets (sorted):
+    cuts[g] = first start >= n*g//world, else n."""
+    import bisect
     cuts = [0]
     for g in range(1, world):
-        c = corpus.find(b"<DOC>", n * g // world)
-        cuts.append(n if c < 0 else max(c, cuts[-1]))
+        i = bisect.bisect_left(starts, n * g // world)
+        cuts.append(starts[i] if i < len(starts) else n)
     cuts.append(n)
     return cuts
 

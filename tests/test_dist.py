@@ -58,7 +58,7 @@ def _worker(rank, world, port, idf_mode, out_dir):
         n = 90
         corpus = synth.gen_corpus(n, V=700, seed=5, len_lo=20, len_hi=70)
         mapping = synth.mapping_bytes(n)
-        cuts = D.split_points(corpus, world)
+        cuts = D.cuts_from_starts([o for o, _ in O.split_records(corpus)], len(corpus), world)
         shard = corpus[cuts[rank]:cuts[rank + 1]]
         ix = O.OracleIndex(shard, mapping, 1, 1)
         terms = [t for t in ix.terms() if t[0] != (" ",)]
@@ -99,12 +99,20 @@ def test_two_shards_gloo(tmp_path, idf_mode):
     assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
 
 
-def test_split_points_own_every_record():
+def test_cuts_own_every_record_and_quirks():
+    """The cut rule over one reader pass: every record in exactly one shard, and
+    no shard starts at a '<<DOC>' or a nested <DOC> (XMLInputFormat.java:173-198)."""
+    import common
     D = importlib.import_module(PKG + ".dist")
     synth = importlib.import_module(PKG + ".synth")
-    corpus = synth.gen_corpus(50, V=300, seed=2, len_lo=5, len_hi=40)
-    for w in (1, 2, 3, 8):
-        cuts = D.split_points(corpus, w)
-        assert cuts[0] == 0 and cuts[-1] == len(corpus) and cuts == sorted(cuts)
-        recs = sum(len(O.split_records(corpus[a:b])) for a, b in zip(cuts, cuts[1:]))
-        assert recs == 50
+    for corpus in (synth.gen_corpus(50, V=300, seed=2, len_lo=5, len_hi=40), common.fuzz_corpus(9, 60)[0],
+                   b"<DOC> a <DOC> b </DOC> <<DOC> c </DOC> <DOC> d </DOC>" * 7):
+        recs = O.split_records(corpus)
+        starts = [o for o, _ in recs]
+        for w in (1, 2, 3, 8, 13):
+            cuts = D.cuts_from_starts(starts, len(corpus), w)
+            assert cuts[0] == 0 and cuts[-1] == len(corpus) and cuts == sorted(cuts)
+            got = []
+            for a, b in zip(cuts, cuts[1:]):
+                got += [(a + o, ln) for o, ln in O.split_records(corpus[a:b])]
+            assert got == recs, w
