@@ -98,6 +98,19 @@ def _check(rc):
         raise SmeError(rc, lib().sme_last_error().decode("utf-8", "replace"))
 
 
+def _hip():
+    h = C.CDLL("libamdhip64.so")
+    h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    return h
+
+
+def _d2h(arr, dptr, nbytes):
+    """hipMemcpy device -> host into a numpy array."""
+    rc = _hip().hipMemcpy(arr.ctypes.data, C.c_void_p(dptr), nbytes, 2)
+    if rc != 0:
+        raise SmeError(-2, "hipMemcpy failed: %d" % rc)
+
+
 def _mutf8_decode(b):
     """DataInput.readUTF body -> str (surrogates kept)."""
     out, i = [], 0
@@ -236,6 +249,20 @@ class Index:
         _check(lib().sme_index_device_arrays(self._h, C.byref(o), C.byref(d), C.byref(w)))
         return o.value, d.value, w.value
 
+    def weights(self):
+        """Host copies of the query-side CSR and the TF-IDF weight pass's output:
+        (offsets[V+1], docno[P] docno-ascending per term, w[P] fp64)."""
+        o, d, w = self.device_arrays()
+        V, P = self.V, self.P
+        off = np.zeros(V + 1, np.int64)
+        dn = np.zeros(max(P, 1), np.int32)
+        ws = np.zeros(max(P, 1), np.float64)
+        _d2h(off, o, 8 * (V + 1))
+        if P:
+            _d2h(dn, d, 4 * P)
+            _d2h(ws, w, 8 * P)
+        return off, dn[:P], ws[:P]
+
     def term(self, t):
         p, n = C.c_void_p(), C.c_size_t()
         _check(lib().sme_index_term(self._h, t, C.byref(p), C.byref(n)))
@@ -290,13 +317,9 @@ class DeviceCorpus:
 
     def to_host(self):
         """Copy the corpus bytes back (hipMemcpy device -> host)."""
-        hip = C.CDLL("libamdhip64.so")
-        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-        out = (C.c_ubyte * max(self.nbytes, 1))()
-        rc = hip.hipMemcpy(out, C.c_void_p(self.ptr), self.nbytes, 2)  # hipMemcpyDeviceToHost
-        if rc != 0:
-            raise SmeError(-2, "hipMemcpy failed: %d" % rc)
-        return bytes(out)[:self.nbytes]
+        out = np.zeros(max(self.nbytes, 1), np.uint8)
+        _d2h(out, self.ptr, self.nbytes)
+        return out[:self.nbytes].tobytes()
 
     def close(self):
         if getattr(self, "ptr", None):

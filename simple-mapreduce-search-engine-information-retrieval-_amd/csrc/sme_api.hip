@@ -202,11 +202,15 @@ int sme_load_docno_mapping(sme_ctx *cx, const uint8_t *m, size_t n) {
     SME_HIP(hipStreamSynchronize(st));
     cx->map_n = (int64_t)off.size() - 1;
     cx->has_map = true;
-    // distinct docids (the file is sorted): the hash lookup equals binarySearch
+    // The docid hash equals Arrays.binarySearch only when the entries {"", docids...}
+    // are strictly ascending in String.compareTo (UTF-16 unit) order -- a sorted
+    // file of distinct docids, as writeDocnoData produces.  Any other file (unsorted,
+    // or with duplicates) keeps the device binary search, which then reproduces
+    // binarySearch's result on that array exactly.
     bool distinct = true;
     for (size_t i = 1; i + 1 < off.size() && distinct; i++)
-      distinct = !(off[i + 1] - off[i] == off[i] - off[i - 1] &&
-                   std::equal(chars.begin() + off[i - 1], chars.begin() + off[i], chars.begin() + off[i]));
+      distinct = std::lexicographical_compare(chars.begin() + off[i - 1], chars.begin() + off[i],
+                                              chars.begin() + off[i], chars.begin() + off[i + 1]);
     sme::build_docid_hash(cx, distinct, st);
   });
 }
@@ -449,6 +453,11 @@ int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offs
     set_device(ix->ctx);
     hipStream_t st = ix->ctx->own_stream;
     const int64_t nt = q_offsets[nq];
+    for (int q = 0; q < nq; q++)
+      if (q_offsets[q + 1] < q_offsets[q] || q_offsets[q] < 0) throw sme::Error(SME_EINVAL, "q_offsets not ascending");
+    for (int64_t i = 0; i < nt; i++)
+      if (term_ids[i] < -1 || term_ids[i] >= ix->V)
+        throw sme::Error(SME_EINVAL, "term id " + std::to_string(term_ids[i]) + " outside [-1, V)");
     sme::DevBuf a, b, c, d;
     int32_t *dt = a.as<int32_t>(nt + 1);
     int64_t *dq = b.as<int64_t>(nq + 1);

@@ -379,3 +379,90 @@ def test_chargram_empty(sme):
     assert (out.ngrams, out.npairs) == (0, 0) and out.partition_text(2) == b""
     out = ctx.build_chargram(b"<DOC><DOCNO>A</DOCNO> the of </DOC>")  # stopwords only
     assert out.ngrams == 0
+
+
+def _expected_weights(ix, idf_mode, N=None, df_override=None):
+    """(1 + ln tf) * log10(N // df) per posting (IntDocVectorsForwardIndex.java:211,
+    T2 int division), docno-ascending per term, from the reduce-order CSR."""
+    import math
+    off, dn, tf, df = ix.csr()
+    N = ix.N if N is None else N
+    exp = []
+    for t in range(ix.V):
+        d = 1 if idf_mode == 0 else int(df[t] if df_override is None else df_override[t])
+        idf = math.log10(float(N // d))
+        ps = sorted(zip(dn[off[t]:off[t + 1]].tolist(), tf[off[t]:off[t + 1]].tolist()))
+        exp += [(1.0 + math.log(float(f))) * idf for _, f in ps]
+    return np.array(exp, np.float64)
+
+
+@pytest.mark.parametrize("idf_mode", [0, 1])
+def test_weight_pass_and_reweight(sme, synth, idf_mode):
+    """The build's fused TF-IDF pass (k_weights) and sme_index_reweight with
+    all-reduced statistics: every fp64 weight bit-equal to the reference formula."""
+    import ctypes as C
+    n = 600
+    c = synth.gen_corpus(n, V=800, seed=17, len_lo=20, len_hi=90)
+    ctx = sme.Context(1, 1, idf_mode)
+    ctx.load_docno_mapping(synth.mapping_bytes(n))
+    ix = ctx.build(c)
+    off, dn, w = ix.weights()
+    assert np.array_equal(off, ix.csr()[0])
+    assert np.array_equal(w, _expected_weights(ix, idf_mode))
+    # reweight with a larger global N and per-term df + 3 (as after a df all-reduce)
+    df = ix.csr()[3].astype(np.int64) + 3
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    hip.hipFree.argtypes = [C.c_void_p]
+    d_df = C.c_void_p()
+    assert hip.hipMalloc(C.byref(d_df), df.nbytes) == 0
+    try:
+        assert hip.hipMemcpy(d_df, df.ctypes.data, df.nbytes, 1) == 0
+        ix.reweight(7 * n, d_df.value)
+        _, _, w2 = ix.weights()
+        assert np.array_equal(w2, _expected_weights(ix, idf_mode, N=7 * n, df_override=df))
+    finally:
+        hip.hipFree(d_df)
+
+
+def test_query_term_id_bounds(sme, synth):
+    """ids outside [-1, V) are rejected by the host entry point."""
+    n = 50
+    c = synth.gen_corpus(n, V=200, seed=3, len_lo=5, len_hi=30)
+    ctx = sme.Context(1, 1)
+    ctx.load_docno_mapping(synth.mapping_bytes(n))
+    ix = ctx.build(c)
+    for bad in (ix.V, ix.V + 5, -2):
+        with pytest.raises(sme.SmeError):
+            ix.query_topk(np.array([0, bad], np.int32), np.array([0, 2], np.int64), 10)
+    dn, _ = ix.query_topk(np.array([0, -1], np.int32), np.array([0, 2], np.int64), 10)
+    assert dn[0, 0] >= 0
+
+
+def test_unsorted_mapping_file(sme, synth):
+    """A mapping file that is not sorted (or repeats a docid): docno lookup falls
+    back to binary search over the file's array, as Arrays.binarySearch does."""
+    n = 40
+    c = synth.gen_corpus(n, V=200, seed=4, len_lo=5, len_hi=30)
+    ids = synth.docids(n)
+    for m in (ids[::-1], ids[:20] + ids[10:], ids[5:] + ids[:5]):
+        _check_build(sme, c, m, R=1)
+
+
+@pytest.mark.parametrize("k", [50, 100, 448])
+def test_queries_large_k(sme, synth, k):
+    """top-k beyond the register lists: k = 50 / 100 / 448 (c5's top-100)."""
+    n = 3000
+    c = synth.gen_corpus(n, V=400, seed=23, len_lo=5, len_hi=40)
+    ix, ref = _check_build(sme, c, synth.docids(n), R=1)
+    _, _, _, df = ix.csr()
+    names = [ix.term(i) for i in range(ix.V)]
+    terms, qoff = synth.queries_by_df(df, 30, seed=9, qlen_lo=1, qlen_hi=6)
+    dn, sc = _query_both_kernels(ix, terms, qoff, k)
+    for q in range(len(qoff) - 1):
+        tl = [names[t] for t in terms[qoff[q]:qoff[q + 1]]]
+        rd, rs = ref.query(tl, k, 0, 0)
+        assert dn[q, :len(rd)].tolist() == rd, q
+        assert np.array_equal(sc[q, :len(rd)], np.array(rs)), q
+        assert (dn[q, len(rd):] == -1).all()
