@@ -1,20 +1,31 @@
-"""bench.py -- index build GB/s (+ top-10 QPS) on MI355X, BASELINE.json configs.
+"""bench.py -- index build GB/s (+ top-k QPS) on MI355X, BASELINE.json configs.
 
-Workload (N=1): configs[1] "Synthetic Zipfian corpus 1M docs x ~500 tokens, 1
-MI355X: index build + TF-IDF" (N=1e6, doc length U[400,600],
-V_w=2^20, Zipf s=1, seed 42).  One step = one full index build + TF-IDF weight
-pass over the HBM-resident corpus (sme_build_index_device): record split, docno
-lookup, tokenize/stop/stem, per-record tf aggregation, term sort, weights, and
-the reduce-order (tf desc, docno asc) postings.  The corpus is generated on the
-device before the timed region.  After the timed build steps, the c3 query batch
-(100k queries, 2-8 terms drawn by df, top-10) is timed the same way and reported
-in "query".
+Default workload (N=1): configs[1] "Synthetic Zipfian corpus 1M docs x ~500
+tokens, 1 MI355X: index build + TF-IDF" (N=1e6, doc length
+U[400,600], V_w=2^20, Zipf s=1, seed 42).  One step = one full index build +
+TF-IDF weight pass over the HBM-resident corpus (sme_build_index_device): record
+split, docno lookup, tokenize/stop/stem, per-record tf aggregation, term sort,
+weights, and the reduce-order (tf desc, docno asc) postings.  The corpus is
+generated on the device before the timed region.  After the timed build steps,
+the c3 query batch (100k queries, 2-8 terms drawn by df, top-10) is timed the
+same way and reported in "query".
 
-Multi-GPU (torchrun, one rank per GPU, RCCL): weak scaling -- every rank owns a
-contiguous shard of N docs (docids offset by rank), builds its local index, and
-the global document count is all-reduced in every step (reference-mode idf =
-log10(N_global)).  Queries are run on every shard and the per-shard top-k lists
-are all-gathered and merged.
+--config c5: MS MARCO-shaped c5 (8,841,823 passages, V_w=30,000, 40-72 tokens,
+seed 9, strong scaling: the passages are split over the ranks) + 1M-query top-100;
+--config c4shard: one GPU's shard of c4 (6.25M docs of ~280 tokens, V_w=2^22,
+seed 44, weak scaling).  These are profiling lines (profiles/), not the driver's.
+
+After the timed regions (untimed): full-size property checks of the built index
+(sum tf = tokens + docid tokens, V = distinct terms of the vocabulary + N, CSR
+offsets monotone, docnos ascending per term), a cross-kernel check of a query
+sample (tiled default == postings-only == streaming kernel, bit for bit), and the
+I9 serialization of the partition records as its own stage.
+
+Multi-GPU (torchrun, one rank per GPU, RCCL): every rank owns a contiguous shard
+of docs (docids offset by rank), builds its local index, and the global document
+count is all-reduced in every step (reference-mode idf = log10(N_global)).
+Queries are run on every shard and the per-shard top-k lists are all-gathered and
+merged.
 
 Prints ONE JSON line on rank 0.
 """
@@ -33,6 +44,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 PKG = "simple-mapreduce-search-engine-information-retrieval-_amd"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+CONFIGS = {
+    "c2": dict(docs=1_000_000, vocab=1 << 20, seed=42, lo=400, hi=600, queries=100_000, k=10, qseed=7,
+               scaling="weak", name="c2: %d docs/GPU x U[400,600] tokens, V_w=%d, Zipf s=1, K=1 index + TF-IDF; "
+                                    "c3: %d queries top-%d"),
+    "c5": dict(docs=8_841_823, vocab=30_000, seed=9, lo=40, hi=72, queries=1_000_000, k=100, qseed=9,
+               scaling="strong", name="c5: %d passages (split over the GPUs) x U[40,72] tokens, V_w=%d, Zipf s=1; "
+                                      "%d queries top-%d"),
+    "c4shard": dict(docs=6_250_000, vocab=1 << 22, seed=44, lo=200, hi=360, queries=100_000, k=10, qseed=7,
+                    scaling="weak", name="c4 shard: %d docs/GPU x U[200,360] tokens, V_w=%d, Zipf s=1; "
+                                         "%d queries top-%d"),
+}
 
 
 def parse():
@@ -40,12 +62,24 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--docs", type=int, default=1_000_000, help="docs per GPU")
-    p.add_argument("--vocab", type=int, default=1 << 20)
-    p.add_argument("--queries", type=int, default=100_000)
-    p.add_argument("--cpu-docs", type=int, default=8000, help="docs in the CPU-baseline sample (0 = skip)")
+    p.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    p.add_argument("--docs", type=int, default=None, help="docs per GPU (weak) / in total (strong)")
+    p.add_argument("--vocab", type=int, default=None)
+    p.add_argument("--queries", type=int, default=None)
+    p.add_argument("--no-checks", action="store_true", help="skip the untimed post-run checks")
+    p.add_argument("--cpu-docs", type=int, default=8000, help="docs in the ref-faithful CPU sample (0 = skip CPU)")
+    p.add_argument("--cpu-opt-docs", type=int, default=50000, help="docs in the cpu-opt CPU sample")
+    p.add_argument("--cpu-ref-queries", type=int, default=50, help="queries timed with the ref-faithful rank()")
+    p.add_argument("--cpu-opt-queries", type=int, default=20000, help="queries timed with the cpu-opt rank()")
     p.add_argument("--no-query", action="store_true")
-    return p.parse_args()
+    a = p.parse_args()
+    cfg = dict(CONFIGS[a.config])
+    for key in ("docs", "vocab", "queries"):
+        if getattr(a, key) is not None:
+            cfg[key] = getattr(a, key)
+    a.cfg = cfg
+    a.docs, a.vocab, a.queries = cfg["docs"], cfg["vocab"], cfg["queries"]
+    return a
 
 
 def main():
@@ -64,20 +98,26 @@ def main():
     L = sme.lib()
 
     # ---- corpus shard in HBM (untimed) ----
-    seed = 42
+    cfg = a.cfg
+    seed = cfg["seed"]
     blob, voff = synth.make_vocab(a.vocab, seed)
     cdf = synth.zipf_cdf(a.vocab, 1.0)
     L.sme_synth_corpus.argtypes = [C.c_int, C.c_char_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int64,
                                    C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
     L.sme_synth_free.argtypes = [C.c_void_p]
     d_corpus, nbytes = C.c_void_p(), C.c_size_t()
-    d0 = rank * a.docs
-    rc = L.sme_synth_corpus(local, blob, voff.ctypes.data, a.vocab, cdf.ctypes.data, a.docs, d0, seed, 400, 600,
-                            C.byref(d_corpus), C.byref(nbytes))
+    if cfg["scaling"] == "weak":
+        n_local, d0, n_total = a.docs, rank * a.docs, a.docs * world
+    else:  # strong: the configured document count is split over the ranks
+        n_local = a.docs // world + (1 if rank < a.docs % world else 0)
+        d0 = rank * (a.docs // world) + min(rank, a.docs % world)
+        n_total = a.docs
+    rc = L.sme_synth_corpus(local, blob, voff.ctypes.data, a.vocab, cdf.ctypes.data, n_local, d0, seed, cfg["lo"],
+                            cfg["hi"], C.byref(d_corpus), C.byref(nbytes))
     assert rc == 0, rc
     nbytes = nbytes.value
-    # every rank loads the global mapping (all world*docs docids), so docnos are global
-    mapping = synth.mapping_bytes(a.docs * world)
+    # every rank loads the global mapping (all docids), so docnos are global
+    mapping = synth.mapping_bytes(n_total)
     ctx = sme.Context(k=1, num_partitions=1, device=local)
     ctx.load_docno_mapping(mapping)
     stream = torch.cuda.current_stream().cuda_stream
@@ -143,7 +183,7 @@ def main():
         query = run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier)
 
     result = {
-        "metric": "index build GB/s of text (top-10 queries/sec in 'query')",
+        "metric": "index build GB/s of text (top-%d queries/sec in 'query')" % cfg["k"],
         "value": round(gbs, 4),
         "unit": "GB/s",
         "n_gpus": world,
@@ -151,13 +191,12 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(t_max * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": cfg["scaling"],
         "vs_baseline": None,
         "dtype": "u8 text / int32 postings / f64 weights",
-        "data": "synthetic (device-generated Zipfian TREC corpus, seed 42)",
-        "config": {"workload": "c2: %d docs/GPU x U[400,600] tokens, V_w=%d, Zipf s=1, K=1 index + TF-IDF"
-                               % (a.docs, a.vocab), "docs_per_gpu": a.docs, "text_bytes_per_gpu": nbytes,
-                   "N": N, "V": V, "P": P, "parallelism": "doc-sharded x%d" % world},
+        "data": "synthetic (device-generated Zipfian TREC corpus, seed %d)" % seed,
+        "config": {"workload": cfg["name"] % (a.docs, a.vocab, a.queries, cfg["k"]), "docs_this_gpu": n_local,
+                   "text_bytes_per_gpu": nbytes, "N": N, "V": V, "P": P, "parallelism": "doc-sharded x%d" % world},
         "roofline": {"bound": "hbm", "kernel": "k_tok_fast", "achieved": round(tok_gbs, 2) if tok_gbs else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(tok_gbs / HBM_PEAK_GBS, 5) if tok_gbs else None,
@@ -172,8 +211,11 @@ def main():
     }
     if query is not None:
         result["query"] = query
-    if rank == 0 and a.cpu_docs > 0:
-        result["cpu_baseline"] = cpu_baseline(synth, a.cpu_docs, a.vocab)
+    if not a.no_checks:
+        result["checks"] = post_checks(a, sme, synth, ix, n_local, d0, query, rank)
+        result["stage_ms"]["serialize_records_untimed"] = serialize_stage(ix)
+    if rank == 0 and a.cpu_docs > 0 and a.config == "c2":
+        result["cpu_baseline"] = cpu_baseline(synth, a)
     if rank == 0:
         print(json.dumps(result), flush=True)
     ix.close()
@@ -184,9 +226,9 @@ def main():
 
 
 def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
-    k = 10
+    k = a.cfg["k"]
     _, _, _, df = ix.csr()
-    terms, qoff = synth.queries_by_df(df, a.queries, seed=7)
+    terms, qoff = synth.queries_by_df(df, a.queries, seed=a.cfg["qseed"])
     if dist is not None:
         # queries are defined by term strings (rank 0's draw); every shard maps them to its own ids
         uniq = np.unique(terms)
@@ -258,10 +300,11 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     alg = 8 * int(df[uniq].sum()) + 4 * int(nt.sum()) + 12 * k * a.queries
     touched = 8 * int(df[tv].sum())
     t_k = (qk_ms * 1e-3) if qk_ms else dt
-    return {"metric": "top-10 queries/sec", "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
-            "terms_per_query": "U{2..8} drawn by df (seed 7)", "ms_per_batch": round(dt * 1e3, 3),
-            "prep_ms": qp_ms,
-            "prep_what": "per-batch skip table (distinct batch terms x 1024-doc tiles) + dense u8 tf rows of terms with df >= span/4, inside ms_per_batch",
+    return {"metric": "top-%d queries/sec" % k, "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
+            "terms_per_query": "U{2..8} drawn by df (seed %d)" % a.cfg["qseed"], "ms_per_batch": round(dt * 1e3, 3),
+            "prep_ms": qp_ms, "_terms": terms, "_qoff": qoff, "_out": (out_d, out_s),
+            "prep_what": "per batch, inside ms_per_batch: skip table (distinct batch terms x 1024-doc tiles), dense "
+                         "u8 tf + impact rows of terms with df >= span/32, heaviest-term query order",
             "roofline": {"bound": "hbm", "kernel": kname, "kernel_ms": qk_ms,
                          "achieved": round(alg / t_k / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(alg / t_k / 1e9 / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname, a),
@@ -269,6 +312,69 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
                                  "mean launch time (HIP events)"},
             "postings_touched_GBps": round(touched / t_k / 1e9, 2),
             "postings_touched_what": "8 B x postings of every query term (re-reads across queries included)"}
+
+
+def post_checks(a, sme, synth, ix, n_local, d0, query, rank):
+    """Untimed, size-independent checks of the full-size build and query batch."""
+    out = {}
+    off, dn, tf, df = ix.csr()
+    lens = synth.doc_lengths(d0, d0 + n_local, a.cfg["seed"], a.cfg["lo"], a.cfg["hi"])
+    # every synthetic token is one term, plus the docid token of <DOCNO> (T7)
+    out["sum_tf_eq_tokens"] = bool(int(tf.astype(np.int64).sum()) == int(lens.sum()) + n_local)
+    out["offsets_monotone"] = bool((np.diff(off) >= 1).all() and off[0] == 0 and off[-1] == ix.P)
+    # reduce order inside every term: tf desc, then docno asc
+    newt = np.zeros(max(ix.P, 1), bool)  # position p starts a term
+    newt[off[:-1][off[:-1] < ix.P]] = True
+    same = ~newt[1:ix.P]
+    out["reduce_order"] = bool((((tf[1:] <= tf[:-1]) | ~same).all()) and
+                               (((tf[1:] != tf[:-1]) | (dn[1:] > dn[:-1]) | ~same).all()))
+    del tf, dn
+    # query-side CSR: docnos strictly ascending per term
+    o2, dd, _ = ix.weights()
+    out["docno_order"] = bool(np.array_equal(o2, off) and ((dd[1:] > dd[:-1]) | ~same).all())
+    del dd, same, newt
+    if rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        blob, voff = synth.make_vocab(a.vocab, a.cfg["seed"])
+        nv = int(O.lib().or_count_distinct_terms(blob, voff.ctypes.data, a.vocab))
+        # every vocabulary word occurs at c2 sizes (rank 2^20 has ~34 expected occurrences)
+        out["V_eq_distinct_terms_plus_docids"] = bool(ix.V == nv + n_local) if a.config == "c2" else None
+        out["V_expected"] = nv + n_local
+    if query is not None:
+        terms, qoff = query.pop("_terms"), query.pop("_qoff")
+        out_d, out_s = query.pop("_out")
+        nq = min(2000, len(qoff) - 1)
+        t_s, q_s = terms[:qoff[nq]], qoff[:nq + 1]
+        k = a.cfg["k"]
+        base = (out_d[:nq].cpu().numpy(), out_s[:nq].cpu().numpy()) if hasattr(out_d, "cpu") else None
+        d1, s1 = ix.query_topk(t_s, q_s, k)
+        ok = base is None or (np.array_equal(base[0], d1) and np.array_equal(base[1], s1))
+        for env in ({"SME_QDENSE": "0"}, {"SME_QUERY_KERNEL": "stream"}):
+            if "SME_QUERY_KERNEL" in env and k > 32:
+                continue
+            old = {n: os.environ.get(n) for n in env}
+            os.environ.update(env)
+            try:
+                d2, s2 = ix.query_topk(t_s, q_s, k)
+            finally:
+                for n, v in old.items():
+                    if v is None:
+                        del os.environ[n]
+                    else:
+                        os.environ[n] = v
+            ok = ok and np.array_equal(d1, d2) and np.array_equal(s1, s2)
+        out["query_sample_kernels_agree"] = bool(ok)
+        out["query_sample"] = nq
+    return out
+
+
+def serialize_stage(ix):
+    """I9: the partition records (device serializer + copy to the host), untimed."""
+    t0 = time.perf_counter()
+    n = sum(len(ix.partition_records(p)) for p in range(ix.ctx.num_partitions))
+    return {"ms": round((time.perf_counter() - t0) * 1e3, 2), "bytes": n,
+            "what": "sme_index_partition_records for every partition (device k_ser_* + D2H), after the timed steps"}
 
 
 def pmc_traffic(kernel, a):
@@ -286,19 +392,70 @@ def pmc_traffic(kernel, a):
     return None if k is None else k.get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(synth, n_docs, V):
-    """The oracle (ref-faithful CPU restatement, single thread) on a bounded sample of the same workload."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(synth, a):
+    """BASELINE.md section 2, on this box's host cores, bounded samples of the c2 / c3
+    distributions (the oracle is the checker and the timed CPU port; the tests hold
+    both modes to identical outputs):
+      ref-faithful  oracle_index.c, 1 thread: per-token emit, string-key merge sort,
+                    the reducer's list sorts; rank() with the reference's indexOf scan
+      cpu-opt       oracle_cpuopt.cc, OpenMP over documents / queries: hash
+                    aggregation, counting sorts, dense accumulators, partial-sort top-k
+    `value` is the cpu-opt build rate (the honest CPU comparison)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    corpus = synth.gen_corpus(n_docs, V=V, seed=42, len_lo=400, len_hi=600)
-    mapping = synth.mapping_bytes(n_docs)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    out = {"unit": "GB/s", "cores": threads, "kind": "port", "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
+    # ref-faithful build + rank() (indexOf scan) on a small sample
+    n_ref = a.cpu_docs
+    corpus = synth.gen_corpus(n_ref, V=a.vocab, seed=42, len_lo=400, len_hi=600)
+    mapping = synth.mapping_bytes(n_ref)
     t0 = time.perf_counter()
-    ix = O.OracleIndex(corpus, mapping, 1, 1)
-    dt = time.perf_counter() - t0
-    del ix
-    return {"value": round(len(corpus) / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": "%d docs (%d bytes) of the c2 distribution, ref-faithful oracle (per-token emit, "
-                      "string-key merge sort, reduce sorts), %.1f s" % (n_docs, len(corpus), dt)}
+    ref = O.OracleIndex(corpus, mapping, 1, 1)
+    dt_ref = time.perf_counter() - t0
+    # cpu-opt build of the same sample (threads), then a larger sample
+    cpu_small = O.CpuOptIndex(corpus, mapping, threads)
+    off, _, _, terms = cpu_small.csr()
+    df = np.diff(off).astype(np.int32)
+    tq, qo = synth.queries_by_df(df, a.cpu_ref_queries, seed=7)
+    O.lib().or_set_ref_scan(1)
+    t0 = time.perf_counter()
+    for q in range(len(qo) - 1):
+        ref.query([terms[t] for t in tq[qo[q]:qo[q + 1]]], 10, 0, 0)
+    dt_rq = time.perf_counter() - t0
+    O.lib().or_set_ref_scan(0)
+    del ref, cpu_small
+    out["ref_faithful"] = {
+        "build_GBps": round(len(corpus) / dt_ref / 1e9, 6), "cores": 1,
+        "build_sample": "%d docs (%d bytes) of c2, %.1f s" % (n_ref, len(corpus), dt_ref),
+        "query_qps": round(a.cpu_ref_queries / dt_rq, 2),
+        "query_sample": "%d c3-style top-10 queries over that %d-doc index (indexOf accumulator), %.1f s"
+                        % (a.cpu_ref_queries, n_ref, dt_rq)}
+    n_opt = a.cpu_opt_docs
+    corpus = synth.gen_corpus(n_opt, V=a.vocab, seed=42, len_lo=400, len_hi=600)
+    mapping = synth.mapping_bytes(n_opt)
+    t0 = time.perf_counter()
+    cpu = O.CpuOptIndex(corpus, mapping, threads)
+    dt_opt = time.perf_counter() - t0
+    off, _, _, _ = cpu.csr()
+    df = np.diff(off).astype(np.int32)
+    tq, qo = synth.queries_by_df(df, a.cpu_opt_queries, seed=7)
+    _, _, dt_q = cpu.query(tq, qo, 10, 0, threads)
+    out["value"] = round(len(corpus) / dt_opt / 1e9, 6)
+    out["sample"] = ("cpu-opt (%d threads): build of %d docs (%d bytes) of c2 in %.1f s; %d c3-style top-10 queries "
+                     "over that index in %.2f s" % (threads, n_opt, len(corpus), dt_opt, a.cpu_opt_queries, dt_q))
+    out["cpu_opt"] = {"build_GBps": out["value"], "query_qps": round(a.cpu_opt_queries / dt_q, 1),
+                      "query_index_docs": n_opt}
+    return out
 
 
 if __name__ == "__main__":

@@ -696,6 +696,12 @@ static int ds_cmp_first(const void *x, const void *y) {
  *        2 = score desc / first-encounter (stable exact ties).
  * Returns number of results written (<= k); scores/docnos out.
  */
+/* ref-faithful timing mode (bench.py cpu_baseline): the accumulator lookup is
+ * the reference's linear scores.indexOf scan (T6) instead of the docno table;
+ * both give the same entry, the scan is O(entries) per posting */
+static int g_ref_scan = 0;
+void or_set_ref_scan(int on) { g_ref_scan = on; }
+
 int or_query(const or_index *ix, const uint16_t *const *terms, const int *lens, int nterms, int k,
              int idf_mode, int order, int32_t *out_docno, double *out_score) {
   int cap = 1024, n = 0;
@@ -718,6 +724,14 @@ int or_query(const or_index *ix, const uint16_t *const *terms, const int *lens, 
       uint32_t h = ((uint32_t)d * 2654435761u) & (uint32_t)(hcap - 1);
       while (ht[h] >= 0 && sc[ht[h]].docId != d) h = (h + 1) & (uint32_t)(hcap - 1);
       int idx = ht[h];
+      if (g_ref_scan) { /* scores.indexOf: first entry with this docId */
+        idx = -1;
+        for (int s2 = 0; s2 < n; s2++)
+          if (sc[s2].docId == d) {
+            idx = s2;
+            break;
+          }
+      }
       if (idx < 0) {
         if (n == cap) {
           cap *= 2;
@@ -883,4 +897,38 @@ int or_lookup_selfcheck(const or_index *ix) {
     if (find_term(ix, g->p, g->n) != find_term_scan(ix, g->p, g->n)) bad++;
   }
   return bad;
+}
+
+/* number of distinct stems (processContent of each word alone) of n UTF-8 words
+ * blob[offs[i] .. offs[i+1]) -- bench.py's full-size vocabulary check */
+int64_t or_count_distinct_terms(const uint8_t *blob, const int64_t *offs, int64_t n) {
+  int64_t cap = 1024;
+  while (cap < 4 * n + 16) cap <<= 1;
+  uint64_t *tab = (uint64_t *)calloc((size_t)cap, sizeof(uint64_t));
+  jstr_list **keep = NULL;
+  (void)keep;
+  int64_t cnt = 0;
+  jstr w;
+  js_init(&w);
+  for (int64_t i = 0; i < n; i++) {
+    utf8_to_utf16(blob + offs[i], (size_t)(offs[i + 1] - offs[i]), &w);
+    jstr_list out;
+    jl_init(&out);
+    or_process_content(w.p, w.n, &out);
+    for (int t = 0; t < out.n; t++) {
+      uint64_t h = 1469598103934665603ull;
+      for (int c = 0; c < out.v[t].n; c++) h = (h ^ out.v[t].p[c]) * 1099511628211ull;
+      h |= 1; /* 0 = empty slot; 64-bit hashes of < 2^21 strings: collisions negligible */
+      int64_t s = (int64_t)(h & (uint64_t)(cap - 1));
+      while (tab[s] && tab[s] != h) s = (s + 1) & (cap - 1);
+      if (!tab[s]) {
+        tab[s] = h;
+        cnt++;
+      }
+    }
+    jl_free(&out);
+  }
+  js_free(&w);
+  free(tab);
+  return cnt;
 }

@@ -511,3 +511,4 @@ void or_process_content(const uint16_t *text, int n, jstr_list *out) {
   js_free(&st);
   jl_free(&toks);
 }
+const char *or_stopword(int i) { return STOP[i]; }

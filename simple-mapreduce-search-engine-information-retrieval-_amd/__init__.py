@@ -111,6 +111,13 @@ def _d2h(arr, dptr, nbytes):
         raise SmeError(-2, "hipMemcpy failed: %d" % rc)
 
 
+def _host_bytes(p, n):
+    """Copy n bytes at host address p (ctypes.string_at takes a C int size: < 2 GiB)."""
+    if not n:
+        return b""
+    return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_ubyte)), shape=(n,)).tobytes()
+
+
 def _mutf8_decode(b):
     """DataInput.readUTF body -> str (surrogates kept)."""
     out, i = [], 0
@@ -232,7 +239,7 @@ class Index:
     def partition_records(self, part):
         p, n = C.c_void_p(), C.c_size_t()
         _check(lib().sme_index_partition_records(self._h, part, C.byref(p), C.byref(n)))
-        return C.string_at(p, n.value) if n.value else b""
+        return _host_bytes(p, n.value)
 
     def csr(self):
         """(offsets[V+1], docno[P], tf[P], true_df[V]) in reduce-output order (tf desc, docno asc)."""
@@ -351,7 +358,7 @@ class CharGramOutput:
     def partition_text(self, part):
         p, n = C.c_void_p(), C.c_size_t()
         _check(lib().sme_chargram_partition_text(self._h, part, C.byref(p), C.byref(n)))
-        return C.string_at(p, n.value) if n.value else b""
+        return _host_bytes(p, n.value)
 
 
 # reference-shaped facades

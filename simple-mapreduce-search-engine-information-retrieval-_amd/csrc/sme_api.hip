@@ -489,7 +489,7 @@ int sme_last_build_profile(const sme_ctx *cx, const char **json) {
       os << (i ? "," : "") << "\"" << cx->last_profile[i].first << "\":" << cx->last_profile[i].second;
     if (cx->last_query_ms >= 0) os << (cx->last_profile.empty() ? "" : ",") << "\"query_kernel\":" << cx->last_query_ms;
     if (cx->last_query_ms >= 0) os << ",\"query_prep\":" << cx->last_query_prep_ms;
-    if (cx->last_query_ms >= 0) os << ",\"query_kernel_name\":\"" << (cx->last_query_tiled ? "k_query_wave" : "k_query") << "\"";
+    if (cx->last_query_ms >= 0) os << ",\"query_kernel_name\":\"" << (cx->last_query_tiled ? "k_query_imp" : "k_query") << "\"";
     os << "}";
     const_cast<sme_ctx *>(cx)->profile_json = os.str();
     *json = cx->profile_json.c_str();

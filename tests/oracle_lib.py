@@ -41,6 +41,9 @@ def lib():
                                     C.c_void_p, C.c_void_p]
         L.or_last_error.restype = C.c_char_p
         L.or_lookup_selfcheck.argtypes = [C.c_void_p]
+        L.or_set_ref_scan.argtypes = [C.c_int]
+        L.or_count_distinct_terms.restype = C.c_int64
+        L.or_count_distinct_terms.argtypes = [C.c_char_p, C.c_void_p, C.c_int64]
         L.or_split_records.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]
         L.or_chargram.restype = C.c_void_p
         L.or_chargram.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int]
@@ -218,3 +221,58 @@ def write_mapping(docids):
         b = d.encode("utf-8")
         out.append(struct.pack(">H", len(b)) + b)
     return b"".join(out)
+
+
+class CpuOptIndex:
+    """The cpu-opt baseline build (oracle/oracle_cpuopt.cc, OpenMP): K = 1, one split."""
+
+    def __init__(self, corpus, mapping, threads=0):
+        import numpy as np
+        L = lib()
+        L.or_cpuopt_build.restype = C.c_void_p
+        L.or_cpuopt_build.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_int]
+        L.or_cpuopt_free.argtypes = [C.c_void_p]
+        L.or_cpuopt_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_int64)] * 3 + [C.POINTER(C.c_double)]
+        L.or_cpuopt_csr.argtypes = [C.c_void_p] + [C.c_void_p] * 5
+        L.or_cpuopt_query.restype = C.c_double
+        L.or_cpuopt_query.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_void_p, C.c_void_p]
+        self._h = L.or_cpuopt_build(corpus, len(corpus), mapping, len(mapping), threads)
+        if not self._h:
+            raise RuntimeError("cpu-opt build rejected the corpus")
+        n, v, p, s = C.c_int64(), C.c_int64(), C.c_int64(), C.c_double()
+        L.or_cpuopt_stats(self._h, C.byref(n), C.byref(v), C.byref(p), C.byref(s))
+        self.N, self.V, self.P, self.build_s = n.value, v.value, p.value, s.value
+        self.threads = threads
+
+    def csr(self):
+        """(offsets, docno, tf) in reduce order and the term strings (TermDF order)."""
+        import numpy as np
+        off = np.zeros(self.V + 1, np.int64)
+        dn = np.zeros(max(self.P, 1), np.int32)
+        tf = np.zeros(max(self.P, 1), np.int32)
+        toff = np.zeros(self.V + 1, np.int64)
+        lib().or_cpuopt_csr(self._h, off.ctypes.data, dn.ctypes.data, tf.ctypes.data, toff.ctypes.data, None)
+        tch = np.zeros(max(int(toff[-1]), 1), np.uint16)
+        lib().or_cpuopt_csr(self._h, off.ctypes.data, dn.ctypes.data, tf.ctypes.data, toff.ctypes.data,
+                            tch.ctypes.data)
+        raw = tch.tobytes()
+        terms = [raw[2 * toff[i]:2 * toff[i + 1]].decode("utf-16-le", "surrogatepass") for i in range(self.V)]
+        return off, dn[:self.P], tf[:self.P], terms
+
+    def query(self, terms, qoff, k, idf_mode=0, threads=0):
+        """Batched rank(); returns (docno [nq, k], score [nq, k], seconds)."""
+        import numpy as np
+        terms = np.ascontiguousarray(terms, np.int32)
+        qoff = np.ascontiguousarray(qoff, np.int64)
+        nq = len(qoff) - 1
+        dn = np.zeros((max(nq, 1), k), np.int32)
+        sc = np.zeros((max(nq, 1), k), np.float64)
+        s = lib().or_cpuopt_query(self._h, terms.ctypes.data, qoff.ctypes.data, nq, k, idf_mode, threads,
+                                  dn.ctypes.data, sc.ctypes.data)
+        return dn[:nq], sc[:nq], s
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().or_cpuopt_free(self._h)
+            self._h = None
