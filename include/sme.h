@@ -170,6 +170,12 @@ int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offs
 int sme_query_topk_device(sme_index *ix, const int32_t *d_term_ids, const int64_t *d_q_offsets,
                           int nq, int k, int32_t *d_out_docno, double *d_out_score, void *stream);
 
+/* 128-bit fingerprint of every index term (two u64 per term into device memory
+ * d_out[2 V]): equal term strings (k-grams) on different shards get equal
+ * fingerprints, so a multi-GPU df exchange can key the all-reduce on them
+ * without gathering and sorting term strings (dist.py global_df). */
+int sme_index_term_fingerprints(sme_index *ix, uint64_t *d_out, void *stream);
+
 /* Recompute the fp64 TF-IDF weights of a doc-sharded index with global
  * statistics: n_global = records over all shards (all-reduced doc counter),
  * d_df_global = per local term the all-reduced df (device int64[V]) or NULL to

@@ -44,7 +44,7 @@ EXPORTS = [
     "sme_index_device_arrays", "sme_index_term", "sme_tokenize", "sme_lookup_terms", "sme_query_topk",
     "sme_query_topk_device", "sme_last_build_profile", "sme_index_reweight", "sme_number_documents",
     "sme_build_chargram", "sme_build_chargram_device", "sme_chargram_partition_text", "sme_chargram_stats",
-    "sme_split_points", "sme_split_points_device",
+    "sme_split_points", "sme_split_points_device", "sme_index_term_fingerprints",
 ]
 
 
@@ -85,6 +85,7 @@ def lib():
     L.sme_chargram_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.sme_synth_corpus.argtypes = [C.c_int, C.c_char_p, vp, C.c_int64, vp, C.c_int64, C.c_int64, C.c_uint64, C.c_int,
                                    C.c_int, C.POINTER(vp), C.POINTER(sz)]
+    L.sme_index_term_fingerprints.argtypes = [vp, vp, vp]
     L.sme_split_points.argtypes = [vp, C.c_char_p, sz, C.c_int, C.POINTER(C.c_uint64)]
     L.sme_split_points_device.argtypes = [vp, vp, sz, C.c_int, vp, C.POINTER(C.c_uint64)]
     L.sme_synth_free.argtypes = [vp]
@@ -255,6 +256,17 @@ class Index:
         o, d, w = C.c_void_p(), C.c_void_p(), C.c_void_p()
         _check(lib().sme_index_device_arrays(self._h, C.byref(o), C.byref(d), C.byref(w)))
         return o.value, d.value, w.value
+
+    def offsets(self):
+        """int64 offsets[V+1] of the postings per term (df = np.diff)."""
+        o, _, _ = self.device_arrays()
+        off = np.zeros(self.V + 1, np.int64)
+        _d2h(off, o, 8 * (self.V + 1))
+        return off
+
+    def term_fingerprints(self, d_out, stream=None):
+        """128-bit fingerprint per term into device memory d_out (uint64 [V, 2])."""
+        _check(lib().sme_index_term_fingerprints(self._h, C.c_void_p(d_out), C.c_void_p(stream or 0)))
 
     def weights(self):
         """Host copies of the query-side CSR and the TF-IDF weight pass's output:

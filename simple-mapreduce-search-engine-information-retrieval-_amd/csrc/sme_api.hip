@@ -472,6 +472,17 @@ int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offs
   });
 }
 
+int sme_index_term_fingerprints(sme_index *ix, uint64_t *d_out, void *stream) {
+  return guard([&] {
+    if (!ix || (!d_out && ix->V > 0)) throw sme::Error(SME_EINVAL, "null argument");
+    if (ix->job != 0) throw sme::Error(SME_EINVAL, "not a TermKGramDocIndexer index");
+    set_device(ix->ctx);
+    hipStream_t st = stream_of(ix->ctx, stream);
+    sme::term_fingerprints(ix, d_out, st);
+    SME_HIP(hipStreamSynchronize(st));
+  });
+}
+
 int sme_index_reweight(sme_index *ix, int64_t n_global, const int64_t *d_df_global, void *stream) {
   return guard([&] {
     if (!ix || n_global < 0) throw sme::Error(SME_EINVAL, "bad argument");

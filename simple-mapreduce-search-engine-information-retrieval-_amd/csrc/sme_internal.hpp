@@ -136,6 +136,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
                 int32_t *d_out_docno, double *d_out_score, hipStream_t st);
 void tokenize_string(sme_ctx *cx, const uint8_t *h_utf8, size_t n, std::vector<std::vector<uint16_t>> &out,
                      hipStream_t st);
+void term_fingerprints(sme_index *ix, uint64_t *d_out, hipStream_t st);
 void lookup_terms(sme_index *ix, const std::vector<std::vector<uint16_t>> &terms, int32_t *ids,
                   hipStream_t st);
 }  // namespace sme

@@ -1106,6 +1106,48 @@ __global__ void k_gram_last(const int32_t *gram, int64_t V, int K, int n, int32_
   }
 }
 
+// 128-bit fingerprints of every index term's string (K = 1) or k-gram (the
+// component terms' fingerprints chained): two independent 64-bit mixes of the
+// UTF-16 units, for the multi-GPU df exchange (dist.py: equal terms on two
+// shards get equal fingerprints without sorting strings on the host).
+__device__ __forceinline__ void fp_string(const uint16_t *c, int64_t n, uint64_t &a, uint64_t &b) {
+  a = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+  b = 0xC2B2AE3D27D4EB4Full + (uint64_t)n * 0x165667B19E3779F9ull;
+  for (int64_t i = 0; i < n; i++) {
+    a = fmix64(a ^ ((uint64_t)c[i] + 0x100));
+    b = (b ^ (uint64_t)c[i]) * 0x100000001B3ull + 0x9E3779B97F4A7C15ull;
+  }
+  b = fmix64(b);
+}
+__global__ void k_term_fp(const int64_t *toff, const uint16_t *tch, const int32_t *gram, int K, int64_t V,
+                          uint64_t *out) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t a = 0, b = 0;
+    if (K == 1) {
+      fp_string(tch + toff[t], toff[t + 1] - toff[t], a, b);
+    } else {
+      a = 0x243F6A8885A308D3ull;
+      b = 0x13198A2E03707344ull;
+      for (int g = 0; g < K; g++) {
+        const int32_t c = gram[t * K + g];
+        uint64_t x, y;
+        fp_string(tch + toff[c], toff[c + 1] - toff[c], x, y);
+        a = fmix64(a ^ x) + (uint64_t)g;
+        b = fmix64(b + y) ^ (uint64_t)g;
+      }
+    }
+    out[2 * t] = a;
+    out[2 * t + 1] = b;
+  }
+}
+void term_fingerprints(sme_index *ix, uint64_t *d_out, hipStream_t st) {
+  if (ix->V <= 0) return;
+  hipLaunchKernelGGL(k_term_fp, dim3((unsigned)std::min<int64_t>((ix->V + 255) / 256, 65536)), dim3(256), 0, st,
+                     (const int64_t *)ix->d_term_off.p, (const uint16_t *)ix->d_term_chars.p,
+                     ix->K > 1 ? (const int32_t *)ix->d_gram.p : nullptr, ix->K, ix->V, d_out);
+  SME_CHECK_LAUNCH();
+}
+
 void lookup_terms(sme_index *ix, const std::vector<std::vector<uint16_t>> &terms, int32_t *ids, hipStream_t st) {
   const int n = (int)terms.size();
   if (n == 0) return;

@@ -14,6 +14,8 @@ the small global statistics and the query results:
                    order (all_gather of UTF-16BE bytes, local sort)
   global_df        df per global term = sum of shard postings lengths (all_reduce);
                    returned per LOCAL term for sme_index_reweight
+  global_df_index  the same for a libsme shard, keyed by 128-bit device term
+                   fingerprints (all_gather + torch.unique, no host strings)
   merge_topk       per-shard top-k -> global top-k, (score desc, docno asc)
                    (all_gather of Q x k x (4 + 8) B)
 
@@ -128,6 +130,39 @@ def global_df(local_df, l2g, n_global_terms, group=None):
         g.index_add_(0, torch.from_numpy(l2g).to(dev), torch.from_numpy(np.asarray(local_df, np.int64)).to(dev))
     dist.all_reduce(g, group=group)
     return g[torch.from_numpy(l2g).to(dev)] if len(l2g) else g[:0]
+
+
+def global_df_index(ix, group=None):
+    """All-reduced df per LOCAL term of a libsme shard index, as a CUDA int64 tensor
+    ready for sme_index_reweight: shards agree on terms through their 128-bit device
+    fingerprints (sme_index_term_fingerprints), gathered and deduplicated with
+    torch.unique on the collective's device -- no term strings on the host."""
+    dev = _dev(group)
+    world = dist.get_world_size(group)
+    V = int(ix.V)
+    fp = torch.zeros((max(V, 1), 2), dtype=torch.int64, device="cuda")
+    if V:
+        ix.term_fingerprints(fp.data_ptr())
+    fp = fp[:V].to(dev)
+    n = torch.tensor([V], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    m = max(max(ns), 1)
+    pad = torch.zeros((m, 2), dtype=torch.int64, device=dev)
+    pad[:V] = fp
+    outs = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    allfp = torch.cat([o[:c] for o, c in zip(outs, ns)], 0)
+    uniq, inv = torch.unique(allfp, dim=0, return_inverse=True)
+    r = dist.get_rank(group)
+    mine = inv[sum(ns[:r]):sum(ns[:r]) + V]
+    df = torch.from_numpy(np.diff(ix.offsets())).to(dev)
+    g = torch.zeros(uniq.shape[0], dtype=torch.int64, device=dev)
+    if V:
+        g.index_add_(0, mine, df)
+    dist.all_reduce(g, group=group)
+    return g[mine].to("cuda").contiguous()
 
 
 def merge_topk(docno, score, k, group=None):

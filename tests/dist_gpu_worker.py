@@ -1,0 +1,68 @@
+"""One rank of the world-2 libsme shard test (tests/test_dist_gpu.py): a fresh
+process that touches the GPU only after it starts.  Builds its shard with libsme,
+all-reduces N and df (gloo) into sme_index_reweight, scores its shard, merges the
+per-shard top-k lists and checks them against the single-index oracle.
+usage: dist_gpu_worker.py RANK WORLD PORT IDF_MODE OUT_DIR"""
+import importlib
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PKG = "simple-mapreduce-search-engine-information-retrieval-_amd"
+
+
+def main():
+    rank, world, port, idf_mode, out_dir = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle_lib as O
+        sme = importlib.import_module(PKG)
+        D = importlib.import_module(PKG + ".dist")
+        synth = importlib.import_module(PKG + ".synth")
+        torch.cuda.set_device(0)
+        n = 700
+        corpus = synth.gen_corpus(n, V=900, seed=31, len_lo=10, len_hi=80)
+        mapping = synth.mapping_bytes(n)
+        ctx = sme.Context(1, 1, idf_mode)
+        cuts = D.split_points(corpus, world, ctx)
+        ctx.load_docno_mapping(mapping)
+        ix = ctx.build(corpus[cuts[rank]:cuts[rank + 1]])
+        N = D.global_count(ix.N)
+        assert N == n
+        gdf = D.global_df_index(ix)
+        ix.reweight(N, gdf.data_ptr())
+        full = O.OracleIndex(corpus, mapping, 1, 1)
+        fterms = sorted({t[0][0] for t in full.terms() if t[0] != (" ",)})
+        fdf = {t[0][0]: len(t[3]) for t in full.terms() if t[0] != (" ",)}
+        names = [ix.term(t) for t in range(ix.V)]
+        g = gdf.cpu().numpy()
+        assert all(int(g[t]) == fdf[names[t]] for t in range(ix.V))  # df all-reduce through fingerprints
+        rng = np.random.default_rng(11)
+        queries = [[fterms[i] for i in rng.integers(0, len(fterms), rng.integers(1, 7))] for _ in range(60)]
+        flat = [t for q in queries for t in q]
+        ids = ix.lookup(flat).astype(np.int32)  # -1: not in this shard, skipped like an unknown term
+        qoff = np.zeros(len(queries) + 1, np.int64)
+        qoff[1:] = np.cumsum([len(q) for q in queries])
+        for k in (10, 100):
+            dn, sc = ix.query_topk(ids, qoff, k)
+            md, ms = D.merge_topk(torch.from_numpy(dn), torch.from_numpy(sc), k)
+            for q, tl in enumerate(queries):
+                rd, rs = full.query(tl, k, idf_mode, 0)
+                assert md[q, :len(rd)].tolist() == rd, (k, q, tl)
+                assert ms[q, :len(rs)].numpy().tolist() == rs, (k, q)  # fp64 bit-exact
+                assert (md[q, len(rd):] == -1).all()
+        open(os.path.join(out_dir, "ok%d" % rank), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
