@@ -440,11 +440,22 @@ class CharKGramTermIndexer:
 
 
 class IntDocVectorsForwardIndex:
-    """Query side: getValue(terms) then rank() -> up to 10 docnos (score desc, docno asc)."""
+    """Query side: getValue(terms) then rank() -> up to 10 docnos (score desc,
+    docno asc), plus the REPL contract of IntDocVectorsForwardIndex.main
+    (C/sa/edu/kaust/fwindex/IntDocVectorsForwardIndex.java:243-322) in query_line."""
 
-    def __init__(self, index):
+    def __init__(self, index, mapping=None):
         self.index = index
         self._terms = []
+        self._docids = None
+        if mapping is not None:  # TrecDocnoMapping.loadMapping: {"", docids...}
+            n = struct.unpack_from(">i", mapping, 0)[0]
+            p, ids = 4, [""]
+            for _ in range(n):
+                ln = struct.unpack_from(">H", mapping, p)[0]
+                ids.append(_mutf8_decode(mapping[p + 2:p + 2 + ln]))
+                p += 2 + ln
+            self._docids = ids
 
     def getValue(self, terms):  # noqa: N802
         ids = self.index.lookup(list(terms))
@@ -455,3 +466,31 @@ class IntDocVectorsForwardIndex:
             return []
         dn, _ = self.index.query_topk(np.array(self._terms, np.int32), np.array([0, len(self._terms)], np.int64), k)
         return [int(d) for d in dn[0] if d >= 0]
+
+    def query_line(self, line, tokenizer=None):
+        """One REPL turn (:284-320): trim; an empty line, or one that is not 1-2
+        raw words (String.split("\\s+")), ends the session (returns None);
+        otherwise processContent -> getValue -> rank, printed as main prints it:
+        Arrays.toString of the docnos, or the docids each followed by a space
+        (mapping given), or "No results ..."."""
+        import re
+        term = line
+        b, e = 0, len(term)
+        while b < e and ord(term[b]) <= 0x20:  # String.trim
+            b += 1
+        while e > b and ord(term[e - 1]) <= 0x20:
+            e -= 1
+        term = term[b:e]
+        if not term:
+            return None
+        orig = re.split(r"[ \t\n\x0b\f\r]+", term)
+        if len(orig) not in (1, 2):
+            return None
+        ctx = tokenizer or self.index.ctx
+        self.getValue(ctx.process_content(term))
+        res = self.rank()
+        if self._docids is None:
+            body = ("[" + ", ".join(str(d) for d in res) + "]") if res else "No results ..."
+        else:
+            body = "".join(self._docids[d] + " " for d in res) if res else "No results ..."
+        return term + ": " + body
