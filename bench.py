@@ -211,8 +211,11 @@ def main():
     }
     if query is not None:
         result["query"] = query
+    qinternal = None
+    if query is not None:
+        qinternal = (query.pop("_terms"), query.pop("_qoff"), query.pop("_out"))
     if not a.no_checks:
-        result["checks"] = post_checks(a, sme, synth, ix, n_local, d0, query, rank)
+        result["checks"] = post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank)
         result["stage_ms"]["serialize_records_untimed"] = serialize_stage(ix)
     if rank == 0 and a.cpu_docs > 0 and a.config == "c2":
         result["cpu_baseline"] = cpu_baseline(synth, a)
@@ -314,7 +317,7 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
             "postings_touched_what": "8 B x postings of every query term (re-reads across queries included)"}
 
 
-def post_checks(a, sme, synth, ix, n_local, d0, query, rank):
+def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank):
     """Untimed, size-independent checks of the full-size build and query batch."""
     out = {}
     off, dn, tf, df = ix.csr()
@@ -341,9 +344,8 @@ def post_checks(a, sme, synth, ix, n_local, d0, query, rank):
         # every vocabulary word occurs at c2 sizes (rank 2^20 has ~34 expected occurrences)
         out["V_eq_distinct_terms_plus_docids"] = bool(ix.V == nv + n_local) if a.config == "c2" else None
         out["V_expected"] = nv + n_local
-    if query is not None:
-        terms, qoff = query.pop("_terms"), query.pop("_qoff")
-        out_d, out_s = query.pop("_out")
+    if qinternal is not None:
+        terms, qoff, (out_d, out_s) = qinternal
         nq = min(2000, len(qoff) - 1)
         t_s, q_s = terms[:qoff[nq]], qoff[:nq + 1]
         k = a.cfg["k"]

@@ -1376,6 +1376,12 @@ struct AggIn {
   const int32_t *multi_term;
   const int64_t *perm;   // records in docno order
   const int32_t *docno;  // per record
+  // emit form: v32 != nullptr writes the sort's packed u32 value (docno - dmin) * F + tf
+  // directly (K = 1, distinct docnos); otherwise p_val = docno << 32 | tf
+  uint32_t *v32 = nullptr;
+  int64_t dmin = 0;
+  uint32_t F = 0;
+  unsigned int *max_tf = nullptr;  // count pass: largest tf of any pair (atomicMax)
 };
 
 // Aggregate record r into table (keys/cnt, capacity mask). Returns distinct count or -1 on overflow.
@@ -1485,6 +1491,7 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
   int32_t *keys = keys_all[wv], *cnt = cnt_all[wv];
   int32_t *distinct = &dist_all[wv];
   const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
+  uint32_t wmax = 0;  // count pass: largest tf over this wave's records
   for (int64_t i = (int64_t)blockIdx.x * (kAggNT / 64) + wv; i < nR; i += nwaves) {
     if (EMIT && prec[i] < 0) continue;  // big record: block path
     const int64_t r = in.perm[i];
@@ -1513,6 +1520,10 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
     const bool big = __any(!ok) || d > kWLimit;
     if (!EMIT) {
       if (lane == 0) prec[i] = big ? -1 : d;
+      if (!big && in.max_tf) {
+#pragma unroll 4
+        for (int k = 0; k < kWCap / 64; k++) wmax = max(wmax, (uint32_t)cnt[k * 64 + lane]);
+      }
       wave_sync_lds();
       continue;
     }
@@ -1525,11 +1536,18 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
       if (key >= 0) {
         const int64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
         p_term[o] = (uint32_t)key;
-        p_val[o] = dn | (uint32_t)cnt[k * 64 + lane];
+        if (in.v32)
+          in.v32[o] = (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + cnt[k * 64 + lane]);
+        else
+          p_val[o] = dn | (uint32_t)cnt[k * 64 + lane];
       }
       base += __popcll(m);
     }
     wave_sync_lds();
+  }
+  if (!EMIT && in.max_tf) {
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
+    if (lane == 0 && wmax) atomicMax(in.max_tf, wmax);
   }
 }
 
@@ -1548,6 +1566,13 @@ __global__ __launch_bounds__(kAggNT) void k_agg_big(AggIn in, const int64_t *big
     int32_t d = agg_record(in, r, keys, cnt, cap - 1, (int32_t)cap, &s_distinct, &s_ovf);
     if (pass == 0) {
       if (threadIdx.x == 0) prec_count[i] = d;
+      if (in.max_tf) {
+        uint32_t m = 0;
+        for (uint32_t k = threadIdx.x; k < cap; k += kAggNT) m = max(m, keys[k] >= 0 ? (uint32_t)cnt[k] : 0u);
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+        if ((threadIdx.x & 63) == 0 && m) atomicMax(in.max_tf, m);
+      }
+      __syncthreads();
       continue;
     }
     // emit: chunked compaction over the table
@@ -1559,7 +1584,10 @@ __global__ __launch_bounds__(kAggNT) void k_agg_big(AggIn in, const int64_t *big
       int32_t o = block_excl_sum<kAggNT, int32_t>(key >= 0 ? 1 : 0, sc32, &tot);
       if (key >= 0) {
         p_term[base + o] = (uint32_t)key;
-        p_val[base + o] = ((uint64_t)(uint32_t)in.docno[r] << 32) | (uint32_t)cnt[k];
+        if (in.v32)
+          in.v32[base + o] = (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + cnt[k]);
+        else
+          p_val[base + o] = ((uint64_t)(uint32_t)in.docno[r] << 32) | (uint32_t)cnt[k];
       }
       base += tot;
     }
@@ -2281,7 +2309,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   DevBuf *W = cx->ws + kBuildWs;
   Prof prof(st);
   auto cub_tmp = [&](size_t bytes) { return cx->cub_tmp.get(bytes); };
-  unsigned long long *cnt = W[W_CNT].as<unsigned long long>(16);
+  unsigned long long *cnt = W[W_CNT].as<unsigned long long>(32);  // [20] max tf, [22..23] docno range
 
   const RecordSpans rsp = find_records(cx, t, n, st, &prof);
   uint64_t *rs = rsp.rs, *re = rsp.re, *C = rsp.C;
@@ -2610,6 +2638,20 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   int64_t P = 0;
   uint32_t *p_term = nullptr;
   uint64_t *p_val = nullptr;
+  // K = 1 with distinct docnos: the count pass also finds the largest tf, so the
+  // emit pass can write the term sort's packed u32 values ((docno - dmin) * F + tf)
+  // directly (no 8-byte pair values, no separate pack / stats passes)
+  const bool want_packed = K == 1 && !dup_docno && nR > 0;
+  unsigned int *mtf = reinterpret_cast<unsigned int *>(cnt + 20);
+  int *dmn = reinterpret_cast<int *>(cnt + 22), *dmx = dmn + 1;
+  int32_t h_mtf = 0, h_drange[2] = {0, -1};
+  if (want_packed) {
+    const int h_init[2] = {INT_MAX, INT_MIN};
+    SME_HIP(hipMemsetAsync(mtf, 0, sizeof(unsigned int), st));
+    SME_HIP(hipMemcpyAsync(dmn, h_init, sizeof h_init, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_docno_range, dim3(grid_for(nR, 256, 1024)), dim3(256), 0, st, docno, nR, dmn, dmx);
+    ai.max_tf = mtf;
+  }
   if (K == 1) {
   int32_t *prec = W[W_PREC].as<int32_t>(nR + 1);
   int64_t *pair_off = W[W_T3].as<int64_t>(nR + 1);  // rank_of_slot no longer needed
@@ -2656,10 +2698,24 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, prec64, pair_off, (int)nR + 1, st));
     SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, prec64, pair_off, (int)nR + 1, st));
   }
-  P = d2h(pair_off + nR, st);
+  SME_HIP(hipMemcpyAsync(&P, pair_off + nR, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  if (want_packed) {
+    SME_HIP(hipMemcpyAsync(&h_mtf, mtf, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipMemcpyAsync(h_drange, dmn, sizeof h_drange, hipMemcpyDeviceToHost, st));
+  }
+  SME_HIP(hipStreamSynchronize(st));
   ix->P = P;
   p_term = W[W_PTERM].as<uint32_t>(P + 1);
-  p_val = W[W_PVAL].as<uint64_t>(P + 1);
+  if (want_packed && P > 0) {
+    const int32_t tbits0 = bits_for((uint64_t)std::max<int64_t>(Vi, 1));
+    const uint64_t Fq = (uint64_t)std::max(h_mtf, 1) + 1, D = (uint64_t)((int64_t)h_drange[1] - h_drange[0] + 1);
+    if (D * Fq < (1ull << 32) && tbits0 + bits_for(Fq - 1) <= 32) {
+      ai.v32 = W[W_PVAL].as<uint32_t>(P + 1);
+      ai.dmin = h_drange[0];
+      ai.F = (uint32_t)Fq;
+    }
+  }
+  if (!ai.v32) p_val = W[W_PVAL].as<uint64_t>(P + 1);
   if (nR > 0) {
     // big records are flagged in prec via a negative marker: keep a copy of flags
     hipLaunchKernelGGL(k_agg_w<true>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, prec, pair_off, p_term, p_val);
@@ -2737,20 +2793,23 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   bool packed = false;
   int64_t dmin = 0;
   uint32_t F = 0;
-  if (P > 0 && !dup_docno && K == 1) {
-    unsigned int *mtf = reinterpret_cast<unsigned int *>(cnt + 11);
-    int *dmn = reinterpret_cast<int *>(cnt + 12), *dmx = dmn + 1;
+  if (ai.v32 != nullptr) {  // emitted packed by the aggregation (see want_packed)
+    max_tf = std::max<int32_t>(1, h_mtf);
+    packed = true;
+    dmin = ai.dmin;
+    F = ai.F;
+  } else if (P > 0 && !dup_docno && K == 1) {
     SME_HIP(hipMemsetAsync(mtf, 0, sizeof(unsigned int), st));
     const int h_init[2] = {INT_MAX, INT_MIN};
     SME_HIP(hipMemcpyAsync(dmn, h_init, sizeof h_init, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_pair_stats, dim3(grid_for(P, 256, 2048)), dim3(256), 0, st, p_val, P, mtf);
     hipLaunchKernelGGL(k_docno_range, dim3(grid_for(nR, 256, 1024)), dim3(256), 0, st, docno, nR, dmn, dmx);
-    unsigned int h_mtf = d2h(mtf, st);
+    unsigned int h_m = d2h(mtf, st);
     int h_r[2];
     SME_HIP(hipMemcpyAsync(h_r, dmn, sizeof h_r, hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
-    const uint64_t Fq = (uint64_t)h_mtf + 1, D = (uint64_t)((int64_t)h_r[1] - (int64_t)h_r[0] + 1);
-    max_tf = std::max<int32_t>(1, (int32_t)h_mtf);
+    const uint64_t Fq = (uint64_t)h_m + 1, D = (uint64_t)((int64_t)h_r[1] - (int64_t)h_r[0] + 1);
+    max_tf = std::max<int32_t>(1, (int32_t)h_m);
     packed = D * Fq < (1ull << 32) && tbits + bits_for((uint64_t)max_tf) <= 32;
     dmin = h_r[0];
     F = (uint32_t)Fq;
@@ -2758,9 +2817,12 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   int32_t *docno_d = nullptr, *tf_d = nullptr;
   int64_t *off = nullptr;
   if (packed) {
-    uint32_t *v32 = reinterpret_cast<uint32_t *>(W[W_T1].as<uint64_t>(P + 1));
+    uint32_t *v32 = ai.v32;
+    if (v32 == nullptr) {
+      v32 = reinterpret_cast<uint32_t *>(W[W_T1].as<uint64_t>(P + 1));
+      hipLaunchKernelGGL(k_pack_pairs, dim3(grid_for(P)), dim3(256), 0, st, p_val, P, dmin, F, v32);
+    }
     uint32_t *v32s = W[W_T2].as<uint32_t>(P + 1);
-    hipLaunchKernelGGL(k_pack_pairs, dim3(grid_for(P)), dim3(256), 0, st, p_val, P, dmin, F, v32);
     size_t tbb = 0;
     SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, p_term, key_s, v32, v32s, (int)P, 0, tbits, st));
     SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, p_term, key_s, v32, v32s, (int)P, 0, tbits, st));
