@@ -175,7 +175,7 @@ def main():
     achieved_build = alg_bytes / dt / 1e9
     tok_ms = prof.get("tok_kernel")
     tok_gbs = nbytes / (tok_ms * 1e-3) / 1e9 if tok_ms else None
-    traffic = pmc_traffic("k_tok_fast", a)
+    traffic, t_fetch_raw, t_write = pmc_traffic("k_tok_fast", a, detail=True)
 
     # ---- queries (c3) ----
     query = None
@@ -200,7 +200,8 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_tok_fast", "achieved": round(tok_gbs, 2) if tok_gbs else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(tok_gbs / HBM_PEAK_GBS, 5) if tok_gbs else None,
-                     "traffic": traffic, "kernel_ms": tok_ms,
+                     "traffic": traffic, "traffic_fetch_raw": t_fetch_raw, "traffic_write": t_write,
+                     "kernel_ms": tok_ms,
                      "what": "dominant kernel k_tok_fast: algorithmic bytes = text bytes B read once per launch, / "
                              "mean launch time (HIP events on its stream); traffic = PMC HBM bytes per launch "
                              "(profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)"},
@@ -303,6 +304,7 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     alg = 8 * int(df[uniq].sum()) + 4 * int(nt.sum()) + 12 * k * a.queries
     touched = 8 * int(df[tv].sum())
     t_k = (qk_ms * 1e-3) if qk_ms else dt
+    qtr = pmc_traffic(kname, a, detail=True)
     return {"metric": "top-%d queries/sec" % k, "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
             "terms_per_query": "U{2..8} drawn by df (seed %d)" % a.cfg["qseed"], "ms_per_batch": round(dt * 1e3, 3),
             "prep_ms": qp_ms, "_terms": terms, "_qoff": qoff, "_out": (out_d, out_s),
@@ -310,7 +312,8 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
                          "u8 tf + impact rows of terms with df >= span/32, heaviest-term query order",
             "roofline": {"bound": "hbm", "kernel": kname, "kernel_ms": qk_ms,
                          "achieved": round(alg / t_k / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(alg / t_k / 1e9 / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname, a),
+                         "frac": round(alg / t_k / 1e9 / HBM_PEAK_GBS, 6), "traffic": qtr[0],
+                         "traffic_fetch_raw": qtr[1], "traffic_write": qtr[2],
                          "what": "A_q = 8*sum(df of distinct batch terms) + 4*sum|q| + 12*k*Q per launch / "
                                  "mean launch time (HIP events)"},
             "postings_touched_GBps": round(touched / t_k / 1e9, 2),
@@ -379,19 +382,24 @@ def serialize_stage(ix):
             "what": "sme_index_partition_records for every partition (device k_ser_* + D2H), after the timed steps"}
 
 
-def pmc_traffic(kernel, a):
+def pmc_traffic(kernel, a, detail=False):
     """HBM bytes per launch of `kernel` from the committed PMC passes
     (profiles/pmc_traffic.json, written by tools/pmc_summary.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench config), or None."""
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench config), or None.
+    detail=True: (corrected total, raw FETCH_SIZE bytes, WRITE_SIZE bytes)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
-        return None
-    if d.get("docs") != a.docs or d.get("vocab") != a.vocab:
-        return None
+        return (None, None, None) if detail else None
+    if d.get("docs") != a.docs or d.get("vocab") != a.vocab or a.config != "c2":
+        return (None, None, None) if detail else None
     k = d.get("kernels", {}).get(kernel)
-    return None if k is None else k.get("hbm_bytes_per_launch")
+    if k is None:
+        return (None, None, None) if detail else None
+    if detail:
+        return k.get("hbm_bytes_per_launch"), k.get("fetch_bytes_raw"), k.get("write_bytes")
+    return k.get("hbm_bytes_per_launch")
 
 
 def _cpu_model():

@@ -2390,7 +2390,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
         // events bracket exactly this launch: "tok_kernel" is the dominant kernel's
         // duration that bench.py reports against the HBM roofline
         prof.mark("tok_setup");
-        const int64_t tgrid = std::min<int64_t>(nF, 4096), rpb = (nF + tgrid - 1) / tgrid;
+        const char *tg = getenv("SME_TOKGRID");
+        const int64_t tgrid = std::min<int64_t>(nF, tg ? atoll(tg) : 4096), rpb = (nF + tgrid - 1) / tgrid;
         hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)((nF + rpb - 1) / rpb)), dim3(kTokNT), 0, st, t, (int64_t)n, rs,
                            re, frec, nF, rpb, tok, ntok, tb);
         SME_CHECK_LAUNCH();
