@@ -409,26 +409,40 @@ __device__ __forceinline__ int64_t dense_pos(int64_t x) {
   const int64_t r = x & (kWTile - 1);
   return (x - r) + kDPL * (r & 63) + (r >> 6);
 }
-// one block per dense row (grid-stride): tf and impact bytes at docno - dmin
-__global__ __launch_bounds__(256) void k_dense_fill(const int32_t *drow, int64_t nrows, const int32_t *term_of_row,
-                                                    const int64_t *off, const int32_t *docno, const int32_t *tf,
-                                                    const double *lut, const double *idf,
-                                                    const unsigned long long *wmax_bits, int64_t dmin, int64_t stride,
-                                                    uint8_t *dtf, uint8_t *dq) {
+// tf and impact bytes at docno - dmin for every posting of a dense row, over the
+// batch rows' postings as one flat list (chunks of kSkipChunk, like k_skip_fill)
+// so a head term's million postings spread over the whole chip
+__global__ __launch_bounds__(256) void k_dense_fill(const int64_t *rpre, int64_t nrows, const int32_t *drow,
+                                                    const int32_t *term_of_row, const int64_t *off,
+                                                    const int32_t *docno, const int32_t *tf, const double *lut,
+                                                    const double *idf, const unsigned long long *wmax_bits,
+                                                    int64_t dmin, int64_t stride, uint8_t *dtf, uint8_t *dq) {
   const double wmax = __longlong_as_double((long long)*wmax_bits);
   const double alpha = wmax > 0.0 ? 253.5 / wmax : 1.0;
-  for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
-    const int32_t d = drow[r];
-    if (d < 0) continue;
-    const int32_t t = term_of_row[r];
-    const int64_t b = off[t], e = off[t + 1];
-    const double widf = idf[t];
-    uint8_t *rt = dtf + (int64_t)d * stride, *rq = dq + (int64_t)d * stride;
-    for (int64_t p = b + threadIdx.x; p < e; p += blockDim.x) {
+  const int64_t total = rpre[nrows];
+  for (int64_t x0 = (int64_t)blockIdx.x * kSkipChunk; x0 < total; x0 += (int64_t)gridDim.x * kSkipChunk) {
+    const int64_t x1 = x0 + kSkipChunk < total ? x0 + kSkipChunk : total;
+    int64_t lo = 0, hi = nrows;  // row of x0
+    while (hi - lo > 1) {
+      const int64_t m = (lo + hi) >> 1;
+      if (rpre[m] <= x0) lo = m;
+      else hi = m;
+    }
+    int64_t row = lo, rb = rpre[row], re = rpre[row + 1];
+    for (int64_t x = x0 + threadIdx.x; x < x1; x += blockDim.x) {
+      while (x >= re) {
+        row++;
+        rb = re;
+        re = rpre[row + 1];
+      }
+      const int32_t d = drow[row];
+      if (d < 0) continue;
+      const int32_t t = term_of_row[row];
+      const int64_t p = off[t] + (x - rb);
       const int32_t f = tf[p];  // <= 255 (k_row_stats)
-      const int64_t pos = dense_pos((int64_t)docno[p] - dmin);
-      rt[pos] = (uint8_t)f;
-      rq[pos] = (uint8_t)impact(lut[f], widf, alpha);
+      const int64_t pos = (int64_t)d * stride + dense_pos((int64_t)docno[p] - dmin);
+      dtf[pos] = (uint8_t)f;
+      dq[pos] = (uint8_t)impact(lut[f], idf[t], alpha);
     }
   }
 }
@@ -902,8 +916,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
               uint8_t *dns = W[61].as<uint8_t>(2 * nd * stride);
               SME_HIP(hipMemsetAsync(dns, 0, (size_t)(2 * nd * stride), st));
               hipLaunchKernelGGL(k_dense_rows, dim3(gR), dim3(256), 0, st, flag, dscan, nrows, cap, drw);
-              hipLaunchKernelGGL(k_dense_fill, dim3((unsigned)std::min<int64_t>(nrows, 8192)), dim3(256), 0, st, drw,
-                                 nrows, tor, off, dn, tf, lut, idf, wmax, ix->dmin, stride, dns, dns + nd * stride);
+              hipLaunchKernelGGL(k_dense_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, drw, tor, off, dn, tf, lut,
+                                 idf, wmax, ix->dmin, stride, dns, dns + nd * stride);
               SME_CHECK_LAUNCH();
               dtf = dns;
               dq = dns + nd * stride;
