@@ -2188,7 +2188,7 @@ enum {
   W_S, W_E, W_C, W_CNT, W_EOF, W_NEXTS, W_RS, W_RE, W_DOCNO, W_SLOW, W_SLOWLIST, W_SCROFF, W_U16, W_BOFF,
   W_TOK, W_NTOK, W_RKEYS, W_RREPS, W_POOL, W_CKEY, W_CSTR, W_NOUT, W_LONG, W_FKEYS, W_FREPS, W_CFINAL,
   W_VSLOT, W_KHI, W_KLO, W_VIDX, W_T0, W_T1, W_T2, W_T3, W_RAWTERM, W_MULTI, W_PERM, W_PREC, W_PTERM, W_PVAL,
-  W_MAXNOUT, W_SS, W_SE, W_SC, W_RLIST, W_RFLAG, W_POFF, W_OVFKEY, W_FREC, W_LT,
+  W_MAXNOUT, W_SS, W_SE, W_SC, W_RLIST, W_RFLAG, W_POFF, W_OVFKEY, W_FREC, W_LT, W_RADIX,
   W_NSLOTS
 };
 constexpr int kBuildWs = 64;  // build slots live at ctx->ws[64..127]
@@ -2824,15 +2824,15 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       hipLaunchKernelGGL(k_pack_pairs, dim3(grid_for(P)), dim3(256), 0, st, p_val, P, dmin, F, v32);
     }
     uint32_t *v32s = W[W_T2].as<uint32_t>(P + 1);
-    size_t tbb = 0;
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, p_term, key_s, v32, v32s, (int)P, 0, tbits, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, p_term, key_s, v32, v32s, (int)P, 0, tbits, st));
+    docno_d = ix->d_docno_d.as<int32_t>(P + 1);
+    tf_d = ix->d_tf_d.as<int32_t>(P + 1);
+    // hand-written stable LSD radix sort by term id (sme_sort.hip); the last
+    // pass unpacks (docno, tf) into the CSR arrays
+    uint32_t *rscr = W[W_RADIX].as<uint32_t>(term_sort_scratch(P) / sizeof(uint32_t) + 1);
+    key_s = term_sort(p_term, v32, key_s, v32s, P, tbits, dmin, F, docno_d, tf_d, rscr, st);
     off = ix->d_off.as<int64_t>(Vi + 1);
     SME_HIP(hipMemsetAsync(off, 0, (Vi + 1) * sizeof(int64_t), st));
     hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, Vi);
-    docno_d = ix->d_docno_d.as<int32_t>(P + 1);
-    tf_d = ix->d_tf_d.as<int32_t>(P + 1);
-    hipLaunchKernelGGL(k_unpack_packed, dim3(grid_for(P)), dim3(256), 0, st, v32s, P, dmin, F, docno_d, tf_d);
     SME_CHECK_LAUNCH();
   } else {
     uint64_t *val_s = W[W_T1].as<uint64_t>(P + 1);

@@ -1,0 +1,316 @@
+// sme_sort.hip -- the shuffle sort of the index job: (term, posting) pairs
+// ordered by term id, stable, so the postings of a term keep the docno order
+// the aggregation emitted them in (the reducer's docno sort,
+// TermKGramDocIndexer.java:168-213; key order TermDF.compareTo,
+// TermDF.java:64-70 = term id order, ids being String.compareTo ranks).
+//
+// LSD radix sort over the term id, <= 11-bit digits (2 passes for the 21-bit
+// ids of c2).  Each pass is reduce-then-scan, no inter-block waiting:
+//   k_rs_count   one 16384-item tile per 1024-thread block: LDS digit
+//                histogram, written tile-major (coalesced)
+//   k_rs_colsum  per (digit, tile group) sums; k_rs_scan one-block exclusive
+//                scan over them in digit-major order; k_rs_colscan turns the
+//                tile counts into each (tile, digit)'s global output offset
+//   k_rs_scatter each wave ranks its 1024 contiguous items with ballot peer
+//                masks and running per-wave digit counters in LDS (stable);
+//                the block scans those counters (digits, then waves) into the
+//                tile's digit-sorted order, stages keys and then values in
+//                LDS in that order, and writes them out as contiguous runs
+//                per digit (offset(tile, digit) + slot - digit's first slot).
+// The last pass writes the sorted keys and unpacks the packed values
+// ((docno - dmin) * F + tf) straight into the CSR's docno / tf arrays.
+#include <hip/hip_runtime.h>
+
+#include "sme_internal.hpp"
+
+namespace sme {
+namespace {
+
+constexpr int kRsNT = 1024;                 // threads per block (16 waves)
+constexpr int kRsWaves = kRsNT / 64;
+constexpr int kRsIPL = 16;                  // items per lane
+constexpr int kRsTile = kRsNT * kRsIPL;     // 16384 items per tile
+constexpr int kRsWaveItems = 64 * kRsIPL;   // 1024 contiguous items per wave
+constexpr int kRsMaxBits = 11;
+constexpr int kRsMaxBins = 1 << kRsMaxBits;
+constexpr int kRsGroups = 256;              // tile groups of the column scan
+
+__global__ __launch_bounds__(kRsNT) void k_rs_count(const uint32_t *__restrict__ key, int64_t P, int shift,
+                                                    int nbins, uint32_t *__restrict__ counts) {
+  __shared__ uint32_t h[kRsMaxBins];
+  const int tid = threadIdx.x;
+  for (int b = tid; b < nbins; b += kRsNT) h[b] = 0;
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * kRsTile;
+  const uint32_t mask = (uint32_t)nbins - 1u;
+  const int64_t n = min((int64_t)kRsTile, P - t0);
+  if (n == kRsTile) {
+    const uint4 *k4 = reinterpret_cast<const uint4 *>(key + t0);
+#pragma unroll
+    for (int i = 0; i < kRsIPL / 4; i++) {
+      const uint4 v = k4[i * kRsNT + tid];
+      atomicAdd(&h[(v.x >> shift) & mask], 1u);
+      atomicAdd(&h[(v.y >> shift) & mask], 1u);
+      atomicAdd(&h[(v.z >> shift) & mask], 1u);
+      atomicAdd(&h[(v.w >> shift) & mask], 1u);
+    }
+  } else {
+    for (int64_t i = tid; i < n; i += kRsNT) atomicAdd(&h[(key[t0 + i] >> shift) & mask], 1u);
+  }
+  __syncthreads();
+  for (int b = tid; b < nbins; b += kRsNT) counts[(int64_t)blockIdx.x * nbins + b] = h[b];
+}
+
+// gsum[b * G + g] = sum of counts[t][b] over the tiles t of group g
+__global__ __launch_bounds__(kRsNT) void k_rs_colsum(const uint32_t *__restrict__ counts, int64_t ntiles, int nbins,
+                                                     int64_t tpg, uint32_t *__restrict__ gsum) {
+  const int g = blockIdx.x;
+  const int64_t ta = (int64_t)g * tpg, tb = min(ntiles, ta + tpg);
+  for (int b = threadIdx.x; b < nbins; b += kRsNT) {
+    uint32_t s = 0;
+    for (int64_t t = ta; t < tb; t++) s += counts[t * nbins + b];
+    gsum[(int64_t)b * kRsGroups + g] = s;
+  }
+}
+
+// in-place exclusive scan of n u32 (one block; n a multiple of 16): rounds
+// of 16384, 16 contiguous elements per thread (four 16-byte loads)
+__global__ __launch_bounds__(kRsNT) void k_rs_scan(uint32_t *__restrict__ a, int n) {
+  __shared__ uint32_t ws[kRsWaves];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t carry = 0;
+  for (int r0 = 0; r0 < n; r0 += 16 * kRsNT) {
+    const int i0 = r0 + 16 * tid;
+    uint4 x[4];
+    uint32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      x[c] = i0 < n ? reinterpret_cast<const uint4 *>(a + i0)[c] : make_uint4(0, 0, 0, 0);
+      s += x[c].x + x[c].y + x[c].z + x[c].w;
+    }
+    uint32_t incl = s;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t wb = carry, tot = 0;
+    for (int j = 0; j < kRsWaves; j++) {
+      const uint32_t t = ws[j];
+      if (j < w) wb += t;
+      tot += t;
+    }
+    uint32_t run = wb + incl - s;
+    if (i0 < n) {
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        uint4 y;
+        y.x = run;
+        run += x[c].x;
+        y.y = run;
+        run += x[c].y;
+        y.z = run;
+        run += x[c].z;
+        y.w = run;
+        run += x[c].w;
+        reinterpret_cast<uint4 *>(a + i0)[c] = y;
+      }
+    }
+    carry += tot;
+    __syncthreads();
+  }
+}
+
+// counts[t][b] <- global offset of digit b's items of tile t
+__global__ __launch_bounds__(kRsNT) void k_rs_colscan(uint32_t *__restrict__ counts, int64_t ntiles, int nbins,
+                                                      int64_t tpg, const uint32_t *__restrict__ gsum) {
+  const int g = blockIdx.x;
+  const int64_t ta = (int64_t)g * tpg, tb = min(ntiles, ta + tpg);
+  for (int b = threadIdx.x; b < nbins; b += kRsNT) {
+    uint32_t run = gsum[(int64_t)b * kRsGroups + g];
+    for (int64_t t = ta; t < tb; t++) {
+      const uint32_t c = counts[t * nbins + b];
+      counts[t * nbins + b] = run;
+      run += c;
+    }
+  }
+}
+
+template <bool LAST>
+__global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict__ key, const uint32_t *__restrict__ val,
+                                                      int64_t P, int shift, int nbits,
+                                                      const uint32_t *__restrict__ offs, uint32_t *__restrict__ okey,
+                                                      uint32_t *__restrict__ oval, int32_t *__restrict__ odocno,
+                                                      int32_t *__restrict__ otf, int64_t dmin, uint32_t F) {
+  // wc: per-wave running digit counts, then each (wave, digit)'s first slot in
+  // the tile sorted by digit; gd: global offset - tile slot of each digit
+  __shared__ uint16_t wc[kRsWaves * kRsMaxBins];
+  __shared__ uint32_t gd[kRsMaxBins];
+  __shared__ uint32_t stage[kRsTile];
+  __shared__ uint32_t ws[kRsWaves];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nbins = 1 << nbits;
+  const uint32_t mask = (uint32_t)nbins - 1u;
+  // XCD-aware tile order: blocks are dealt round-robin to the 8 XCDs, so XCD x
+  // gets the contiguous tile range [x * per, (x + 1) * per).  Neighbouring
+  // tiles write neighbouring pieces of every digit's run at about the same
+  // time, and those partial lines meet in one L2 instead of reaching HBM as
+  // partial writes from different XCDs.
+  const int64_t per = (int64_t)(gridDim.x >> 3);
+  const int64_t tile = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const int64_t t0 = tile * kRsTile;
+  if (t0 >= P) return;
+  const int n = (int)min((int64_t)kRsTile, P - t0);
+  for (int i = tid; i < kRsWaves * kRsMaxBins / 2; i += kRsNT) reinterpret_cast<uint32_t *>(wc)[i] = 0u;
+  __syncthreads();
+  uint16_t *mine = wc + w * kRsMaxBins;
+  const int wb = w * kRsWaveItems;  // this wave's items: tile slots [wb, wb + 1024)
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t k[kRsIPL], v[kRsIPL], pos[kRsIPL];
+#pragma unroll
+  for (int s = 0; s < kRsIPL; s++) {
+    const int i = wb + s * 64 + lane;
+    const bool ok = i < n;
+    k[s] = ok ? key[t0 + i] : 0u;
+    v[s] = ok ? val[t0 + i] : 0u;
+  }
+  // 1. stable rank of every item among its wave's items of the same digit
+#pragma unroll
+  for (int s = 0; s < kRsIPL; s++) {
+    const bool ok = wb + s * 64 + lane < n;
+    const uint32_t d = (k[s] >> shift) & mask;
+    uint64_t peers = (uint64_t)__ballot(ok);
+    for (int b = 0; b < nbits; b++) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = (uint64_t)__ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    uint32_t r = 0;
+    if (ok) {
+      const uint32_t c = mine[d];
+      r = c + (uint32_t)__popcll(peers & lt);
+      if ((peers & lt) == 0) mine[d] = (uint16_t)(c + (uint32_t)__popcll(peers));
+    }
+    pos[s] = r;
+  }
+  __syncthreads();
+  // 2. tile slot of each (wave, digit): digits in order, waves in order
+  {
+    const int b0 = 2 * tid;
+    uint32_t t0c = 0, t1c = 0;
+    if (b0 < nbins) {
+#pragma unroll
+      for (int x = 0; x < kRsWaves; x++) {
+        t0c += wc[x * kRsMaxBins + b0];
+        t1c += wc[x * kRsMaxBins + b0 + 1];
+      }
+    }
+    const uint32_t s2 = t0c + t1c;
+    uint32_t incl = s2;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t ex = incl - s2;
+    for (int j = 0; j < w; j++) ex += ws[j];
+    if (b0 < nbins) {
+      uint32_t r0 = ex, r1 = ex + t0c;
+      gd[b0] = offs[tile * nbins + b0] - r0;
+      gd[b0 + 1] = offs[tile * nbins + b0 + 1] - r1;
+#pragma unroll
+      for (int x = 0; x < kRsWaves; x++) {
+        const uint32_t c0 = wc[x * kRsMaxBins + b0], c1 = wc[x * kRsMaxBins + b0 + 1];
+        wc[x * kRsMaxBins + b0] = (uint16_t)r0;
+        wc[x * kRsMaxBins + b0 + 1] = (uint16_t)r1;
+        r0 += c0;
+        r1 += c1;
+      }
+    }
+  }
+  __syncthreads();
+  // 3. keys through LDS in digit order, then coalesced runs to their digits
+#pragma unroll
+  for (int s = 0; s < kRsIPL; s++) {
+    if (wb + s * 64 + lane >= n) continue;
+    pos[s] += mine[(k[s] >> shift) & mask];
+    stage[pos[s]] = k[s];
+  }
+  __syncthreads();
+  uint32_t dst[kRsIPL];
+#pragma unroll
+  for (int j = 0; j < kRsIPL; j++) {
+    const int p = j * kRsNT + tid;
+    if (p < n) {
+      const uint32_t kk = stage[p];
+      dst[j] = gd[(kk >> shift) & mask] + (uint32_t)p;
+      okey[dst[j]] = kk;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < kRsIPL; s++)
+    if (wb + s * 64 + lane < n) stage[pos[s]] = v[s];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRsIPL; j++) {
+    const int p = j * kRsNT + tid;
+    if (p < n) {
+      const uint32_t vv = stage[p];
+      if (LAST) {
+        odocno[dst[j]] = (int32_t)((int64_t)(vv / F) + dmin);
+        otf[dst[j]] = (int32_t)(vv % F);
+      } else {
+        oval[dst[j]] = vv;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// Stable sort of P (key, packed value) pairs by the low `bits` bits of key.
+// k0/v0 hold the input; k1/v1 are a second buffer pair of the same size.  The
+// sorted keys end in k0 or k1 (returned); the values are unpacked into docno /
+// tf.  counts: ceil(P / 16384) * 2048 + 2048 * 256 u32 of scratch.
+uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t P, int bits, int64_t dmin,
+                    uint32_t F, int32_t *docno, int32_t *tf, uint32_t *counts, hipStream_t st) {
+  if (P <= 0) return k0;
+  if (P > 0xFFFFFFFFll) throw Error(SME_ELIMIT, "term sort of more than 2^32 pairs");
+  bits = std::max(bits, 1);
+  const int npass = (bits + kRsMaxBits - 1) / kRsMaxBits;
+  const int64_t ntiles = (P + kRsTile - 1) / kRsTile;
+  const int64_t tpg = (ntiles + kRsGroups - 1) / kRsGroups;
+  uint32_t *gsum = counts + ntiles * kRsMaxBins;
+  int shift = 0;
+  for (int p = 0; p < npass; p++) {
+    const int nb = (bits - shift + (npass - p) - 1) / (npass - p);  // near-equal digits
+    const int nbins = 1 << nb;
+    const bool last = p == npass - 1;
+    hipLaunchKernelGGL(k_rs_count, dim3((unsigned)ntiles), dim3(kRsNT), 0, st, k0, P, shift, nbins, counts);
+    hipLaunchKernelGGL(k_rs_colsum, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
+    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, nbins * kRsGroups);
+    hipLaunchKernelGGL(k_rs_colscan, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
+    const unsigned sgrid = (unsigned)(8 * ((ntiles + 7) / 8));  // see the XCD tile order in k_rs_scatter
+    if (last)
+      hipLaunchKernelGGL(k_rs_scatter<true>, dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, P, shift, nb, counts,
+                         k1, nullptr, docno, tf, dmin, F);
+    else
+      hipLaunchKernelGGL(k_rs_scatter<false>, dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, P, shift, nb,
+                         counts, k1, v1, nullptr, nullptr, dmin, F);
+    SME_CHECK_LAUNCH();
+    std::swap(k0, k1);
+    std::swap(v0, v1);
+    shift += nb;
+  }
+  return k0;
+}
+
+size_t term_sort_scratch(int64_t P) {
+  const int64_t ntiles = (std::max<int64_t>(P, 1) + kRsTile - 1) / kRsTile;
+  return (size_t)(ntiles * kRsMaxBins + (int64_t)kRsMaxBins * kRsGroups) * sizeof(uint32_t);
+}
+
+}  // namespace sme
