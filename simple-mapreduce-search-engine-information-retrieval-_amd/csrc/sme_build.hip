@@ -493,16 +493,35 @@ struct RawTable {
 };
 
 // Raw-token signature: w0/w1 = the first 16 bytes (little-endian, zero padded),
-// h = a word-wise mix of (len, w0, w1, further 8-byte words).  (w0, w1, len)
-// identify tokens of <= 16 bytes exactly; longer ones are compared byte-wise.
+// h = a hash of them (+ the length and further 8-byte words for tokens longer
+// than 16 bytes).  No token byte is 0 (0 is a split byte), so (w0, w1) alone
+// identify a token of <= 16 bytes; longer ones are compared byte-wise.
+// The hash is multilinear in the four 32-bit words (two v_mad_u64_u32) and ends
+// in a 32-bit finaliser: low word of h = table hash, high word = the product's
+// low word | 1 (h != 0 marks a used slot).  Every multiply is 32-bit: 64-bit
+// multiplies are four quarter-rate VALU ops each on CDNA.
 struct TokSig {
   uint64_t h, w0, w1;
 };
-__device__ __forceinline__ uint64_t sig_mix(uint64_t h, uint64_t w) { return fmix64(h ^ (w * 0x9E3779B97F4A7C15ull)); }
-__device__ __forceinline__ uint64_t sig_head(uint64_t len, uint64_t w0, uint64_t w1) {
-  return sig_mix(sig_mix(0xC2B2AE3D27D4EB4Full ^ len, w0), w1);
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
 }
-__device__ __forceinline__ uint64_t sig_fin(uint64_t h) { return h ? h : 1; }
+__device__ __forceinline__ uint64_t sig_head(uint64_t w0, uint64_t w1) {
+  const uint64_t p = (uint64_t)((uint32_t)w0 + 0x9E3779B9u) * (uint64_t)((uint32_t)(w0 >> 32) + 0x85EBCA6Bu) +
+                     (uint64_t)((uint32_t)w1 + 0xC2B2AE35u) * (uint64_t)((uint32_t)(w1 >> 32) + 0x27D4EB2Fu);
+  const uint32_t x = fmix32((uint32_t)(p >> 32) ^ ((uint32_t)p >> 13));
+  return ((uint64_t)((uint32_t)p | 1u) << 32) | x;
+}
+__device__ __forceinline__ uint64_t sig_mix(uint64_t h, uint64_t w) {  // long tokens: length and words 16..
+  const uint64_t p = (uint64_t)((uint32_t)w + 0x165667B1u) * (uint64_t)((uint32_t)(w >> 32) + 0xD3A2646Cu);
+  const uint32_t x = fmix32((uint32_t)h ^ (uint32_t)(p >> 32) ^ ((uint32_t)p >> 11));
+  return ((uint64_t)(((uint32_t)(h >> 32) ^ (uint32_t)p) | 1u) << 32) | x;
+}
 __device__ __forceinline__ uint64_t load_word_bytes(const uint8_t *p, int64_t n) {  // n in [0, 8]
   uint64_t w = 0;
   for (int64_t i = 0; i < n; i++) w |= (uint64_t)p[i] << (8 * i);
@@ -512,9 +531,10 @@ __device__ __forceinline__ TokSig sig_bytes(const uint8_t *p, int64_t len) {
   TokSig g;
   g.w0 = load_word_bytes(p, len < 8 ? len : 8);
   g.w1 = len > 8 ? load_word_bytes(p + 8, len < 16 ? len - 8 : 8) : 0;
-  uint64_t h = sig_head((uint64_t)len, g.w0, g.w1);
+  uint64_t h = sig_head(g.w0, g.w1);
+  if (len > 16) h = sig_mix(h, (uint64_t)len);
   for (int64_t o = 16; o < len; o += 8) h = sig_mix(h, load_word_bytes(p + o, len - o < 8 ? len - o : 8));
-  g.h = sig_fin(h);
+  g.h = h;
   return g;
 }
 
@@ -550,9 +570,18 @@ __device__ __forceinline__ SlotVal ld_slot_plain(const RawSlot *s) {
   return v;
 }
 
-// Find-or-insert the raw token (signature g, text[off, off+len)); v holds the
-// plainly loaded words of its home slot (g.h & mask).  Returns the slot index.
-__device__ __noinline__ uint32_t raw_insert(const RawTable &tb, const TokSig &g, uint64_t off, uint64_t len, SlotVal v) {
+// Find-or-insert the raw token (signature gh/gw0/gw1, text[off, off+len)); v holds
+// the plainly loaded words of its home slot (gh & mask).  Returns the slot index.
+// Scalar arguments only: a struct passed by reference to a non-inlined call
+// lives in scratch memory, and the token loop would spill every signature.
+__device__ __noinline__ uint32_t raw_insert_s(RawSlot *slots, uint64_t mask, const uint8_t *text,
+                                              unsigned int *overflow, uint64_t gh, uint64_t gw0, uint64_t gw1,
+                                              uint64_t off, uint64_t len, unsigned long long vkey,
+                                              unsigned long long vrep, unsigned long long vw0,
+                                              unsigned long long vw1) {
+  const RawTable tb{slots, mask, text, overflow};
+  const TokSig g{gh, gw0, gw1};
+  SlotVal v{vkey, vrep, vw0, vw1};
   if (len >= (1ull << 24)) {
     atomicOr(tb.overflow, 2u);
     return 0xFFFFFFFFu;
@@ -609,6 +638,10 @@ __device__ __noinline__ uint32_t raw_insert(const RawTable &tb, const TokSig &g,
   atomicOr(tb.overflow, 1u);
   return 0xFFFFFFFFu;
 }
+__device__ __forceinline__ uint32_t raw_insert(const RawTable &tb, const TokSig &g, uint64_t off, uint64_t len,
+                                               const SlotVal &v) {
+  return raw_insert_s(tb.slots, tb.mask, tb.text, tb.overflow, g.h, g.w0, g.w1, off, len, v.key, v.rep, v.w0, v.w1);
+}
 __device__ __forceinline__ uint32_t raw_insert(const RawTable &tb, const TokSig &g, uint64_t off, uint64_t len) {
   return raw_insert(tb, g, off, len, ld_slot_plain(&tb.slots[g.h & tb.mask]));
 }
@@ -622,13 +655,20 @@ __device__ __forceinline__ uint32_t raw_insert(const RawTable &tb, const TokSig 
 // is either wholly inside a span or wholly outside).
 //
 // A workgroup owns a contiguous range of records and walks their bytes as ONE
-// stream of 4 KiB chunks (records are ~4 KiB: a chunk-per-record walk would
-// leave most of every second chunk idle).  Per chunk: coalesced 16-byte loads
-// into LDS (+1 KiB lookahead), the overlapping records' spans into LDS, per-lane
-// split classes over 16 bytes, span coverage by a block max-scan, token ranks by
-// a block sum-scan.  Each kept token is then read as 8-byte LDS words (no
-// byte-serial loop), its signature is mixed word-wise, and its raw-vocabulary
-// slot is found with the home slot's load issued for two tokens at once.
+// stream of 16 KiB chunks (records are ~4 KiB: a chunk-per-record walk would
+// leave most of every second chunk idle).  Per chunk:
+//   1. coalesced 16-byte loads into LDS (+1 KiB lookahead), the overlapping
+//      records' spans into LDS;
+//   2. byte classes of every lane's 64 bytes from a 1 KiB LDS class table (one
+//      ds_read_b32 + one v_lshl_or per byte builds the split and span-starter
+//      bit masks together), span coverage by a block max-scan, token ranks by a
+//      block sum-scan, each lane's token-end mask into LDS;
+//   3. the chunk's token start positions listed in LDS by rank, then dealt
+//      round-robin to the 256 lanes (no lane idles behind a lane with more
+//      tokens): token end from the end masks, 16 bytes from LDS dwords by
+//      v_alignbyte, a 32-bit-multiply signature, and the raw-vocabulary home
+//      slots of two tokens loaded together;
+//   4. the raw slots stored coalesced per record.
 // Token i of record r goes to tokstream[(rs[r] >> 1) + i]; ntok[r] is written by
 // the lane holding r's last byte.
 constexpr int kTokNT = 256;
@@ -637,7 +677,7 @@ constexpr int kTokBytes = 16 * kTokWords;         // 64 bytes per lane
 constexpr int kChunk = kTokNT * kTokBytes;        // 16 KiB of text per block step
 constexpr int kStageV = kTokNT * kTokWords + 64;  // staged 16-byte words: chunk + 1 KiB lookahead
 constexpr int kRecWin = 384;  // records overlapping one chunk: fast-path records are >= kMinFastRec bytes
-constexpr int kTokBuf = 1536;  // chunk tokens staged in LDS for coalesced stores (a 16 KiB chunk holds ~1950)
+constexpr int kTokCap = 2560;  // chunk tokens per round (a c2 chunk holds ~1950; more take further rounds)
 
 // entity span end: '&' [a-z0-9#]* ';'  (TagTokenizer.onAmpersand 644-662); p if none
 template <typename B>
@@ -680,9 +720,10 @@ struct TokLds {
   int64_t tbase0;                    // tokstream offset (rs >> 1) of window record 0 (others: from rs)
   int32_t c0[kRecWin];
   int32_t rid[kRecWin];               // record index
-  uint64_t smask[kTokNT];             // split-byte mask of every lane's 64 bytes
+  uint64_t emask[kTokNT];             // token-end bytes of every lane's 64: split, outside a fast record, record start
   int32_t sc32[kTokNT / 64 + 1];
-  uint32_t tokbuf[kTokBuf];           // raw slots of chunk tokens 0 .. kTokBuf-1
+  uint32_t cls[256];                  // byte class: bit 0 split byte, bit 16 span starter ('<' or '&')
+  uint32_t tl[kTokCap];               // round's chunk tokens by rank: start position, then raw slot
 };
 
 // byte at chunk-relative position p (stage, or global beyond the lookahead)
@@ -727,15 +768,69 @@ __device__ __forceinline__ int first_split16(uint64_t lo, uint64_t hi, int k) {
 
 // signature of the token starting at chunk-relative x (its first byte is a word
 // char); e bounds it (the record end).  Long tokens continue byte-wise.
-__device__ __noinline__ TokSig tok_sig_long(const uint8_t *stg, const uint8_t *t, int64_t c_lo, int32_t x, int32_t e,
-                                            int32_t *len_o) {
+struct TokSigLen {
+  uint64_t h, w0, w1;
+  int32_t len;
+};
+__device__ __noinline__ TokSigLen tok_sig_long(const uint8_t *stg, const uint8_t *t, int64_t c_lo, int32_t x,
+                                               int32_t e) {
   int32_t y = x;
   while (y < e && !is_split_byte(tok_byte(stg, t, c_lo, y))) y++;
-  *len_o = y - x;
-  return sig_bytes(t + c_lo + x, y - x);
+  const TokSig g = sig_bytes(t + c_lo + x, y - x);
+  return TokSigLen{g.h, g.w0, g.w1, y - x};
 }
 
-__global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n,
+// Signature and length of the token starting at chunk-relative x.  The end is
+// the first token-end byte after x in this lane's or the next lane's mask;
+// tokens running further (> 16 bytes, or past the chunk) take the byte path.
+__device__ __forceinline__ void tok_sig_at(const TokLds &L, const uint8_t *t, int64_t c_lo, int32_t x, TokSig *g,
+                                           int32_t *len_o) {
+  const int ln = x >> 6, bi = x & 63;
+  const uint64_t rest = L.emask[ln] >> bi >> 1;  // bytes x+1 .. end of lane
+  int32_t len = 99;
+  if (rest) {
+    len = __ffsll((unsigned long long)rest);
+  } else if (ln + 1 < kTokNT) {
+    const uint64_t m = L.emask[ln + 1];
+    if (m) len = 64 - bi + __ffsll((unsigned long long)m) - 1;
+  }
+  if (len <= 16) {
+    const uint32_t *st32 = reinterpret_cast<const uint32_t *>(L.st4);
+    const int a = x >> 2, r = x & 3;
+    const uint32_t d0 = st32[a], d1 = st32[a + 1], d2 = st32[a + 2], d3 = st32[a + 3], d4 = st32[a + 4];
+    const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, r) |
+                        ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32);
+    const uint64_t hi = (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, r) |
+                        ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, r) << 32);
+    g->w0 = len >= 8 ? lo : (lo & ((1ull << (8 * len)) - 1ull));
+    g->w1 = len <= 8 ? 0ull : (len >= 16 ? hi : (hi & ((1ull << (8 * (len - 8))) - 1ull)));
+    g->h = sig_head(g->w0, g->w1);
+  } else {
+    // record end bounds the byte walk
+    int lo_k = 0, hi_k = kRecWin;
+    while (lo_k < hi_k) {
+      const int m = (lo_k + hi_k) >> 1;
+      if (L.rs[m] <= x)
+        lo_k = m + 1;
+      else
+        hi_k = m;
+    }
+    const int32_t e = L.re[lo_k > 0 ? lo_k - 1 : 0];
+    const TokSigLen s = tok_sig_long(reinterpret_cast<const uint8_t *>(L.st4), t, c_lo, x, e);
+    g->h = s.h;
+    g->w0 = s.w0;
+    g->w1 = s.w1;
+    len = s.len;
+  }
+  *len_o = len;
+}
+
+__device__ __forceinline__ bool slot_hit(const SlotVal &v, const TokSig &g, int32_t len) {
+  return len <= 16 && v.key == g.h && v.rep != 0 && (v.rep & 0xFFFFFFull) == (uint64_t)len && v.w0 == g.w0 &&
+         v.w1 == g.w1;
+}
+
+__global__ __launch_bounds__(kTokNT, 4) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n,
                                                      const uint64_t *__restrict__ rs_g,
                                                      const uint64_t *__restrict__ re_g,
                                                      const int32_t *__restrict__ frec, int64_t nF, int64_t rpb,
@@ -750,8 +845,8 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
   const uint4 *a4 = reinterpret_cast<const uint4 *>(t - mis);
   const int64_t nq = n + mis;
   const uint8_t *stg = reinterpret_cast<const uint8_t *>(L.st4);
-  const uint64_t *st8 = reinterpret_cast<const uint64_t *>(L.st4);
   const int tid = threadIdx.x;
+  L.cls[tid] = (is_split_byte((uint32_t)tid) ? 1u : 0u) | ((tid == '<' || tid == '&') ? 0x10000u : 0u);
   const int64_t end_all = (int64_t)re_g[frec[f1 - 1]];
   int64_t fcur = f0;        // first fast record not wholly before the current chunk
   int64_t mask_carry = -1;  // absolute end of the furthest span begun in earlier chunks
@@ -793,40 +888,49 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
     const int32_t mc = (int32_t)max<int64_t>(min<int64_t>(mask_carry - c_lo, kFar), -1);
     // pass 1: byte classes of this lane's 64 bytes as bit masks (bit i = byte p0 + i)
     uint64_t S = 0, SPN = 0;  // split bytes; '<' / '&' bytes (span starters)
-#pragma unroll 1
+#pragma unroll
     for (int w = 0; w < kTokWords; w++) {
-      const uint64_t wlo = st8[2 * (kTokWords * tid + w)], whi = st8[2 * (kTokWords * tid + w) + 1];
-      uint32_t s16 = 0, x16 = 0;
+      const uint4 q = L.st4[kTokWords * tid + w];
+      uint32_t acc = 0;  // bits 0-15 split, 16-31 span starter
 #pragma unroll
       for (int i = 0; i < 16; i++) {
-        const uint32_t b = (uint32_t)((i < 8 ? wlo >> (8 * i) : whi >> (8 * (i - 8))) & 0xFF);
-        s16 |= (uint32_t)is_split_byte(b) << i;
-        x16 |= (uint32_t)(b == '<' || b == '&') << i;
+        const uint32_t dw = i < 4 ? q.x : (i < 8 ? q.y : (i < 12 ? q.z : q.w));
+        acc |= L.cls[(dw >> (8 * (i & 3))) & 0xFFu] << i;
       }
-      S |= (uint64_t)s16 << (16 * w);
-      SPN |= (uint64_t)x16 << (16 * w);
+      S |= (uint64_t)(acc & 0xFFFFu) << (16 * w);
+      SPN |= (uint64_t)(acc >> 16) << (16 * w);
     }
-    L.smask[tid] = S;
     // bytes inside a (fast-path) record: all of them unless a record boundary
-    // falls in this lane
-    uint64_t IN;
+    // falls in this lane; record-start bytes end a token too
+    uint64_t IN, RS = 0;
     const bool whole = j >= 0 && L.re[j] >= p0 + kTokBytes;
     if (whole) {
       IN = ~0ull;
+      RS = L.rs[j] == p0 ? 1ull : 0ull;
     } else {
       IN = 0;
-      int jj = j;
-      for (int i = 0; i < kTokBytes; i++) {
-        const int32_t p = p0 + i;
-        while (jj + 1 < kRecWin && L.rs[jj + 1] <= p) jj++;
-        if (jj >= 0 && p < L.re[jj]) IN |= 1ull << i;
+      for (int k = j < 0 ? 0 : j; k < kRecWin && L.rs[k] < p0 + kTokBytes; k++) {
+        const int32_t a = max(L.rs[k] - p0, 0), b = min(L.re[k] - p0, kTokBytes);
+        if (b > a) IN |= (b >= 64 ? ~0ull : ((1ull << b) - 1ull)) & ~((1ull << a) - 1ull);
+        if (L.rs[k] >= p0) RS |= 1ull << (L.rs[k] - p0);
       }
     }
+    L.emask[tid] = S | ~IN | RS;
     const uint64_t prev_split = is_split_byte(tid > 0 ? stg[p0 - 1] : prev_chunk_byte) ? 1ull : 0ull;
     uint64_t cand = IN & ~S & ((S << 1) | prev_split);
     int32_t lane_max = -1;
     uint64_t sp = SPN & IN;
     if (sp) {  // rare: markup / entities in this lane
+      // '>' bytes of the lane: a '<' followed by neither '!' nor '?' spans to the
+      // first '>' after it (lt_span_end), found here from the mask when it lies
+      // in this lane and before the record end
+      uint64_t GT = 0;
+#pragma unroll
+      for (int w = 0; w < kTokWords * 4; w++) {
+        const uint32_t d = reinterpret_cast<const uint32_t *>(L.st4)[kTokWords * 4 * tid + w] ^ 0x3E3E3E3Eu;
+        const uint32_t z = ~(((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;  // 0x80 where byte == '>'
+        GT |= (uint64_t)(((z >> 7) * 0x10204080u) >> 28) << (4 * w);
+      }
       int jj = j;
       while (sp) {
         const int i = __ffsll((unsigned long long)sp) - 1;
@@ -834,13 +938,20 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
         const int32_t p = p0 + i;
         while (jj + 1 < kRecWin && L.rs[jj + 1] <= p) jj++;
         const int32_t e = L.re[jj];
-        const int32_t q = stg[p] == '<' ? lt_span_rel(stg, t, c_lo, e, p) : amp_span_rel(stg, t, c_lo, e, p);
+        int32_t q;
+        const uint8_t c1 = i < kTokBytes - 1 ? stg[p + 1] : 0;
+        const uint64_t gt_after = i < 63 ? (GT >> i >> 1) : 0ull;
+        if (stg[p] == '<' && i < kTokBytes - 1 && c1 != '!' && c1 != '?' && gt_after &&
+            p + __ffsll((unsigned long long)gt_after) < e)
+          q = p + __ffsll((unsigned long long)gt_after);
+        else
+          q = stg[p] == '<' ? lt_span_rel(stg, t, c_lo, e, p) : amp_span_rel(stg, t, c_lo, e, p);
         lane_max = q > lane_max ? q : lane_max;
         // tokens may not start inside the span (p, q]
         const int32_t hi_bit = q - p0;
         if (hi_bit > i) {
           const uint64_t upto = hi_bit >= 63 ? ~0ull : ((1ull << (hi_bit + 1)) - 1ull);
-          cand &= ~(upto & ~((1ull << (i + 1)) - 1ull));
+          cand &= ~(upto & (i >= 63 ? 0ull : (~0ull << (i + 1))));  // bits (i, hi_bit]; no shift by 64
         }
       }
     }
@@ -858,58 +969,6 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
       if (L.rs[k] >= p0) L.c0[k] = base + __popcll(keep_all & ((1ull << (L.rs[k] - p0)) - 1ull));
     __syncthreads();
     const int32_t carry0 = L.rs[0] < 0 ? tok_carry : 0;  // window record 0 began in an earlier chunk
-    // pass 2: signature + raw-vocabulary slot of every kept token
-    uint64_t keep = keep_all;
-    int32_t idx = base;
-    int jt = j < 0 ? 0 : j;
-    while (keep) {
-      const int i0 = __ffsll((unsigned long long)keep) - 1;
-      keep &= keep - 1;
-      const int32_t x = p0 + i0;
-      while (jt + 1 < kRecWin && L.rs[jt + 1] <= x) jt++;
-      const int32_t e = L.re[jt];
-      TokSig g;
-      int32_t len;
-      if (x + 24 <= kStageV * 16) {
-        // token end: first split byte after x, from this lane's or the next lane's mask
-        const uint64_t rest = S >> i0 >> 1;  // bytes x+1 .. p0+63
-        if (rest) {
-          len = __ffsll((unsigned long long)rest);
-        } else if (tid + 1 < kTokNT && L.smask[tid + 1]) {
-          len = (kTokBytes - i0) + __ffsll((unsigned long long)L.smask[tid + 1]) - 1;
-        } else {
-          len = 16;  // long, or running past the chunk: handled below
-        }
-        const int a = x >> 3, sh = (x & 7) * 8;
-        const uint64_t u0 = st8[a], u1 = st8[a + 1], u2 = st8[a + 2];
-        const uint64_t lo = sh ? (u0 >> sh) | (u1 << (64 - sh)) : u0;
-        const uint64_t hi = sh ? (u1 >> sh) | (u2 << (64 - sh)) : u1;
-        if (len >= 16) len = first_split16(lo, hi, 1);
-        if (len > e - x) len = e - x;
-        if (len < 16) {
-          g.w0 = len >= 8 ? lo : (lo & ((1ull << (8 * len)) - 1));
-          g.w1 = len <= 8 ? 0 : (hi & ((1ull << (8 * (len - 8))) - 1));
-          g.h = sig_fin(sig_head((uint64_t)len, g.w0, g.w1));
-        } else {
-          g = tok_sig_long(stg, t, c_lo, x, e, &len);
-        }
-      } else {
-        g = tok_sig_long(stg, t, c_lo, x, e, &len);
-      }
-      const SlotVal v = ld_slot_plain(&tb.slots[g.h & tb.mask]);
-      // a hit at the home slot (the common case) is decided inline
-      const bool hit = len <= 16 && v.key == g.h && v.rep != 0 && (v.rep & 0xFFFFFFull) == (uint64_t)len &&
-                       v.w0 == g.w0 && v.w1 == g.w1;
-      const uint32_t slot = hit ? (uint32_t)(g.h & tb.mask) : raw_insert(tb, g, (uint64_t)(c_lo + x), (uint64_t)len, v);
-      if (idx < kTokBuf) {
-        L.tokbuf[idx] = slot;  // stored coalesced after the chunk
-      } else {
-        const int32_t r0k = jt == 0 ? L.c0[0] - carry0 : L.c0[jt];
-        const int64_t tb = jt == 0 ? L.tbase0 : ((c_lo + L.rs[jt]) >> 1);
-        tokstream[tb + (idx - r0k)] = slot;
-      }
-      idx++;
-    }
     // ntok of every record whose last byte is in this lane (no token starts at its '>')
     for (int k = (j < 0 ? 0 : j); k < kRecWin && L.rs[k] < p0 + kTokBytes; k++) {
       const int32_t last = L.re[k] - 1;
@@ -931,43 +990,82 @@ __global__ __launch_bounds__(kTokNT, 5) void k_tok_fast(const uint8_t *__restric
     }
     if (blk_max >= 0) mask_carry = max<int64_t>(mask_carry, c_lo + blk_max);
     prev_chunk_byte = stg[kChunk - 1];
-    __syncthreads();
-    // coalesced stores of the staged tokens: chunk token i belongs to the last
-    // window record whose first chunk token is <= i (records without tokens
-    // share that rank with their successor, so they are skipped)
+    int nk;  // window records starting before the chunk end
     {
-      const int nbuf = blk_cnt < kTokBuf ? blk_cnt : kTokBuf;
-      int nk;  // window records starting before the chunk end
-      {
-        int lo = 0, hi = kRecWin;
-        while (lo < hi) {
-          const int m = (lo + hi) >> 1;
-          if (L.rs[m] < kChunk) lo = m + 1;
-          else hi = m;
-        }
-        nk = lo;
+      int lo = 0, hi = kRecWin;
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (L.rs[m] < kChunk) lo = m + 1;
+        else hi = m;
       }
-      auto fr = [&](int k) { return (k == 0 && L.rs[0] < 0) ? 0 : L.c0[k]; };
-      int k = 0;
-      if (tid < nbuf) {
-        int lo = 0, hi = nk;  // last k with fr(k) <= tid
-        while (hi - lo > 1) {
-          const int m = (lo + hi) >> 1;
-          if (fr(m) <= tid) lo = m;
-          else hi = m;
-        }
-        k = lo;
-      }
-      for (int i = tid; i < nbuf; i += kTokNT) {
-        while (k + 1 < nk && fr(k + 1) <= i) k++;
-        const int32_t r0k = k == 0 ? L.c0[0] - carry0 : L.c0[k];
-        const int64_t tb = k == 0 ? L.tbase0 : ((c_lo + L.rs[k]) >> 1);
-        tokstream[tb + (i - r0k)] = L.tokbuf[i];
-      }
+      nk = lo;
     }
+    auto fr = [&](int k) { return (k == 0 && L.rs[0] < 0) ? 0 : L.c0[k]; };
+    for (int32_t rlo = 0; rlo < blk_cnt; rlo += kTokCap) {
+      const int32_t nr = min(kTokCap, blk_cnt - rlo);
+      // pass 2: start positions of the round's tokens by chunk rank
+      {
+        uint64_t keep = keep_all;
+        int32_t idx = base - rlo;
+        if (idx < nr && idx + __popcll(keep) > 0) {
+          while (keep) {
+            const int i0 = __ffsll((unsigned long long)keep) - 1;
+            keep &= keep - 1;
+            if (idx >= 0 && idx < nr) L.tl[idx] = (uint32_t)(p0 + i0);
+            idx++;
+          }
+        }
+      }
+      __syncthreads();
+      // pass 3: signature + raw-vocabulary slot, two tokens per lane step
+      for (int32_t r = tid; r < nr; r += 2 * kTokNT) {
+        const int32_t r2 = r + kTokNT;
+        const bool two = r2 < nr;
+        const int32_t xa = (int32_t)L.tl[r], xb = two ? (int32_t)L.tl[r2] : xa;
+        TokSig ga, gb;
+        int32_t la, lb;
+        tok_sig_at(L, t, c_lo, xa, &ga, &la);
+        tok_sig_at(L, t, c_lo, xb, &gb, &lb);
+        const SlotVal va = ld_slot_plain(&tb.slots[ga.h & tb.mask]);
+        const SlotVal vb = ld_slot_plain(&tb.slots[gb.h & tb.mask]);
+        const uint32_t sa =
+            slot_hit(va, ga, la) ? (uint32_t)(ga.h & tb.mask) : raw_insert(tb, ga, (uint64_t)(c_lo + xa), (uint64_t)la, va);
+        L.tl[r] = sa;
+        if (two) {
+          const uint32_t sb = slot_hit(vb, gb, lb) ? (uint32_t)(gb.h & tb.mask)
+                                                   : raw_insert(tb, gb, (uint64_t)(c_lo + xb), (uint64_t)lb, vb);
+          L.tl[r2] = sb;
+        }
+      }
+      __syncthreads();
+      // pass 4: coalesced stores: chunk token i belongs to the last window record
+      // whose first chunk token is <= i (records without tokens share that rank
+      // with their successor, so they are skipped)
+      {
+        const int32_t i0 = rlo + tid;
+        int k = 0;
+        if (i0 < rlo + nr) {
+          int lo = 0, hi = nk;  // last k with fr(k) <= i0
+          while (hi - lo > 1) {
+            const int m = (lo + hi) >> 1;
+            if (fr(m) <= i0) lo = m;
+            else hi = m;
+          }
+          k = lo;
+        }
+        for (int32_t i = i0; i < rlo + nr; i += kTokNT) {
+          while (k + 1 < nk && fr(k + 1) <= i) k++;
+          const int32_t r0k = k == 0 ? L.c0[0] - carry0 : L.c0[k];
+          const int64_t tbse = k == 0 ? L.tbase0 : ((c_lo + L.rs[k]) >> 1);
+          tokstream[tbse + (i - r0k)] = L.tl[i - rlo];
+        }
+      }
+      if (rlo + kTokCap < blk_cnt) __syncthreads();  // the next round rewrites tl
+    }
+    __syncthreads();  // LDS is overwritten by the next chunk (s_adv / sc32[0] are rewritten only after
+                      // the next chunk's staging barrier)
     fcur += s_adv;
     tok_carry = L.sc32[0];
-    __syncthreads();  // LDS is overwritten by the next chunk
   }
 }
 
