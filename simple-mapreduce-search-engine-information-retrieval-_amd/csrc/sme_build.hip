@@ -1480,6 +1480,16 @@ struct AggIn {
   int64_t dmin = 0;
   uint32_t F = 0;
   unsigned int *max_tf = nullptr;  // count pass: largest tf of any pair (atomicMax)
+  // single-pass form (reg_off != nullptr): record i's pairs go to the start of its
+  // region [reg_off[i], reg_off[i + 1]) (sized by its token count times max_nout,
+  // an upper bound of its distinct terms) and their number to dcnt[i]; the term
+  // sort's first pass reads pair x of the docno order from the region of the
+  // record holding it (exclusive scan of dcnt), so no count pass and no
+  // compaction.  Big records are listed for k_agg_big.
+  const int64_t *reg_off = nullptr;
+  int64_t *dcnt = nullptr;
+  int64_t *big_out = nullptr;
+  unsigned long long *nbig = nullptr;
 };
 
 // Aggregate record r into table (keys/cnt, capacity mask). Returns distinct count or -1 on overflow.
@@ -1589,9 +1599,10 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
   int32_t *keys = keys_all[wv], *cnt = cnt_all[wv];
   int32_t *distinct = &dist_all[wv];
   const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
-  uint32_t wmax = 0;  // count pass: largest tf over this wave's records
+  uint32_t wmax = 0;  // count pass / single pass: largest tf over this wave's records
+  const bool fused = EMIT && in.reg_off != nullptr;
   for (int64_t i = (int64_t)blockIdx.x * (kAggNT / 64) + wv; i < nR; i += nwaves) {
-    if (EMIT && prec[i] < 0) continue;  // big record: block path
+    if (EMIT && !fused && prec[i] < 0) continue;  // big record: block path
     const int64_t r = in.perm[i];
 #pragma unroll
     for (int k = 0; k < kWCap / 64; k++) {
@@ -1625,7 +1636,12 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
       wave_sync_lds();
       continue;
     }
-    int64_t base = pair_off[i];
+    if (fused && big) {
+      if (lane == 0) in.big_out[atomicAdd(in.nbig, 1ull)] = i;
+      wave_sync_lds();
+      continue;
+    }
+    int64_t base = fused ? in.reg_off[i] : pair_off[i];
     const uint64_t dn = (uint64_t)(uint32_t)in.docno[r] << 32;
 #pragma unroll 4
     for (int k = 0; k < kWCap / 64; k++) {
@@ -1633,15 +1649,22 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
       const uint64_t m = __ballot(key >= 0);
       if (key >= 0) {
         const int64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
+        const int32_t c = cnt[k * 64 + lane];
         p_term[o] = (uint32_t)key;
         if (in.v32)
-          in.v32[o] = (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + cnt[k * 64 + lane]);
+          in.v32[o] = (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c);
         else
-          p_val[o] = dn | (uint32_t)cnt[k * 64 + lane];
+          p_val[o] = dn | (uint32_t)c;
+        if (fused) wmax = max(wmax, (uint32_t)c);
       }
       base += __popcll(m);
     }
+    if (fused && lane == 0) in.dcnt[i] = d;
     wave_sync_lds();
+  }
+  if (fused) {
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
+    if (lane == 0 && wmax) atomicMax(in.max_tf, wmax);
   }
   if (!EMIT && in.max_tf) {
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
@@ -1673,8 +1696,15 @@ __global__ __launch_bounds__(kAggNT) void k_agg_big(AggIn in, const int64_t *big
       __syncthreads();
       continue;
     }
-    // emit: chunked compaction over the table
+    // emit: chunked compaction over the table (pass 2: into the record's region,
+    // whose rest gets gap keys; pair count and largest tf to the counters)
     int64_t base = pair_off[i];
+    if (pass == 2 && in.max_tf) {
+      uint32_t m = 0;
+      for (uint32_t k = threadIdx.x; k < cap; k += kAggNT) m = max(m, keys[k] >= 0 ? (uint32_t)cnt[k] : 0u);
+      for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+      if ((threadIdx.x & 63) == 0 && m) atomicMax(in.max_tf, m);
+    }
     for (uint32_t c0 = 0; c0 < cap; c0 += kAggNT) {
       uint32_t k = c0 + threadIdx.x;
       int32_t key = k < cap ? keys[k] : -1;
@@ -1689,6 +1719,7 @@ __global__ __launch_bounds__(kAggNT) void k_agg_big(AggIn in, const int64_t *big
       }
       base += tot;
     }
+    if (pass == 2 && threadIdx.x == 0) in.dcnt[i] = base - pair_off[i];
     __syncthreads();
   }
 }
@@ -1843,6 +1874,21 @@ __global__ void k_long_lens(const int64_t *list, int64_t n, const int32_t *rlist
 __global__ void k_big_list(const int32_t *prec, int64_t n, int64_t *list, unsigned long long *cnt) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     if (prec[i] < 0) list[atomicAdd(cnt, 1ull)] = i;
+}
+// single-pass aggregation: region of record i (docno order) = ntok * max_nout,
+// which bounds both its distinct terms and any of its tf (the largest region
+// bounds tf for the packed values)
+__global__ void k_agg_regions(const int64_t *perm, const int32_t *ntok, int64_t nR, const int32_t *max_nout,
+                              int64_t *reg, unsigned long long *mx) {
+  unsigned long long m = 0;
+  const int64_t mn = max(*max_nout, 1);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nR; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = (int64_t)ntok[perm[i]] * mn;
+    reg[i] = c;
+    m = max(m, (unsigned long long)c);
+  }
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
 }
 __global__ void k_big_caps(const int64_t *list, int64_t nbig, const int64_t *perm, const int32_t *ntok,
                            const int32_t *max_nout, int64_t *caps) {
@@ -2286,7 +2332,8 @@ enum {
   W_S, W_E, W_C, W_CNT, W_EOF, W_NEXTS, W_RS, W_RE, W_DOCNO, W_SLOW, W_SLOWLIST, W_SCROFF, W_U16, W_BOFF,
   W_TOK, W_NTOK, W_RKEYS, W_RREPS, W_POOL, W_CKEY, W_CSTR, W_NOUT, W_LONG, W_FKEYS, W_FREPS, W_CFINAL,
   W_VSLOT, W_KHI, W_KLO, W_VIDX, W_T0, W_T1, W_T2, W_T3, W_RAWTERM, W_MULTI, W_PERM, W_PREC, W_PTERM, W_PVAL,
-  W_MAXNOUT, W_SS, W_SE, W_SC, W_RLIST, W_RFLAG, W_POFF, W_OVFKEY, W_FREC, W_LT, W_RADIX,
+  W_MAXNOUT, W_SS, W_SE, W_SC, W_RLIST, W_RFLAG, W_POFF, W_OVFKEY, W_FREC, W_LT, W_RADIX, W_NTOK2, W_BIGL2,
+  W_BIGCAP, W_SEGB,
   W_NSLOTS
 };
 constexpr int kBuildWs = 64;  // build slots live at ctx->ws[64..127]
@@ -2751,7 +2798,74 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     hipLaunchKernelGGL(k_docno_range, dim3(grid_for(nR, 256, 1024)), dim3(256), 0, st, docno, nR, dmn, dmx);
     ai.max_tf = mtf;
   }
-  if (K == 1) {
+  bool fused = false;
+  // single pass: the term sort's first pass reads pair x from the region of its record
+  const int64_t *sort_reg = nullptr, *sort_xoff = nullptr;
+  int64_t sort_nrec = 0;
+  if (K == 1 && want_packed && !getenv("SME_AGG2")) {
+    // single-pass aggregation: record regions sized by ntok * max_nout
+    int64_t *reg = W[W_T2].as<int64_t>(nR + 1), *reg_off = W[W_SEGB].as<int64_t>(nR + 1);
+    SME_HIP(hipMemsetAsync(cnt + 24, 0, 4 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_agg_regions, dim3(grid_for(nR, 256, 1024)), dim3(256), 0, st, perm, ntok, nR, max_nout, reg,
+                       cnt + 24);
+    SME_HIP(hipMemsetAsync(reg + nR, 0, sizeof(int64_t), st));
+    size_t tbb = 0;
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, reg, reg_off, (int)nR + 1, st));
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, reg, reg_off, (int)nR + 1, st));
+    int64_t Pb = 0;
+    unsigned long long h_rmx = 0;
+    SME_HIP(hipMemcpyAsync(&Pb, reg_off + nR, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipMemcpyAsync(&h_rmx, cnt + 24, sizeof h_rmx, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipMemcpyAsync(h_drange, dmn, sizeof h_drange, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    const int32_t tbits0 = bits_for((uint64_t)std::max<int64_t>(Vi, 1));
+    const uint64_t Fq = h_rmx + 1, D = (uint64_t)((int64_t)h_drange[1] - h_drange[0] + 1);
+    if (Pb > 0 && Pb < (1ll << 32) && D * Fq < (1ull << 32) && tbits0 + bits_for(Fq - 1) <= 32) {
+      fused = true;
+      p_term = W[W_PTERM].as<uint32_t>(Pb + 1);
+      ai.v32 = W[W_PVAL].as<uint32_t>(Pb + 1);
+      ai.dmin = h_drange[0];
+      ai.F = (uint32_t)Fq;
+      ai.reg_off = reg_off;
+      ai.dcnt = W[W_T3].as<int64_t>(nR + 1);
+      ai.nbig = cnt + 26;
+      ai.big_out = W[W_SLOWLIST].as<int64_t>(nR + 1);
+      SME_HIP(hipMemsetAsync(mtf, 0, sizeof(unsigned int), st));
+      const unsigned agg_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
+      hipLaunchKernelGGL(k_agg_w<true>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, nullptr, nullptr, p_term,
+                         nullptr);
+      SME_CHECK_LAUNCH();
+      const int64_t nbig = (int64_t)d2h(cnt + 26, st);
+      if (nbig > 0) {
+        int64_t *bl2 = W[W_BIGL2].as<int64_t>(nbig);
+        SME_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tbb, ai.big_out, bl2, (int)nbig, 0, 64, st));
+        SME_HIP(hipcub::DeviceRadixSort::SortKeys(cub_tmp(tbb), tbb, ai.big_out, bl2, (int)nbig, 0, 64, st));
+        int64_t *bcap = W[W_BIGCAP].as<int64_t>(nbig + 1), *boff = W[W_RLIST].as<int64_t>(nbig + 1);
+        hipLaunchKernelGGL(k_big_caps, dim3(grid_for(nbig)), dim3(256), 0, st, bl2, nbig, perm, ntok, max_nout, bcap);
+        SME_HIP(hipMemsetAsync(bcap + nbig, 0, sizeof(int64_t), st));
+        SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, bcap, boff, (int)nbig + 1, st));
+        SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, bcap, boff, (int)nbig + 1, st));
+        const int64_t gtot = d2h(boff + nbig, st);
+        int32_t *gkeys = W[W_U16].as<int32_t>(gtot), *gcnt = W[W_BOFF].as<int32_t>(gtot);
+        hipLaunchKernelGGL(k_agg_big, dim3((unsigned)std::min<int64_t>(nbig, 4096)), dim3(kAggNT), 0, st, ai, bl2,
+                           nbig, boff, bcap, gkeys, gcnt, nullptr, reg_off, p_term, nullptr, 2);
+        SME_CHECK_LAUNCH();
+      }
+      // exact pair offsets of the records (docno order)
+      int64_t *xoff = W[W_NTOK2].as<int64_t>(nR + 1);
+      SME_HIP(hipMemsetAsync(ai.dcnt + nR, 0, sizeof(int64_t), st));
+      SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, ai.dcnt, xoff, (int)nR + 1, st));
+      SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, ai.dcnt, xoff, (int)nR + 1, st));
+      SME_HIP(hipMemcpyAsync(&P, xoff + nR, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      SME_HIP(hipMemcpyAsync(&h_mtf, mtf, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+      SME_HIP(hipStreamSynchronize(st));
+      ix->P = P;
+      sort_reg = reg_off;
+      sort_xoff = xoff;
+      sort_nrec = nR;
+    }
+  }
+  if (K == 1 && !fused) {
   int32_t *prec = W[W_PREC].as<int32_t>(nR + 1);
   int64_t *pair_off = W[W_T3].as<int64_t>(nR + 1);  // rank_of_slot no longer needed
   unsigned agg_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
@@ -2825,7 +2939,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
                        nbig, boff, bcap, gkeys, gcnt, bcount, pair_off, p_term, p_val, 1);
     SME_CHECK_LAUNCH();
   }
-  } else {
+  } else if (K >= 2) {
     // K >= 2: term streams, k-gram pairs per record, gram ids in TermDF order
     const int tb = bits_for((uint64_t)std::max<int64_t>(V, 1));
     if ((int64_t)K * tb > 63)
@@ -2877,7 +2991,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       ix->d_gram.get(16);
     }
     P = Pg;
-    Vi = Vg;
+      Vi = Vg;
     ix->P = P;
     dup_docno = true;  // occurrences of big records and equal docnos merge in the reducer step
   }
@@ -2927,7 +3041,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     // hand-written stable LSD radix sort by term id (sme_sort.hip); the last
     // pass unpacks (docno, tf) into the CSR arrays
     uint32_t *rscr = W[W_RADIX].as<uint32_t>(term_sort_scratch(P) / sizeof(uint32_t) + 1);
-    key_s = term_sort(p_term, v32, key_s, v32s, P, tbits, dmin, F, docno_d, tf_d, rscr, st);
+    key_s = term_sort(p_term, v32, key_s, v32s, sort_nrec, sort_reg, sort_xoff, P, tbits, dmin, F, docno_d, tf_d, rscr,
+                      st);
     off = ix->d_off.as<int64_t>(Vi + 1);
     SME_HIP(hipMemsetAsync(off, 0, (Vi + 1) * sizeof(int64_t), st));
     hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, Vi);

@@ -131,8 +131,11 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *d_text, uint64_t n, hipStream
 void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t M, int64_t V, const int64_t *term_off,
                     const uint16_t *term_chars, hipStream_t st, Prof *prof);
 // stable LSD radix sort of (term id, packed posting) pairs (sme_sort.hip)
-uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t P, int bits, int64_t dmin,
-                    uint32_t F, int32_t *docno, int32_t *tf, uint32_t *counts, hipStream_t st);
+// (reg != nullptr: the first pass reads pair x from reg[i] + x - xoff[i], record i
+// holding it -- the single-pass aggregation's layout)
+uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t nrec, const int64_t *reg,
+                    const int64_t *xoff, int64_t P, int bits, int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf,
+                    uint32_t *counts, hipStream_t st);
 size_t term_sort_scratch(int64_t P);
 void serialize_index(sme_index *ix, hipStream_t st);
 void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t st);

@@ -35,8 +35,42 @@ constexpr int kRsMaxBits = 11;
 constexpr int kRsMaxBins = 1 << kRsMaxBits;
 constexpr int kRsGroups = 256;              // tile groups of the column scan
 
+// Gather mode (first pass after the single-pass aggregation): pair x of the
+// docno order lives in the region of the record i holding it,
+// reg[i] + (x - xoff[i]) (xoff = exclusive scan of the records' pair counts);
+// crec[c] = the record holding pair 1024 c, so a wave's walk over its 1024
+// items starts there and advances a record at a time.
+struct Gather {
+  const int64_t *reg, *xoff, *crec;
+};
+__device__ __forceinline__ void gather_start(const Gather &g, int64_t x, int64_t &rec, int64_t &nx, int64_t &dl) {
+  rec = g.crec[x >> 10];
+  nx = g.xoff[rec + 1];
+  dl = g.reg[rec] - g.xoff[rec];
+}
+__device__ __forceinline__ int64_t gather_pos(const Gather &g, int64_t x, int64_t &rec, int64_t &nx, int64_t &dl) {
+  while (x >= nx) {
+    rec++;
+    nx = g.xoff[rec + 1];
+    dl = g.reg[rec] - g.xoff[rec];
+  }
+  return x + dl;
+}
+__global__ void k_rs_chunk_rec(const int64_t *__restrict__ xoff, int64_t nrec, int64_t P, int64_t *__restrict__ crec) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; (c << 10) < P; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = c << 10;
+    int64_t lo = 0, hi = nrec;  // last record i with xoff[i] <= x
+    while (hi - lo > 1) {
+      const int64_t m = (lo + hi) >> 1;
+      if (xoff[m] <= x) lo = m;
+      else hi = m;
+    }
+    crec[c] = lo;
+  }
+}
+
 __global__ __launch_bounds__(kRsNT) void k_rs_count(const uint32_t *__restrict__ key, int64_t P, int shift,
-                                                    int nbins, uint32_t *__restrict__ counts) {
+                                                    int nbins, uint32_t *__restrict__ counts, Gather g) {
   __shared__ uint32_t h[kRsMaxBins];
   const int tid = threadIdx.x;
   for (int b = tid; b < nbins; b += kRsNT) h[b] = 0;
@@ -44,7 +78,19 @@ __global__ __launch_bounds__(kRsNT) void k_rs_count(const uint32_t *__restrict__
   const int64_t t0 = (int64_t)blockIdx.x * kRsTile;
   const uint32_t mask = (uint32_t)nbins - 1u;
   const int64_t n = min((int64_t)kRsTile, P - t0);
-  if (n == kRsTile) {
+  if (g.reg != nullptr) {
+    const int lane = tid & 63;
+    const int64_t wb = t0 + (int64_t)(tid >> 6) * kRsWaveItems;
+    if (wb < P) {
+      int64_t rec, nx, dl;
+      gather_start(g, wb, rec, nx, dl);
+#pragma unroll 4
+      for (int s = 0; s < kRsIPL; s++) {
+        const int64_t x = wb + s * 64 + lane;
+        if (x < P) atomicAdd(&h[(key[gather_pos(g, x, rec, nx, dl)] >> shift) & mask], 1u);
+      }
+    }
+  } else if (n == kRsTile) {
     const uint4 *k4 = reinterpret_cast<const uint4 *>(key + t0);
 #pragma unroll
     for (int i = 0; i < kRsIPL / 4; i++) {
@@ -142,7 +188,8 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
                                                       int64_t P, int shift, int nbits,
                                                       const uint32_t *__restrict__ offs, uint32_t *__restrict__ okey,
                                                       uint32_t *__restrict__ oval, int32_t *__restrict__ odocno,
-                                                      int32_t *__restrict__ otf, int64_t dmin, uint32_t F) {
+                                                      int32_t *__restrict__ otf, int64_t dmin, uint32_t F,
+                                                      Gather g) {
   // wc: per-wave running digit counts, then each (wave, digit)'s first slot in
   // the tile sorted by digit; gd: global offset - tile slot of each digit
   __shared__ uint16_t wc[kRsWaves * kRsMaxBins];
@@ -168,12 +215,28 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
   const int wb = w * kRsWaveItems;  // this wave's items: tile slots [wb, wb + 1024)
   const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t k[kRsIPL], v[kRsIPL], pos[kRsIPL];
+  if (g.reg != nullptr) {
+    int64_t rec = 0, nx = 0, dl = 0;
+    if (wb < n) gather_start(g, t0 + wb, rec, nx, dl);
 #pragma unroll
-  for (int s = 0; s < kRsIPL; s++) {
-    const int i = wb + s * 64 + lane;
-    const bool ok = i < n;
-    k[s] = ok ? key[t0 + i] : 0u;
-    v[s] = ok ? val[t0 + i] : 0u;
+    for (int s = 0; s < kRsIPL; s++) {
+      const int i = wb + s * 64 + lane;
+      k[s] = 0u;
+      v[s] = 0u;
+      if (i < n) {
+        const int64_t p = gather_pos(g, t0 + i, rec, nx, dl);
+        k[s] = key[p];
+        v[s] = val[p];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < kRsIPL; s++) {
+      const int i = wb + s * 64 + lane;
+      const bool ok = i < n;
+      k[s] = ok ? key[t0 + i] : 0u;
+      v[s] = ok ? val[t0 + i] : 0u;
+    }
   }
   // 1. stable rank of every item among its wave's items of the same digit
 #pragma unroll
@@ -275,8 +338,9 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
 // k0/v0 hold the input; k1/v1 are a second buffer pair of the same size.  The
 // sorted keys end in k0 or k1 (returned); the values are unpacked into docno /
 // tf.  counts: ceil(P / 16384) * 2048 + 2048 * 256 u32 of scratch.
-uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t P, int bits, int64_t dmin,
-                    uint32_t F, int32_t *docno, int32_t *tf, uint32_t *counts, hipStream_t st) {
+uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t nrec, const int64_t *reg,
+                    const int64_t *xoff, int64_t P, int bits, int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf,
+                    uint32_t *counts, hipStream_t st) {
   if (P <= 0) return k0;
   if (P > 0xFFFFFFFFll) throw Error(SME_ELIMIT, "term sort of more than 2^32 pairs");
   bits = std::max(bits, 1);
@@ -284,22 +348,31 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
   const int64_t ntiles = (P + kRsTile - 1) / kRsTile;
   const int64_t tpg = (ntiles + kRsGroups - 1) / kRsGroups;
   uint32_t *gsum = counts + ntiles * kRsMaxBins;
+  Gather g0{nullptr, nullptr, nullptr};
+  if (reg != nullptr) {
+    int64_t *crec = reinterpret_cast<int64_t *>(gsum + kRsMaxBins * kRsGroups);
+    const int64_t nch = (P + 1023) >> 10;
+    hipLaunchKernelGGL(k_rs_chunk_rec, dim3((unsigned)std::min<int64_t>((nch + 255) / 256, 4096)), dim3(256), 0, st,
+                       xoff, nrec, P, crec);
+    g0 = Gather{reg, xoff, crec};
+  }
   int shift = 0;
   for (int p = 0; p < npass; p++) {
+    const Gather g = p == 0 ? g0 : Gather{nullptr, nullptr, nullptr};
     const int nb = (bits - shift + (npass - p) - 1) / (npass - p);  // near-equal digits
     const int nbins = 1 << nb;
     const bool last = p == npass - 1;
-    hipLaunchKernelGGL(k_rs_count, dim3((unsigned)ntiles), dim3(kRsNT), 0, st, k0, P, shift, nbins, counts);
+    hipLaunchKernelGGL(k_rs_count, dim3((unsigned)ntiles), dim3(kRsNT), 0, st, k0, P, shift, nbins, counts, g);
     hipLaunchKernelGGL(k_rs_colsum, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
     hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, nbins * kRsGroups);
     hipLaunchKernelGGL(k_rs_colscan, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
     const unsigned sgrid = (unsigned)(8 * ((ntiles + 7) / 8));  // see the XCD tile order in k_rs_scatter
     if (last)
       hipLaunchKernelGGL(k_rs_scatter<true>, dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, P, shift, nb, counts,
-                         k1, nullptr, docno, tf, dmin, F);
+                         k1, nullptr, docno, tf, dmin, F, g);
     else
       hipLaunchKernelGGL(k_rs_scatter<false>, dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, P, shift, nb,
-                         counts, k1, v1, nullptr, nullptr, dmin, F);
+                         counts, k1, v1, nullptr, nullptr, dmin, F, g);
     SME_CHECK_LAUNCH();
     std::swap(k0, k1);
     std::swap(v0, v1);
@@ -310,7 +383,7 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
 
 size_t term_sort_scratch(int64_t P) {
   const int64_t ntiles = (std::max<int64_t>(P, 1) + kRsTile - 1) / kRsTile;
-  return (size_t)(ntiles * kRsMaxBins + (int64_t)kRsMaxBins * kRsGroups) * sizeof(uint32_t);
+  return (size_t)(ntiles * kRsMaxBins + (int64_t)kRsMaxBins * kRsGroups) * sizeof(uint32_t) +
+         (size_t)(((std::max<int64_t>(P, 1) + 1023) >> 10) + 1) * sizeof(int64_t);
 }
-
 }  // namespace sme
