@@ -678,6 +678,13 @@ constexpr int kChunk = kTokNT * kTokBytes;        // 16 KiB of text per block st
 constexpr int kStageV = kTokNT * kTokWords + 64;  // staged 16-byte words: chunk + 1 KiB lookahead
 constexpr int kRecWin = 384;  // records overlapping one chunk: fast-path records are >= kMinFastRec bytes
 constexpr int kTokCap = 2560;  // chunk tokens per round (a c2 chunk holds ~1950; more take further rounds)
+#ifndef SME_TOKOCC
+#define SME_TOKOCC 4
+#endif
+#ifndef SME_TOKG
+#define SME_TOKG 2
+#endif
+constexpr int kTokG = SME_TOKG;  // tokens per lane step in the probe pass
 
 // entity span end: '&' [a-z0-9#]* ';'  (TagTokenizer.onAmpersand 644-662); p if none
 template <typename B>
@@ -830,12 +837,12 @@ __device__ __forceinline__ bool slot_hit(const SlotVal &v, const TokSig &g, int3
          v.w1 == g.w1;
 }
 
-__global__ __launch_bounds__(kTokNT, 4) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n,
+__global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n,
                                                      const uint64_t *__restrict__ rs_g,
                                                      const uint64_t *__restrict__ re_g,
                                                      const int32_t *__restrict__ frec, int64_t nF, int64_t rpb,
                                                      uint32_t *__restrict__ tokstream, int32_t *__restrict__ ntok,
-                                                     RawTable tb) {
+                                                     RawTable tb, int texp) {
   __shared__ TokLds L;
   __shared__ int32_t s_adv;
   const int64_t f0 = blockIdx.x * rpb;
@@ -1017,24 +1024,27 @@ __global__ __launch_bounds__(kTokNT, 4) void k_tok_fast(const uint8_t *__restric
         }
       }
       __syncthreads();
-      // pass 3: signature + raw-vocabulary slot, two tokens per lane step
-      for (int32_t r = tid; r < nr; r += 2 * kTokNT) {
-        const int32_t r2 = r + kTokNT;
-        const bool two = r2 < nr;
-        const int32_t xa = (int32_t)L.tl[r], xb = two ? (int32_t)L.tl[r2] : xa;
-        TokSig ga, gb;
-        int32_t la, lb;
-        tok_sig_at(L, t, c_lo, xa, &ga, &la);
-        tok_sig_at(L, t, c_lo, xb, &gb, &lb);
-        const SlotVal va = ld_slot_plain(&tb.slots[ga.h & tb.mask]);
-        const SlotVal vb = ld_slot_plain(&tb.slots[gb.h & tb.mask]);
-        const uint32_t sa =
-            slot_hit(va, ga, la) ? (uint32_t)(ga.h & tb.mask) : raw_insert(tb, ga, (uint64_t)(c_lo + xa), (uint64_t)la, va);
-        L.tl[r] = sa;
-        if (two) {
-          const uint32_t sb = slot_hit(vb, gb, lb) ? (uint32_t)(gb.h & tb.mask)
-                                                   : raw_insert(tb, gb, (uint64_t)(c_lo + xb), (uint64_t)lb, vb);
-          L.tl[r2] = sb;
+      // pass 3: signature + raw-vocabulary slot, kTokG tokens per lane step (their
+      // home-slot loads in flight together)
+      for (int32_t r0 = (texp & 1) ? nr : tid; r0 < nr; r0 += kTokG * kTokNT) {
+        TokSig g[kTokG];
+        int32_t len[kTokG], x[kTokG];
+        SlotVal v[kTokG];
+#pragma unroll
+        for (int u = 0; u < kTokG; u++) {
+          const int32_t r = r0 + u * kTokNT;
+          x[u] = (int32_t)L.tl[r < nr ? r : r0];
+          tok_sig_at(L, t, c_lo, x[u], &g[u], &len[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kTokG; u++) v[u] = ld_slot_plain(&tb.slots[g[u].h & tb.mask]);
+#pragma unroll
+        for (int u = 0; u < kTokG; u++) {
+          const int32_t r = r0 + u * kTokNT;
+          if (r < nr)
+            L.tl[r] = slot_hit(v[u], g[u], len[u])
+                          ? (uint32_t)(g[u].h & tb.mask)
+                          : raw_insert(tb, g[u], (uint64_t)(c_lo + x[u]), (uint64_t)len[u], v[u]);
         }
       }
       __syncthreads();
@@ -1053,7 +1063,7 @@ __global__ __launch_bounds__(kTokNT, 4) void k_tok_fast(const uint8_t *__restric
           }
           k = lo;
         }
-        for (int32_t i = i0; i < rlo + nr; i += kTokNT) {
+        for (int32_t i = (texp & 2) ? rlo + nr : i0; i < rlo + nr; i += kTokNT) {
           while (k + 1 < nk && fr(k + 1) <= i) k++;
           const int32_t r0k = k == 0 ? L.c0[0] - carry0 : L.c0[k];
           const int64_t tbse = k == 0 ? L.tbase0 : ((c_lo + L.rs[k]) >> 1);
@@ -1323,13 +1333,28 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
 __global__ void k_final_compact(const unsigned long long *fkeys, const unsigned long long *freps, uint64_t fmask,
                                 const uint64_t *cand_str, unsigned long long *nV, uint32_t *vslot, uint32_t *vidx,
                                 int32_t *maxlen) {
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s <= fmask; s += (uint64_t)gridDim.x * blockDim.x) {
-    if (fkeys[s] == 0) continue;
-    unsigned long long i = atomicAdd(nV, 1ull);
-    vslot[i] = (uint32_t)s;
-    vidx[i] = (uint32_t)i;
-    atomicMax(maxlen, (int32_t)(cand_str[freps[s] - 1] & 0xFFFF));
+  // one counter atomic per wave and step (entries compacted in any order: the
+  // term sort that follows fixes the order); the longest term by wave max
+  const int lane = threadIdx.x & 63;
+  int32_t ml = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t s0 = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); s0 <= fmask; s0 += stride) {
+    const uint64_t s = s0 + lane;
+    const bool used = s <= fmask && fkeys[s] != 0;
+    const uint64_t m = (uint64_t)__ballot(used);
+    if (m == 0) continue;
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(nV, (unsigned long long)__popcll(m));
+    b = __shfl(b, 0, 64);
+    if (used) {
+      const unsigned long long i = b + __popcll(m & ((1ull << lane) - 1ull));
+      vslot[i] = (uint32_t)s;
+      vidx[i] = (uint32_t)i;
+      ml = max(ml, (int32_t)(cand_str[freps[s] - 1] & 0xFFFF));
+    }
   }
+  for (int o = 32; o > 0; o >>= 1) ml = max(ml, __shfl_xor(ml, o, 64));
+  if (lane == 0 && ml > 0) atomicMax(maxlen, ml);
 }
 
 // key word w (units 4w..4w+3, big-endian, zero padded) of the term at each order position
@@ -2537,8 +2562,10 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
         prof.mark("tok_setup");
         const char *tg = getenv("SME_TOKGRID");
         const int64_t tgrid = std::min<int64_t>(nF, tg ? atoll(tg) : 4096), rpb = (nF + tgrid - 1) / tgrid;
+        // SME_TOKEXP (timing experiments only, wrong results): 1 no signatures / probes, 2 no token stores
+        const char *tx = getenv("SME_TOKEXP");
         hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)((nF + rpb - 1) / rpb)), dim3(kTokNT), 0, st, t, (int64_t)n, rs,
-                           re, frec, nF, rpb, tok, ntok, tb);
+                           re, frec, nF, rpb, tok, ntok, tb, tx ? atoi(tx) : 0);
         SME_CHECK_LAUNCH();
         prof.mark("tok_kernel");
       }

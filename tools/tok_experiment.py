@@ -13,7 +13,8 @@ sme = importlib.import_module(PKG)
 synth = importlib.import_module(PKG + ".synth")
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 250000
-for V in (64, 1 << 14, 1 << 20):
+VS = [int(os.environ["TOK_V"])] if os.environ.get("TOK_V") else [64, 1 << 14, 1 << 20]
+for V in VS:
     c = sme.DeviceCorpus(n, V=V, seed=42)
     ctx = sme.Context(1, 1)
     ctx.load_docno_mapping(synth.mapping_bytes(n))
