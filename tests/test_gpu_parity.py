@@ -100,6 +100,23 @@ def test_build_invalid_utf8_and_big_record(sme):
     _check_build(sme, b"".join(docs), sorted(["U%02d" % i for i in range(20)] + ["BIG"]), R=3)
 
 
+def test_build_big_records_interleaved(sme, synth):
+    """Several records with more distinct terms than the LDS table holds, between
+    ordinary ones (single-pass aggregation: their pairs are placed in their own
+    regions by the global-table path, in docno order with their neighbours)."""
+    rng = random.Random(5)
+    docs, ids = [], []
+    for i in range(40):
+        did = "R%03d" % i
+        ids.append(did)
+        if i in (3, 17, 18, 39):
+            words = ["b%04d" % rng.randrange(3000) for _ in range(2500)] + ["w%02d" % (i % 7)] * 3
+        else:
+            words = ["w%02d" % rng.randrange(60) for _ in range(rng.randint(20, 200))]
+        docs.append(b"<DOC>\n<DOCNO>" + did.encode() + b"</DOCNO>\n" + " ".join(words).encode() + b"\n</DOC>\n")
+    _check_build(sme, b"".join(docs), ids, R=3)
+
+
 def test_build_nested_doc_tags(sme):
     """A <DOC> inside a record is content (XMLRecordReader reads to the next
     </DOC>); a start tag after the last </DOC> opens no record."""
