@@ -1330,28 +1330,51 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
 }
 
 // compact occupied final slots; longest term (in units) for the LSD sort depth
-__global__ void k_final_compact(const unsigned long long *fkeys, const unsigned long long *freps, uint64_t fmask,
-                                const uint64_t *cand_str, unsigned long long *nV, uint32_t *vslot, uint32_t *vidx,
-                                int32_t *maxlen) {
-  // one counter atomic per wave and step (entries compacted in any order: the
-  // term sort that follows fixes the order); the longest term by wave max
-  const int lane = threadIdx.x & 63;
+// One counter atomic per block: block b owns the slot range [b R, (b + 1) R);
+// it counts its used slots, reserves their output range with one atomicAdd and
+// writes them (entries come out in any block order: the term sort that follows
+// fixes the order).  The longest term by block max.  (A counter atomic per wave
+// still serialised 131 k atomics on one address: 0.84 ms on c2.)
+__global__ __launch_bounds__(256) void k_final_compact(const unsigned long long *fkeys,
+                                                       const unsigned long long *freps, uint64_t fmask,
+                                                       const uint64_t *cand_str, unsigned long long *nV,
+                                                       uint32_t *vslot, uint32_t *vidx, int32_t *maxlen) {
+  __shared__ uint32_t s_w[4];
+  __shared__ unsigned long long s_base;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t n = fmask + 1, R = (n + gridDim.x - 1) / gridDim.x;
+  const uint64_t a = blockIdx.x * R, b = min(n, a + R);
+  uint32_t c = 0;
+  for (uint64_t s = a + threadIdx.x; s < b; s += 256) c += fkeys[s] != 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane == 0) s_w[w] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    s_base = tot ? atomicAdd(nV, (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+  unsigned long long base = s_base;
   int32_t ml = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t s0 = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); s0 <= fmask; s0 += stride) {
-    const uint64_t s = s0 + lane;
-    const bool used = s <= fmask && fkeys[s] != 0;
+  for (uint64_t s0 = a; s0 < b; s0 += 256) {
+    const uint64_t s = s0 + threadIdx.x;
+    const bool used = s < b && fkeys[s] != 0;
     const uint64_t m = (uint64_t)__ballot(used);
-    if (m == 0) continue;
-    unsigned long long b = 0;
-    if (lane == 0) b = atomicAdd(nV, (unsigned long long)__popcll(m));
-    b = __shfl(b, 0, 64);
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (int x = 0; x < 4; x++) {
+      before += x < w ? s_w[x] : 0u;
+      tot += s_w[x];
+    }
     if (used) {
-      const unsigned long long i = b + __popcll(m & ((1ull << lane) - 1ull));
+      const unsigned long long i = base + before + __popcll(m & ((1ull << lane) - 1ull));
       vslot[i] = (uint32_t)s;
       vidx[i] = (uint32_t)i;
       ml = max(ml, (int32_t)(cand_str[freps[s] - 1] & 0xFFFF));
     }
+    base += tot;
+    __syncthreads();
   }
   for (int o = 32; o > 0; o >>= 1) ml = max(ml, __shfl_xor(ml, o, 64));
   if (lane == 0 && ml > 0) atomicMax(maxlen, ml);
@@ -1596,20 +1619,16 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ bool aggw_insert(int32_t *keys, int32_t *cnt, int32_t term, int32_t *distinct) {
-  uint32_t h = hash32((uint32_t)term) & (kWCap - 1);
-  for (int probe = 0; probe < kWCap; probe++) {
+// insert into the record's table of cap slots (a power of two <= kWCap)
+__device__ __forceinline__ bool aggw_insert(int32_t *keys, int32_t *cnt, int32_t term, uint32_t cap) {
+  uint32_t h = hash32((uint32_t)term) & (cap - 1);
+  for (uint32_t probe = 0; probe < cap; probe++) {
     const int32_t old = atomicCAS(&keys[h], -1, term);
-    if (old == -1) {
-      atomicAdd(distinct, 1);
+    if (old == -1 || old == term) {
       atomicAdd(&cnt[h], 1);
       return true;
     }
-    if (old == term) {
-      atomicAdd(&cnt[h], 1);
-      return true;
-    }
-    h = (h + 1) & (kWCap - 1);
+    h = (h + 1) & (cap - 1);
   }
   return false;
 }
@@ -1619,44 +1638,46 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
                                                   uint32_t *p_term, uint64_t *p_val) {
   __shared__ int32_t keys_all[kAggNT / 64][kWCap];
   __shared__ int32_t cnt_all[kAggNT / 64][kWCap];
-  __shared__ int32_t dist_all[kAggNT / 64];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int32_t *keys = keys_all[wv], *cnt = cnt_all[wv];
-  int32_t *distinct = &dist_all[wv];
   const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
   uint32_t wmax = 0;  // count pass / single pass: largest tf over this wave's records
   const bool fused = EMIT && in.reg_off != nullptr;
   for (int64_t i = (int64_t)blockIdx.x * (kAggNT / 64) + wv; i < nR; i += nwaves) {
     if (EMIT && !fused && prec[i] < 0) continue;  // big record: block path
     const int64_t r = in.perm[i];
-#pragma unroll
-    for (int k = 0; k < kWCap / 64; k++) {
-      keys[k * 64 + lane] = -1;
-      cnt[k * 64 + lane] = 0;
-    }
-    if (lane == 0) *distinct = 0;
-    wave_sync_lds();
     const uint32_t *ts = in.tokstream + (in.rs[r] >> 1);
     const int32_t nt = in.ntok[r];
+    // table of cap slots: 2 x the token count (load <= 1/2 when every token has
+    // one term), so short records clear and scan little; a record whose terms do
+    // not fit goes to the big-record path
+    uint32_t cap = 64;
+    while (cap < kWCap && (int64_t)cap < 2 * (int64_t)nt) cap <<= 1;
+    for (uint32_t k = lane; k < cap; k += 64) {
+      keys[k] = -1;
+      cnt[k] = 0;
+    }
+    wave_sync_lds();
     bool ok = true;
     for (int32_t t = lane; t < nt; t += 64) {
       const uint32_t slot = ts[t];
       const int32_t rt = in.raw_term[slot];
       if (rt >= 0) {
-        ok &= aggw_insert(keys, cnt, rt, distinct);
+        ok &= aggw_insert(keys, cnt, rt, cap);
       } else if (rt <= -2) {
         const int32_t m0 = -rt - 2, mn = in.raw_nout[slot];
-        for (int32_t m = 0; m < mn; m++) ok &= aggw_insert(keys, cnt, in.multi_term[m0 + m], distinct);
+        for (int32_t m = 0; m < mn; m++) ok &= aggw_insert(keys, cnt, in.multi_term[m0 + m], cap);
       }
     }
     wave_sync_lds();
-    const int32_t d = *distinct;
+    int32_t d = 0;
+    for (uint32_t k = 0; k < cap; k += 64) d += __popcll((uint64_t)__ballot(keys[k + lane] >= 0));
     const bool big = __any(!ok) || d > kWLimit;
     if (!EMIT) {
       if (lane == 0) prec[i] = big ? -1 : d;
       if (!big && in.max_tf) {
 #pragma unroll 4
-        for (int k = 0; k < kWCap / 64; k++) wmax = max(wmax, (uint32_t)cnt[k * 64 + lane]);
+        for (uint32_t k = 0; k < cap; k += 64) wmax = max(wmax, (uint32_t)cnt[k + lane]);
       }
       wave_sync_lds();
       continue;
@@ -1668,13 +1689,12 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
     }
     int64_t base = fused ? in.reg_off[i] : pair_off[i];
     const uint64_t dn = (uint64_t)(uint32_t)in.docno[r] << 32;
-#pragma unroll 4
-    for (int k = 0; k < kWCap / 64; k++) {
-      const int32_t key = keys[k * 64 + lane];
+    for (uint32_t k = 0; k < cap; k += 64) {
+      const int32_t key = keys[k + lane];
       const uint64_t m = __ballot(key >= 0);
       if (key >= 0) {
         const int64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
-        const int32_t c = cnt[k * 64 + lane];
+        const int32_t c = cnt[k + lane];
         p_term[o] = (uint32_t)key;
         if (in.v32)
           in.v32[o] = (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c);
