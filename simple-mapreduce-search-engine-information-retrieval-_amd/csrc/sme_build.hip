@@ -405,30 +405,73 @@ __global__ void k_map_hash(const uint16_t *mchars, const int64_t *moff, int64_t 
   }
 }
 
-__global__ void k_docno(const uint8_t *t, const uint64_t *rs, const uint64_t *re, int64_t nR,
-                        const uint16_t *mchars, const int64_t *moff, int64_t mn, const uint32_t *mslots,
-                        uint64_t mmask, int32_t *docno, unsigned long long *err) {
+// One thread per record.  The record's first kDocWin bytes are staged into a
+// private LDS window with six independent 16-byte loads, and <DOCNO>..</DOCNO>
+// is located and the docid hashed from there (one load latency instead of a
+// dependent byte walk through global memory); a docid not inside the window
+// takes the byte walk over the text (docid_span).
+constexpr int kDocWin = 96;
+__global__ __launch_bounds__(256) void k_docno(const uint8_t *t, int64_t n, const uint64_t *rs, const uint64_t *re,
+                                               int64_t nR, const uint16_t *mchars, const int64_t *moff, int64_t mn,
+                                               const uint32_t *mslots, uint64_t mmask, int32_t *docno,
+                                               unsigned long long *err) {
+  __shared__ uint4 win[256][kDocWin / 16];
+  uint8_t *w = reinterpret_cast<uint8_t *>(win[threadIdx.x]);
+  const int64_t mis = (int64_t)((uintptr_t)t & 15);
+  const uint4 *a4 = reinterpret_cast<const uint4 *>(t - mis);
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nR; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = (int64_t)rs[r], e = (int64_t)re[r];
+    const int64_t Q = (s + mis) & ~(int64_t)15;  // window byte j = text position Q - mis + j
+    const int64_t w0 = Q - mis;
+#pragma unroll
+    for (int c = 0; c < kDocWin / 16; c++)
+      win[threadIdx.x][c] = Q + 16 * c < n + mis ? a4[(Q >> 4) + c] : make_uint4(0, 0, 0, 0);
+    const int js = (int)(s - w0), je = (int)min<int64_t>(kDocWin, e - w0);
+    int a = -1, z = -1;
+    for (int j = js; j + 7 <= je; j++)
+      if (w[j] == '<' && w[j + 1] == 'D' && w[j + 2] == 'O' && w[j + 3] == 'C' && w[j + 4] == 'N' &&
+          w[j + 5] == 'O' && w[j + 6] == '>') {
+        a = j;
+        break;
+      }
+    if (a >= 0)
+      for (int j = a; j + 8 <= je; j++)
+        if (w[j] == '<' && w[j + 1] == '/' && w[j + 2] == 'D' && w[j + 3] == 'O' && w[j + 4] == 'C' &&
+            w[j + 5] == 'N' && w[j + 6] == 'O' && w[j + 7] == '>') {
+          z = j;
+          break;
+        }
     int64_t ib, ie;
-    if (!docid_span(t, s, e, &ib, &ie)) {  // getDocid throws: the map task fails
-      atomicAdd(err, 1ull);
-      docno[r] = 0;
-      continue;
+    const uint8_t *db;  // the docid's bytes (window or text)
+    if (a >= 0 && z >= 0) {
+      int b = a + 7, f = z;
+      while (b < f && w[b] <= 0x20) b++;
+      while (f > b && w[f - 1] <= 0x20) f--;
+      ib = w0 + b;
+      ie = w0 + f;
+      db = w + b;
+    } else {
+      if (!docid_span(t, s, e, &ib, &ie)) {  // getDocid throws: the map task fails
+        atomicAdd(err, 1ull);
+        docno[r] = 0;
+        continue;
+      }
+      db = t + ib;
     }
+    const int64_t dl = ie - ib;
     if (mslots) {
       uint64_t h = 0xCBF29CE484222325ull;
-      for (int64_t p = ib; p < ie;) {
+      for (int64_t p = 0; p < dl;) {
         uint16_t u[2];
         int nu;
-        p += utf8_step(t, p, ie, u, &nu);
+        p += utf8_step(db, p, dl, u, &nu);
         for (int x = 0; x < nu; x++) h = docid_hash_step(h, u[x]);
       }
       uint64_t sl = docid_hash_fin(h) & mmask;
       int64_t found = -1;
       for (uint32_t v; (v = mslots[sl]) != 0u; sl = (sl + 1) & mmask) {
         const int64_t m = (int64_t)v - 1;
-        if (cmp_u16_utf8(mchars + moff[m], moff[m + 1] - moff[m], t + ib, ie - ib) == 0) {
+        if (cmp_u16_utf8(mchars + moff[m], moff[m + 1] - moff[m], db, dl) == 0) {
           found = m;
           break;
         }
@@ -443,7 +486,7 @@ __global__ void k_docno(const uint8_t *t, const uint64_t *rs, const uint64_t *re
     int64_t res = INT64_MIN;
     while (lo <= hi) {
       int64_t mid = (int64_t)(((uint64_t)lo + (uint64_t)hi) >> 1);
-      int c = cmp_u16_utf8(mchars + moff[mid], moff[mid + 1] - moff[mid], t + ib, ie - ib);
+      int c = cmp_u16_utf8(mchars + moff[mid], moff[mid + 1] - moff[mid], db, dl);
       if (c < 0)
         lo = mid + 1;
       else if (c > 0)
@@ -2509,7 +2552,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   int32_t *docno = W[W_DOCNO].as<int32_t>(nR + 1);
   SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
   if (nR > 0 && job == 0) {
-    hipLaunchKernelGGL(k_docno, dim3(grid_for(nR)), dim3(256), 0, st, t, rs, re, nR,
+    hipLaunchKernelGGL(k_docno, dim3(grid_for(nR)), dim3(256), 0, st, t, (int64_t)n, rs, re, nR,
                        (const uint16_t *)cx->map_chars.p, (const int64_t *)cx->map_off.p, cx->map_n,
                        cx->map_hash_ok ? (const uint32_t *)cx->map_slots.p : nullptr, cx->map_mask, docno, cnt);
     SME_CHECK_LAUNCH();
