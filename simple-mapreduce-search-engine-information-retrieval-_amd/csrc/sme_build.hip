@@ -1380,11 +1380,13 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
 // still serialised 131 k atomics on one address: 0.84 ms on c2.)
 __global__ __launch_bounds__(256) void k_final_compact(const unsigned long long *fkeys,
                                                        const unsigned long long *freps, uint64_t fmask,
-                                                       const uint64_t *cand_str, unsigned long long *nV,
-                                                       uint32_t *vslot, uint32_t *vidx, int32_t *maxlen) {
+                                                       const uint64_t *cand_str, const uint16_t *pool,
+                                                       unsigned long long *nV, uint32_t *vslot, uint32_t *vidx,
+                                                       int32_t *maxlen) {
   __shared__ uint32_t s_w[4];
   __shared__ unsigned long long s_base;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t wide = 0;  // a term with a unit >= 128 (no 7-bit packing of the sort keys)
   const uint64_t n = fmask + 1, R = (n + gridDim.x - 1) / gridDim.x;
   const uint64_t a = blockIdx.x * R, b = min(n, a + R);
   uint32_t c = 0;
@@ -1414,24 +1416,35 @@ __global__ __launch_bounds__(256) void k_final_compact(const unsigned long long 
       const unsigned long long i = base + before + __popcll(m & ((1ull << lane) - 1ull));
       vslot[i] = (uint32_t)s;
       vidx[i] = (uint32_t)i;
-      ml = max(ml, (int32_t)(cand_str[freps[s] - 1] & 0xFFFF));
+      const uint64_t cs = cand_str[freps[s] - 1];
+      const int32_t l = (int32_t)(cs & 0xFFFF);
+      ml = max(ml, l);
+      uint32_t orv = 0;
+      for (int32_t j = 0; j < l; j++) orv |= pool[(cs >> 16) + j];
+      wide |= orv >= 128u ? 1 : 0;
     }
     base += tot;
     __syncthreads();
   }
-  for (int o = 32; o > 0; o >>= 1) ml = max(ml, __shfl_xor(ml, o, 64));
+  for (int o = 32; o > 0; o >>= 1) {
+    ml = max(ml, __shfl_xor(ml, o, 64));
+    wide |= __shfl_xor(wide, o, 64);
+  }
   if (lane == 0 && ml > 0) atomicMax(maxlen, ml);
+  if (lane == 0 && wide) atomicOr(maxlen + 1, 1);
 }
 
 // key word w (units 4w..4w+3, big-endian, zero padded) of the term at each order position
+// (cpw units of ub bits per word: 4 x 16 in general, 9 x 7 when every unit is
+// ASCII -- unit order is code order either way, so fewer words to sort)
 __global__ void k_term_word(const uint32_t *order, int64_t V, const uint32_t *vslot, const unsigned long long *freps,
-                            const uint64_t *cand_str, const uint16_t *pool, int w, uint64_t *key) {
+                            const uint64_t *cand_str, const uint16_t *pool, int w, int cpw, int ub, uint64_t *key) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t cs = cand_str[freps[vslot[order[i]]] - 1];
     const uint16_t *u = pool + (cs >> 16);
     int l = (int)(cs & 0xFFFF);
     uint64_t k = 0;
-    for (int j = 4 * w; j < 4 * w + 4; j++) k = (k << 16) | (j < l ? u[j] : 0);
+    for (int j = cpw * w; j < cpw * w + cpw; j++) k = (k << ub) | (j < l ? u[j] : 0);
     key[i] = k;
   }
 }
@@ -2759,7 +2772,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   uint32_t *vidx = W[W_VIDX].as<uint32_t>(ncand + 1);
   int32_t *maxlen = reinterpret_cast<int32_t *>(cnt + 12);
   hipLaunchKernelGGL(k_final_compact, dim3(grid_for((int64_t)fcap)), dim3(256), 0, st, fkeys, freps, fcap - 1,
-                     co.cand_str, cnt + 1, vslot, vidx, maxlen);
+                     co.cand_str, co.pool, cnt + 1, vslot, vidx, maxlen);
   SME_CHECK_LAUNCH();
   unsigned long long hv[13];
   SME_HIP(hipMemcpyAsync(hv, cnt, sizeof hv, hipMemcpyDeviceToHost, st));
@@ -2767,6 +2780,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   if (d2h(ovf, st)) throw Error(SME_ELIMIT, "final term table overflow");
   const int64_t V = (int64_t)hv[1];
   const int term_maxlen = (int)(int32_t)(uint32_t)hv[12];
+  const bool term_wide = (hv[12] >> 32) != 0;  // maxlen + 1: a term has a unit >= 128
 
   sme_index *ix = new sme_index(cx);
   std::unique_ptr<sme_index> ix_guard(ix);  // freed (back to the pool) if a later stage throws
@@ -2783,15 +2797,17 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     // LSD radix sort of the vocabulary in String.compareTo order: 4 UTF-16 units per
     // 64-bit key word, least significant word first, stable; terms are at most
     // 99 units and all words below the longest term's length are sorted.
-    const int nwords = std::min(8, (std::max(term_maxlen, 1) + 3) / 4);
+    // (9 ASCII units of 7 bits per word when no unit is >= 128)
+    const int cpw = term_wide ? 4 : 9, ub = term_wide ? 16 : 7, kbits = cpw * ub;
+    const int nwords = std::min(8, (std::max(term_maxlen, 1) + cpw - 1) / cpw);
     uint64_t *kw = W[W_KHI].as<uint64_t>(V), *kw2 = W[W_KLO].as<uint64_t>(V);
     uint32_t *ord_a = vidx, *ord_b = order;
     size_t tbb = 0;
     for (int w = nwords - 1; w >= 0; w--) {
       hipLaunchKernelGGL(k_term_word, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V, vslot, freps, co.cand_str,
-                         co.pool, w, kw);
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, kw, kw2, ord_a, ord_b, (int)V, 0, 64, st));
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, kw, kw2, ord_a, ord_b, (int)V, 0, 64, st));
+                         co.pool, w, cpw, ub, kw);
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, kw, kw2, ord_a, ord_b, (int)V, 0, kbits, st));
+      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, kw, kw2, ord_a, ord_b, (int)V, 0, kbits, st));
       std::swap(ord_a, ord_b);
     }
     if (ord_a != order)
