@@ -1883,7 +1883,8 @@ __global__ void k_pair_stats(const uint64_t *val, int64_t P, unsigned int *max_t
   for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
   if ((threadIdx.x & 63) == 0) atomicMax(max_tf, m);
 }
-__global__ void k_docno_range(const int32_t *docno, int64_t n, int *mn, int *mx) {
+__global__ __launch_bounds__(256) void k_docno_range(const int32_t *docno, int64_t n, int *mn, int *mx) {
+  __shared__ int s_a[4], s_b[4];
   int a = INT_MAX, b = INT_MIN;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     a = min(a, docno[i]);
@@ -1894,6 +1895,15 @@ __global__ void k_docno_range(const int32_t *docno, int64_t n, int *mn, int *mx)
     b = max(b, __shfl_xor(b, o, 64));
   }
   if ((threadIdx.x & 63) == 0) {
+    s_a[threadIdx.x >> 6] = a;
+    s_b[threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // one atomic pair per block (single-address atomics serialise)
+    for (int x = 1; x < 4; x++) {
+      a = min(a, s_a[x]);
+      b = max(b, s_b[x]);
+    }
     atomicMin(mn, a);
     atomicMax(mx, b);
   }
@@ -3289,7 +3299,11 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
 
   // doc-counter postings need every record's docno in input order
   int32_t *rdn = ix->d_rec_docno.as<int32_t>(nR + 1);
-  if (nR > 0) {
+  if (nR > 0 && want_packed && h_drange[1] >= h_drange[0]) {  // range known from the aggregation
+    SME_HIP(hipMemcpyAsync(rdn, docno, nR * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    ix->dmin = h_drange[0];
+    ix->dmax = h_drange[1];
+  } else if (nR > 0) {
     SME_HIP(hipMemcpyAsync(rdn, docno, nR * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     int *dmn = reinterpret_cast<int *>(cnt + 12), *dmx = dmn + 1;
     const int h_init[2] = {INT_MAX, INT_MIN};
