@@ -1763,13 +1763,15 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
     if (fused && lane == 0) in.dcnt[i] = d;
     wave_sync_lds();
   }
-  if (fused) {
+  if (fused || (!EMIT && in.max_tf)) {  // largest tf: one atomic per block (single-address atomics serialise)
+    __shared__ uint32_t s_wmax[kAggNT / 64];
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
-    if (lane == 0 && wmax) atomicMax(in.max_tf, wmax);
-  }
-  if (!EMIT && in.max_tf) {
-    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
-    if (lane == 0 && wmax) atomicMax(in.max_tf, wmax);
+    if (lane == 0) s_wmax[wv] = wmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int x = 1; x < kAggNT / 64; x++) wmax = max(wmax, s_wmax[x]);
+      if (wmax) atomicMax(in.max_tf, wmax);
+    }
   }
 }
 
