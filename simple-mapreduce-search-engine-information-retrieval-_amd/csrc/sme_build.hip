@@ -1669,6 +1669,10 @@ __global__ __launch_bounds__(kAggNT) void k_agg(AggIn in, int64_t nR, int32_t *p
 // are written at pair_off[i] in 16 coalesced rounds of 64 table entries.
 constexpr int kWCap = 1024;
 constexpr int kWLimit = 768;
+#ifndef SME_AGGU
+#define SME_AGGU 8
+#endif
+constexpr int kAggU = SME_AGGU;
 
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1715,14 +1719,23 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
     }
     wave_sync_lds();
     bool ok = true;
-    for (int32_t t = lane; t < nt; t += 64) {
-      const uint32_t slot = ts[t];
-      const int32_t rt = in.raw_term[slot];
-      if (rt >= 0) {
-        ok &= aggw_insert(keys, cnt, rt, cap);
-      } else if (rt <= -2) {
-        const int32_t m0 = -rt - 2, mn = in.raw_nout[slot];
-        for (int32_t m = 0; m < mn; m++) ok &= aggw_insert(keys, cnt, in.multi_term[m0 + m], cap);
+    // kAggU tokens per lane step: their stream loads, then their raw_term
+    // gathers, are in flight together (one step was two dependent latencies)
+    for (int32_t t0 = lane; t0 < nt; t0 += kAggU * 64) {
+      uint32_t slot[kAggU];
+      int32_t rt[kAggU];
+#pragma unroll
+      for (int u = 0; u < kAggU; u++) slot[u] = t0 + u * 64 < nt ? ts[t0 + u * 64] : 0u;
+#pragma unroll
+      for (int u = 0; u < kAggU; u++) rt[u] = t0 + u * 64 < nt ? in.raw_term[slot[u]] : -1;
+#pragma unroll
+      for (int u = 0; u < kAggU; u++) {
+        if (rt[u] >= 0) {
+          ok &= aggw_insert(keys, cnt, rt[u], cap);
+        } else if (rt[u] <= -2) {
+          const int32_t m0 = -rt[u] - 2, mn = in.raw_nout[slot[u]];
+          for (int32_t m = 0; m < mn; m++) ok &= aggw_insert(keys, cnt, in.multi_term[m0 + m], cap);
+        }
       }
     }
     wave_sync_lds();
