@@ -2357,32 +2357,36 @@ __global__ __launch_bounds__(256) void k_tf_tile_count(const int64_t *__restrict
   }
 }
 
-// (2) one block per large segment: counters -> segment-relative start positions
+// (2) one block per large segment: counters -> segment-relative start positions,
+// in (tf desc, tile asc) order.  Thread f owns counter column f (= max_tf - tf,
+// up to 4 per thread): its total over the segment's tiles, one block scan of the
+// totals, then a walk down its column (coalesced across threads at every tile).
 __global__ __launch_bounds__(256) void k_tf_tile_scan(const int64_t *__restrict__ off, int64_t V,
                                                       const int64_t *__restrict__ toff, int max_tf, int32_t *tcnt) {
-  __shared__ int32_t wsum[4];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, F = max_tf + 1;
+  __shared__ int32_t sc[256 / 64 + 1];
+  const int tid = threadIdx.x, F = max_tf + 1;
   for (int64_t s = blockIdx.x; s < V; s += gridDim.x) {
     const int64_t t0 = toff[s], T = toff[s + 1] - t0;
     if (T == 0) continue;  // block-uniform
-    int base = 0;          // identical in every thread
-    for (int f = 0; f < F; f++) {
-      for (int64_t j0 = 0; j0 < T; j0 += 256) {
-        const int64_t j = j0 + tid;
-        const int32_t c = j < T ? tcnt[(t0 + j) * F + f] : 0;
-        int inc = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int u = __shfl_up(inc, o, 64);
-          if (lane >= o) inc += u;
+    int32_t *c = tcnt + t0 * F;
+    int32_t carry = 0;
+    for (int f0 = 0; f0 < F; f0 += 256) {  // block-uniform
+      const int f = f0 + tid;
+      int32_t tot = 0;
+      if (f < F) {
+#pragma unroll 8
+        for (int64_t j = 0; j < T; j++) tot += c[j * F + f];
+      }
+      int32_t all;
+      int32_t run = carry + block_excl_sum<256, int32_t>(tot, sc, &all);
+      carry += all;
+      if (f < F) {
+#pragma unroll 8
+        for (int64_t j = 0; j < T; j++) {
+          const int32_t x = c[j * F + f];
+          c[j * F + f] = run;
+          run += x;
         }
-        if (lane == 63) wsum[w] = inc;
-        __syncthreads();
-        int pre = base;
-        for (int k = 0; k < w; k++) pre += wsum[k];
-        if (j < T) tcnt[(t0 + j) * F + f] = pre + inc - c;
-        base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        __syncthreads();
       }
     }
   }
