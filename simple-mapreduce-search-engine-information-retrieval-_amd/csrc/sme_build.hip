@@ -2242,16 +2242,18 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_tfsort_block(const int64_t *__restrict__ off, int64_t V,
                                                           const int32_t *__restrict__ docno_d,
                                                           const int32_t *__restrict__ tf_d, int32_t *docno_o,
-                                                          int32_t *tf_o, int64_t lo, int64_t hi, int max_tf) {
+                                                          int32_t *tf_o, const int32_t *__restrict__ seg,
+                                                          const unsigned long long *__restrict__ nseg, int max_tf) {
   extern __shared__ int32_t cnt[];  // [(max_tf - tf) * NW + w]
   __shared__ int32_t wsum[NW];
   constexpr int NT = NW * 64;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int L = (max_tf + 1) * NW;
   const uint64_t lt_mask = (1ull << lane) - 1;
-  for (int64_t s = blockIdx.x; s < V; s += gridDim.x) {
+  const int64_t ns = (int64_t)*nseg;
+  for (int64_t q = blockIdx.x; q < ns; q += gridDim.x) {
+    const int64_t s = seg[q];
     const int64_t b = off[s], n = off[s + 1] - b;
-    if (n <= lo || n > hi) continue;  // block-uniform
     for (int j = tid; j < L; j += NT) cnt[j] = 0;
     __syncthreads();
     const int64_t nch = (n + 63) >> 6, cpw = (nch + NW - 1) / NW;
@@ -2318,10 +2320,37 @@ __global__ __launch_bounds__(NW * 64) void k_tfsort_block(const int64_t *__restr
 // ballot placement of k_tfsort_block from the tile's scanned counters.
 constexpr int kTfTile = 4096;
 
-__global__ void k_tf_ntiles(const int64_t *off, int64_t V, int64_t *nt) {
-  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s <= V; s += (int64_t)gridDim.x * blockDim.x) {
+// segment lists by class (medium: 4-wave blocks, large: tiles), appended with
+// one global atomic per block and list; list order is free (segments are
+// independent and their output ranges fixed)
+__global__ __launch_bounds__(256) void k_tf_classify(const int64_t *__restrict__ off, int64_t V, int32_t *med,
+                                                     int32_t *large, unsigned long long *ctr) {
+  __shared__ unsigned int s_n[2];
+  __shared__ unsigned long long s_b[2];
+  for (int64_t s0 = (int64_t)blockIdx.x * 256; s0 < V; s0 += (int64_t)gridDim.x * 256) {  // block-uniform
+    const int64_t s = s0 + threadIdx.x;
     const int64_t n = s < V ? off[s + 1] - off[s] : 0;
-    nt[s] = n > kTfMedium ? (n + kTfTile - 1) / kTfTile : 0;
+    const bool is_l = n > kTfMedium, is_m = n > kTfSmall && !is_l;
+    if (threadIdx.x < 2) s_n[threadIdx.x] = 0;
+    __syncthreads();
+    unsigned int pm = 0, pl = 0;
+    if (is_m) pm = atomicAdd(&s_n[0], 1u);
+    if (is_l) pl = atomicAdd(&s_n[1], 1u);
+    __syncthreads();
+    if (threadIdx.x < 2) s_b[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&ctr[threadIdx.x], (unsigned long long)s_n[threadIdx.x]) : 0ull;
+    __syncthreads();
+    if (is_m) med[s_b[0] + pm] = (int32_t)s;
+    if (is_l) large[s_b[1] + pl] = (int32_t)s;
+    __syncthreads();
+  }
+}
+// tiles of large segment q (0 beyond the list: the scan covers V + 1 entries)
+__global__ void k_tf_ntiles(const int64_t *off, const int32_t *large, const unsigned long long *nlarge, int64_t V,
+                            int64_t *nt) {
+  const int64_t nl = (int64_t)*nlarge;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q <= V; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = q < nl ? off[large[q] + 1] - off[large[q]] : 0;
+    nt[q] = (n + kTfTile - 1) / kTfTile;
   }
 }
 
@@ -2337,7 +2366,9 @@ __device__ __forceinline__ int64_t tile_segment(const int64_t *toff, int64_t V, 
 }
 
 // (1) one wave per tile: LDS counts (order-free), written as tcnt[tau][max_tf - tf]
-__global__ __launch_bounds__(256) void k_tf_tile_count(const int64_t *__restrict__ off, int64_t V,
+__global__ __launch_bounds__(256) void k_tf_tile_count(const int64_t *__restrict__ off,
+                                                       const int32_t *__restrict__ large,
+                                                       const unsigned long long *__restrict__ nlarge,
                                                        const int64_t *__restrict__ toff, int64_t ntiles,
                                                        const int32_t *__restrict__ tf_d, int max_tf,
                                                        int32_t *tcnt) {
@@ -2345,9 +2376,10 @@ __global__ __launch_bounds__(256) void k_tf_tile_count(const int64_t *__restrict
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, F = max_tf + 1;
   int32_t *hw = h + w * F;
   const int64_t nwv = (int64_t)gridDim.x * 4;
+  const int64_t nl = (int64_t)*nlarge;
   for (int64_t tau = (int64_t)blockIdx.x * 4 + w; tau < ntiles; tau += nwv) {  // wave-uniform
-    const int64_t s = tile_segment(toff, V, tau);
-    const int64_t b = off[s] + (tau - toff[s]) * kTfTile, e = min(off[s + 1], b + (int64_t)kTfTile);
+    const int64_t q = tile_segment(toff, nl, tau), s = large[q];
+    const int64_t b = off[s] + (tau - toff[q]) * kTfTile, e = min(off[s + 1], b + (int64_t)kTfTile);
     for (int j = lane; j < F; j += 64) hw[j] = 0;
     __builtin_amdgcn_wave_barrier();
     for (int64_t i = b + lane; i < e; i += 64) atomicAdd(&hw[max_tf - tf_d[i]], 1);
@@ -2361,13 +2393,13 @@ __global__ __launch_bounds__(256) void k_tf_tile_count(const int64_t *__restrict
 // in (tf desc, tile asc) order.  Thread f owns counter column f (= max_tf - tf,
 // up to 4 per thread): its total over the segment's tiles, one block scan of the
 // totals, then a walk down its column (coalesced across threads at every tile).
-__global__ __launch_bounds__(256) void k_tf_tile_scan(const int64_t *__restrict__ off, int64_t V,
+__global__ __launch_bounds__(256) void k_tf_tile_scan(const unsigned long long *__restrict__ nlarge,
                                                       const int64_t *__restrict__ toff, int max_tf, int32_t *tcnt) {
   __shared__ int32_t sc[256 / 64 + 1];
   const int tid = threadIdx.x, F = max_tf + 1;
-  for (int64_t s = blockIdx.x; s < V; s += gridDim.x) {
-    const int64_t t0 = toff[s], T = toff[s + 1] - t0;
-    if (T == 0) continue;  // block-uniform
+  const int64_t nl = (int64_t)*nlarge;
+  for (int64_t q = blockIdx.x; q < nl; q += gridDim.x) {
+    const int64_t t0 = toff[q], T = toff[q + 1] - t0;
     int32_t *c = tcnt + t0 * F;
     int32_t carry = 0;
     for (int f0 = 0; f0 < F; f0 += 256) {  // block-uniform
@@ -2393,7 +2425,9 @@ __global__ __launch_bounds__(256) void k_tf_tile_scan(const int64_t *__restrict_
 }
 
 // (3) one wave per tile: stable placement from the tile's counters
-__global__ __launch_bounds__(256) void k_tf_tile_place(const int64_t *__restrict__ off, int64_t V,
+__global__ __launch_bounds__(256) void k_tf_tile_place(const int64_t *__restrict__ off,
+                                                       const int32_t *__restrict__ large,
+                                                       const unsigned long long *__restrict__ nlarge,
                                                        const int64_t *__restrict__ toff, int64_t ntiles,
                                                        const int32_t *__restrict__ docno_d,
                                                        const int32_t *__restrict__ tf_d, int max_tf,
@@ -2404,10 +2438,11 @@ __global__ __launch_bounds__(256) void k_tf_tile_place(const int64_t *__restrict
   int32_t *hw = h + w * F;
   const uint64_t lt_mask = (1ull << lane) - 1;
   const int64_t nwv = (int64_t)gridDim.x * 4;
+  const int64_t nl = (int64_t)*nlarge;
   for (int64_t tau = (int64_t)blockIdx.x * 4 + w; tau < ntiles; tau += nwv) {
-    const int64_t s = tile_segment(toff, V, tau);
+    const int64_t q = tile_segment(toff, nl, tau), s = large[q];
     const int64_t sb = off[s];
-    const int64_t b = sb + (tau - toff[s]) * kTfTile, e = min(off[s + 1], b + (int64_t)kTfTile);
+    const int64_t b = sb + (tau - toff[q]) * kTfTile, e = min(off[s + 1], b + (int64_t)kTfTile);
     for (int j = lane; j < F; j += 64) hw[j] = tcnt[tau * F + j];
     __builtin_amdgcn_wave_barrier();
     for (int64_t c = b; c < e; c += 64) {
@@ -3266,13 +3301,18 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     // segmented counting sort over the term CSR (no full-width key sort)
     hipLaunchKernelGGL(k_tfsort_small, dim3(grid_for(Vi * 64, 256, 8192)), dim3(256), 0, st, off, Vi, docno_d, tf_d,
                        docno_o, tf_o);
+    // medium and large segments as lists (a grid-stride walk over all V terms costs a
+    // dependent offset load per term and block)
+    int64_t *ntl = W[W_FKEYS].as<int64_t>(2 * (Vi + 1)), *toff = W[W_FREPS].as<int64_t>(Vi + 1);
+    int32_t *seg_med = reinterpret_cast<int32_t *>(ntl + Vi + 1), *seg_large = seg_med + Vi;
+    unsigned long long *nseg = cnt + 28;  // [0] medium, [1] large
+    SME_HIP(hipMemsetAsync(nseg, 0, 2 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_tf_classify, dim3(grid_for(Vi)), dim3(256), 0, st, off, Vi, seg_med, seg_large, nseg);
     const size_t lds4 = (size_t)(max_tf + 1) * 4 * sizeof(int32_t);
     hipLaunchKernelGGL(k_tfsort_block<4>, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(Vi, 1), 4096)),
-                       dim3(256), lds4, st, off, Vi, docno_d, tf_d, docno_o, tf_o, (int64_t)kTfSmall,
-                       (int64_t)kTfMedium, max_tf);
+                       dim3(256), lds4, st, off, Vi, docno_d, tf_d, docno_o, tf_o, seg_med, nseg, max_tf);
     // large segments: tiles spread over the whole chip
-    int64_t *ntl = W[W_FKEYS].as<int64_t>(Vi + 1), *toff = W[W_FREPS].as<int64_t>(Vi + 1);
-    hipLaunchKernelGGL(k_tf_ntiles, dim3(grid_for(Vi + 1)), dim3(256), 0, st, off, Vi, ntl);
+    hipLaunchKernelGGL(k_tf_ntiles, dim3(grid_for(Vi + 1)), dim3(256), 0, st, off, seg_large, nseg + 1, Vi, ntl);
     size_t tbb = 0;
     SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, ntl, toff, (int)Vi + 1, st));
     SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, ntl, toff, (int)Vi + 1, st));
@@ -3281,12 +3321,12 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       const int F = max_tf + 1;
       int32_t *tcnt = reinterpret_cast<int32_t *>(W[W_CKEY].as<uint64_t>((ntiles * F + 1) / 2 + 1));
       const unsigned tg = (unsigned)std::min<int64_t>((ntiles + 3) / 4, 8192);
-      hipLaunchKernelGGL(k_tf_tile_count, dim3(tg), dim3(256), (size_t)4 * F * sizeof(int32_t), st, off, Vi, toff,
-                         ntiles, tf_d, max_tf, tcnt);
-      hipLaunchKernelGGL(k_tf_tile_scan, dim3((unsigned)std::min<int64_t>(Vi, 8192)), dim3(256), 0, st, off, Vi,
+      hipLaunchKernelGGL(k_tf_tile_count, dim3(tg), dim3(256), (size_t)4 * F * sizeof(int32_t), st, off, seg_large,
+                         nseg + 1, toff, ntiles, tf_d, max_tf, tcnt);
+      hipLaunchKernelGGL(k_tf_tile_scan, dim3((unsigned)std::min<int64_t>(Vi, 8192)), dim3(256), 0, st, nseg + 1,
                          toff, max_tf, tcnt);
-      hipLaunchKernelGGL(k_tf_tile_place, dim3(tg), dim3(256), (size_t)4 * F * sizeof(int32_t), st, off, Vi, toff,
-                         ntiles, docno_d, tf_d, max_tf, tcnt, docno_o, tf_o);
+      hipLaunchKernelGGL(k_tf_tile_place, dim3(tg), dim3(256), (size_t)4 * F * sizeof(int32_t), st, off, seg_large,
+                         nseg + 1, toff, ntiles, docno_d, tf_d, max_tf, tcnt, docno_o, tf_o);
     }
     SME_CHECK_LAUNCH();
   } else if (PP > 0) {

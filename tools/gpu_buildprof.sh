@@ -8,6 +8,6 @@ python3 - "$f" <<'PY'
 import csv,sys
 rows=list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r:-float(r["TotalDurationNs"]))
-for r in rows[:28]:
+for r in rows[:45]:
     print("%-60s %6s %10.3f ms avg %8.3f ms" % (r["Name"][:60], r["Calls"], float(r["TotalDurationNs"])/1e6, float(r["AverageNs"])/1e6))
 PY
