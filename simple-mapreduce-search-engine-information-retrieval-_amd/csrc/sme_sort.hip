@@ -42,6 +42,7 @@ constexpr int kRsGroups = 256;              // tile groups of the column scan
 // items starts there and advances a record at a time.
 struct Gather {
   const int64_t *reg, *xoff, *crec;
+  int64_t nrec;
 };
 __device__ __forceinline__ void gather_start(const Gather &g, int64_t x, int64_t &rec, int64_t &nx, int64_t &dl) {
   rec = g.crec[x >> 10];
@@ -55,6 +56,27 @@ __device__ __forceinline__ int64_t gather_pos(const Gather &g, int64_t x, int64_
     dl = g.reg[rec] - g.xoff[rec];
   }
   return x + dl;
+}
+// A wave's 1024 items span a few records: lane j loads record rec0 + j's pair
+// start and region delta into LDS once, so the per-item walk reads LDS and the
+// item loads are not held behind dependent global loads (vmcnt is in order).
+// Walks past 64 records fall back to the global walk.
+__device__ __forceinline__ int64_t gather_table(const Gather &g, int64_t x0, int lane, int64_t *gx, int64_t *gdl) {
+  const int64_t rec0 = g.crec[x0 >> 10];
+  const int64_t r = rec0 + lane;
+  gx[lane] = r <= g.nrec ? g.xoff[r] : INT64_MAX;
+  gdl[lane] = r < g.nrec ? g.reg[r] - g.xoff[r] : 0;
+  if (lane == 0) gx[64] = rec0 + 64 <= g.nrec ? g.xoff[rec0 + 64] : INT64_MAX;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  return rec0;
+}
+__device__ __forceinline__ int64_t gather_at(const Gather &g, int64_t x, int &j, const int64_t *gx, const int64_t *gdl,
+                                             int64_t rec0) {
+  while (j < 63 && x >= gx[j + 1]) j++;
+  if (x < gx[j + 1]) return x + gdl[j];
+  int64_t rec = rec0 + 63, nx = g.xoff[rec + 1], dl = g.reg[rec] - g.xoff[rec];
+  return gather_pos(g, x, rec, nx, dl);
 }
 __global__ void k_rs_chunk_rec(const int64_t *__restrict__ xoff, int64_t nrec, int64_t P, int64_t *__restrict__ crec) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; (c << 10) < P; c += (int64_t)gridDim.x * blockDim.x) {
@@ -79,16 +101,21 @@ __global__ __launch_bounds__(kRsNT) void k_rs_count(const uint32_t *__restrict__
   const uint32_t mask = (uint32_t)nbins - 1u;
   const int64_t n = min((int64_t)kRsTile, P - t0);
   if (g.reg != nullptr) {
-    const int lane = tid & 63;
-    const int64_t wb = t0 + (int64_t)(tid >> 6) * kRsWaveItems;
+    __shared__ int64_t gx_all[kRsWaves][65], gdl_all[kRsWaves][64];
+    const int lane = tid & 63, w = tid >> 6;
+    const int64_t wb = t0 + (int64_t)w * kRsWaveItems;
     if (wb < P) {
-      int64_t rec, nx, dl;
-      gather_start(g, wb, rec, nx, dl);
-#pragma unroll 4
+      const int64_t rec0 = gather_table(g, wb, lane, gx_all[w], gdl_all[w]);
+      int j = 0;
+      uint32_t kk[kRsIPL];
+#pragma unroll
       for (int s = 0; s < kRsIPL; s++) {
         const int64_t x = wb + s * 64 + lane;
-        if (x < P) atomicAdd(&h[(key[gather_pos(g, x, rec, nx, dl)] >> shift) & mask], 1u);
+        kk[s] = x < P ? key[gather_at(g, x, j, gx_all[w], gdl_all[w], rec0)] : 0u;
       }
+#pragma unroll
+      for (int s = 0; s < kRsIPL; s++)
+        if (wb + s * 64 + lane < P) atomicAdd(&h[(kk[s] >> shift) & mask], 1u);
     }
   } else if (n == kRsTile) {
     const uint4 *k4 = reinterpret_cast<const uint4 *>(key + t0);
@@ -216,15 +243,17 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
   const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t k[kRsIPL], v[kRsIPL], pos[kRsIPL];
   if (g.reg != nullptr) {
-    int64_t rec = 0, nx = 0, dl = 0;
-    if (wb < n) gather_start(g, t0 + wb, rec, nx, dl);
+    __shared__ int64_t gx_all[kRsWaves][65], gdl_all[kRsWaves][64];
+    int64_t rec0 = 0;
+    if (wb < n) rec0 = gather_table(g, t0 + wb, lane, gx_all[w], gdl_all[w]);
+    int j = 0;
 #pragma unroll
     for (int s = 0; s < kRsIPL; s++) {
       const int i = wb + s * 64 + lane;
       k[s] = 0u;
       v[s] = 0u;
       if (i < n) {
-        const int64_t p = gather_pos(g, t0 + i, rec, nx, dl);
+        const int64_t p = gather_at(g, t0 + i, j, gx_all[w], gdl_all[w], rec0);
         k[s] = key[p];
         v[s] = val[p];
       }
@@ -348,17 +377,17 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
   const int64_t ntiles = (P + kRsTile - 1) / kRsTile;
   const int64_t tpg = (ntiles + kRsGroups - 1) / kRsGroups;
   uint32_t *gsum = counts + ntiles * kRsMaxBins;
-  Gather g0{nullptr, nullptr, nullptr};
+  Gather g0{nullptr, nullptr, nullptr, 0};
   if (reg != nullptr) {
     int64_t *crec = reinterpret_cast<int64_t *>(gsum + kRsMaxBins * kRsGroups);
     const int64_t nch = (P + 1023) >> 10;
     hipLaunchKernelGGL(k_rs_chunk_rec, dim3((unsigned)std::min<int64_t>((nch + 255) / 256, 4096)), dim3(256), 0, st,
                        xoff, nrec, P, crec);
-    g0 = Gather{reg, xoff, crec};
+    g0 = Gather{reg, xoff, crec, nrec};
   }
   int shift = 0;
   for (int p = 0; p < npass; p++) {
-    const Gather g = p == 0 ? g0 : Gather{nullptr, nullptr, nullptr};
+    const Gather g = p == 0 ? g0 : Gather{nullptr, nullptr, nullptr, 0};
     const int nb = (bits - shift + (npass - p) - 1) / (npass - p);  // near-equal digits
     const int nbins = 1 << nb;
     const bool last = p == npass - 1;
