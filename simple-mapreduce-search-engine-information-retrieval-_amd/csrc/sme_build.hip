@@ -1843,11 +1843,22 @@ __global__ __launch_bounds__(kAggNT) void k_agg_big(AggIn in, const int64_t *big
 // ============================================================================
 // K6-K8: CSR assembly
 // ============================================================================
+// first posting of every term (key sorted); four keys per 16-byte load
 __global__ void k_term_offsets(const uint32_t *key, int64_t P, int64_t *off, int64_t V) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
-    if (i == 0 || key[i] != key[i - 1]) off[key[i]] = i;
-    if (i == 0) off[V] = P;
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = P >> 2;
+  for (int64_t q = gid; q < n4; q += gs) {
+    const uint4 k = reinterpret_cast<const uint4 *>(key)[q];
+    const int64_t i = q << 2;
+    const uint32_t prev = i == 0 ? ~k.x : key[i - 1];
+    if (k.x != prev) off[k.x] = i;
+    if (k.y != k.x) off[k.y] = i + 1;
+    if (k.z != k.y) off[k.z] = i + 2;
+    if (k.w != k.z) off[k.w] = i + 3;
   }
+  for (int64_t i = (n4 << 2) + gid; i < P; i += gs)
+    if (i == 0 || key[i] != key[i - 1]) off[key[i]] = i;
+  if (gid == 0) off[V] = P;
 }
 
 __global__ void k_unpack_vals(const uint64_t *val, int64_t P, int32_t *docno, int32_t *tf) {
@@ -1872,21 +1883,39 @@ __global__ void k_dup_unpack(const uint64_t *ck, const int32_t *tf, int64_t P, u
   }
 }
 
+__device__ __forceinline__ double weight_at(uint32_t t, int32_t tf, const double *lut, double idf_ref,
+                                            const int64_t *off, int64_t N, const double *idf_by_df, int64_t sdf,
+                                            const double *idf_by_q, int mode) {
+  double idf;
+  if (mode == SME_IDF_REFERENCE) {
+    idf = idf_ref;
+  } else {
+    const int64_t df = off[t + 1] - off[t];
+    idf = df <= sdf ? idf_by_df[df] : idf_by_q[N / df];
+  }
+  return __dmul_rn(lut[tf], idf);
+}
+// w = LUT[tf] * idf per posting; four postings per thread step (16-byte tf
+// loads, two 16-byte weight stores); the key is read only in the df modes
 __global__ void k_weights(const uint32_t *key, const int32_t *tf, int64_t P, const double *lut, double idf_ref,
                           const int64_t *off, int64_t N, const double *idf_by_df, int64_t sdf,
                           const double *idf_by_q, int mode, double *w) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
-    double idf;
-    if (mode == SME_IDF_REFERENCE) {
-      idf = idf_ref;
-    } else {
-      uint32_t t = key[i];
-      int64_t df = off[t + 1] - off[t];
-      idf = df <= sdf ? idf_by_df[df] : idf_by_q[N / df];
-    }
-    double a = lut[tf[i]];
-    w[i] = __dmul_rn(a, idf);
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = P >> 2;
+  const bool ref = mode == SME_IDF_REFERENCE;
+  for (int64_t q = gid; q < n4; q += gs) {
+    const int4 f = reinterpret_cast<const int4 *>(tf)[q];
+    const uint4 k = ref ? make_uint4(0, 0, 0, 0) : reinterpret_cast<const uint4 *>(key)[q];
+    double2 a, b;
+    a.x = weight_at(k.x, f.x, lut, idf_ref, off, N, idf_by_df, sdf, idf_by_q, mode);
+    a.y = weight_at(k.y, f.y, lut, idf_ref, off, N, idf_by_df, sdf, idf_by_q, mode);
+    b.x = weight_at(k.z, f.z, lut, idf_ref, off, N, idf_by_df, sdf, idf_by_q, mode);
+    b.y = weight_at(k.w, f.w, lut, idf_ref, off, N, idf_by_df, sdf, idf_by_q, mode);
+    reinterpret_cast<double2 *>(w)[2 * q] = a;
+    reinterpret_cast<double2 *>(w)[2 * q + 1] = b;
   }
+  for (int64_t i = (n4 << 2) + gid; i < P; i += gs)
+    w[i] = weight_at(ref ? 0u : key[i], tf[i], lut, idf_ref, off, N, idf_by_df, sdf, idf_by_q, mode);
 }
 
 // Packed 32-bit sort path (the common case): a posting's (docno, tf) fits one

@@ -117,6 +117,22 @@ def test_build_big_records_interleaved(sme, synth):
     _check_build(sme, b"".join(docs), ids, R=3)
 
 
+def test_build_many_tiny_records(sme):
+    """Thousands of records with 0-3 words (a few pairs each, some only the
+    docid): a wave's 1024 pairs of the term sort's gather pass span hundreds of
+    records, past its 64-record LDS table (the global walk takes over)."""
+    rng = random.Random(11)
+    docs, ids = [], []
+    for i in range(3000):
+        did = "T%05d" % i
+        ids.append(did)
+        words = ["t%03d" % rng.randrange(400) for _ in range(rng.randint(0, 3))]
+        if i % 7 == 0:
+            words = ["one", "two"]  # stopwords only
+        docs.append(b"<DOC>\n<DOCNO>" + did.encode() + b"</DOCNO>\n" + " ".join(words).encode() + b"\n</DOC>\n")
+    _check_build(sme, b"".join(docs), ids, R=2)
+
+
 def test_build_nested_doc_tags(sme):
     """A <DOC> inside a record is content (XMLRecordReader reads to the next
     </DOC>); a start tag after the last </DOC> opens no record."""
