@@ -1327,7 +1327,9 @@ __device__ __forceinline__ uint64_t hash_u16(const uint16_t *p, int l) {
 
 __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, int64_t ncand,
                                unsigned long long *fkeys, unsigned long long *freps, uint64_t fmask,
-                               uint32_t *cand_final, unsigned int *overflow) {
+                               uint32_t *cand_final, unsigned int *overflow, int32_t *maxlen) {
+  int32_t ml = 0;
+  uint32_t orv = 0;  // OR of every unit: a term with a unit >= 128 (no 7-bit packing of the sort keys)
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncand; c += (int64_t)gridDim.x * blockDim.x) {
     uint64_t cs = cand_str[c];
     if (cs == kNoCand) {  // raw token with no output (stopword / dropped)
@@ -1336,6 +1338,8 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
     }
     const uint16_t *w = pool + (cs >> 16);
     int l = (int)(cs & 0xFFFF);
+    ml = max(ml, l);
+    for (int i = 0; i < l; i++) orv |= w[i];
     uint64_t h = hash_u16(w, l);
     uint64_t slot = h & fmask;
     uint32_t res = 0xFFFFFFFFu;
@@ -1370,6 +1374,27 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
     if (res == 0xFFFFFFFFu) atomicOr(overflow, 1u);
     cand_final[c] = res;
   }
+  // longest term and the wide flag: one atomic each per block (the candidates
+  // are exactly the final terms' strings, duplicates included)
+  __shared__ int32_t s_ml[4];
+  __shared__ uint32_t s_or[4];
+  for (int o = 32; o > 0; o >>= 1) {
+    ml = max(ml, __shfl_xor(ml, o, 64));
+    orv |= (uint32_t)__shfl_xor((int)orv, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_ml[threadIdx.x >> 6] = ml;
+    s_or[threadIdx.x >> 6] = orv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int x = 1; x < (int)(blockDim.x >> 6); x++) {
+      ml = max(ml, s_ml[x]);
+      orv |= s_or[x];
+    }
+    if (ml > 0) atomicMax(maxlen, ml);
+    if (orv >= 128u) atomicOr(maxlen + 1, 1);
+  }
 }
 
 // compact occupied final slots; longest term (in units) for the LSD sort depth
@@ -1381,12 +1406,10 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
 __global__ __launch_bounds__(256) void k_final_compact(const unsigned long long *fkeys,
                                                        const unsigned long long *freps, uint64_t fmask,
                                                        const uint64_t *cand_str, const uint16_t *pool,
-                                                       unsigned long long *nV, uint32_t *vslot, uint32_t *vidx,
-                                                       int32_t *maxlen) {
+                                                       unsigned long long *nV, uint32_t *vslot, uint32_t *vidx) {
   __shared__ uint32_t s_w[4];
   __shared__ unsigned long long s_base;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int32_t wide = 0;  // a term with a unit >= 128 (no 7-bit packing of the sort keys)
   const uint64_t n = fmask + 1, R = (n + gridDim.x - 1) / gridDim.x;
   const uint64_t a = blockIdx.x * R, b = min(n, a + R);
   uint32_t c = 0;
@@ -1400,7 +1423,6 @@ __global__ __launch_bounds__(256) void k_final_compact(const unsigned long long 
   }
   __syncthreads();
   unsigned long long base = s_base;
-  int32_t ml = 0;
   for (uint64_t s0 = a; s0 < b; s0 += 256) {
     const uint64_t s = s0 + threadIdx.x;
     const bool used = s < b && fkeys[s] != 0;
@@ -1416,22 +1438,10 @@ __global__ __launch_bounds__(256) void k_final_compact(const unsigned long long 
       const unsigned long long i = base + before + __popcll(m & ((1ull << lane) - 1ull));
       vslot[i] = (uint32_t)s;
       vidx[i] = (uint32_t)i;
-      const uint64_t cs = cand_str[freps[s] - 1];
-      const int32_t l = (int32_t)(cs & 0xFFFF);
-      ml = max(ml, l);
-      uint32_t orv = 0;
-      for (int32_t j = 0; j < l; j++) orv |= pool[(cs >> 16) + j];
-      wide |= orv >= 128u ? 1 : 0;
     }
     base += tot;
     __syncthreads();
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    ml = max(ml, __shfl_xor(ml, o, 64));
-    wide |= __shfl_xor(wide, o, 64);
-  }
-  if (lane == 0 && ml > 0) atomicMax(maxlen, ml);
-  if (lane == 0 && wide) atomicOr(maxlen + 1, 1);
 }
 
 // key word w (units 4w..4w+3, big-endian, zero padded) of the term at each order position
@@ -2858,14 +2868,14 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   SME_HIP(hipMemsetAsync(fkeys, 0, fcap * 8, st));
   SME_HIP(hipMemsetAsync(freps, 0, fcap * 8, st));
   SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
+  int32_t *maxlen = reinterpret_cast<int32_t *>(cnt + 12);
   if (ncand > 0)
     hipLaunchKernelGGL(k_final_insert, dim3(grid_for(ncand)), dim3(256), 0, st, co.pool, co.cand_str, ncand, fkeys,
-                       freps, fcap - 1, cand_final, ovf);
+                       freps, fcap - 1, cand_final, ovf, maxlen);
   uint32_t *vslot = W[W_VSLOT].as<uint32_t>(ncand + 1);
   uint32_t *vidx = W[W_VIDX].as<uint32_t>(ncand + 1);
-  int32_t *maxlen = reinterpret_cast<int32_t *>(cnt + 12);
   hipLaunchKernelGGL(k_final_compact, dim3(grid_for((int64_t)fcap)), dim3(256), 0, st, fkeys, freps, fcap - 1,
-                     co.cand_str, co.pool, cnt + 1, vslot, vidx, maxlen);
+                     co.cand_str, co.pool, cnt + 1, vslot, vidx);
   SME_CHECK_LAUNCH();
   unsigned long long hv[13];
   SME_HIP(hipMemcpyAsync(hv, cnt, sizeof hv, hipMemcpyDeviceToHost, st));
