@@ -1406,7 +1406,8 @@ __global__ void k_final_insert(const uint16_t *pool, const uint64_t *cand_str, i
 __global__ __launch_bounds__(256) void k_final_compact(const unsigned long long *fkeys,
                                                        const unsigned long long *freps, uint64_t fmask,
                                                        const uint64_t *cand_str, const uint16_t *pool,
-                                                       unsigned long long *nV, uint32_t *vslot, uint32_t *vidx) {
+                                                       unsigned long long *nV, uint32_t *vslot, uint32_t *vidx,
+                                                       uint64_t *vcs) {
   __shared__ uint32_t s_w[4];
   __shared__ unsigned long long s_base;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1438,6 +1439,7 @@ __global__ __launch_bounds__(256) void k_final_compact(const unsigned long long 
       const unsigned long long i = base + before + __popcll(m & ((1ull << lane) - 1ull));
       vslot[i] = (uint32_t)s;
       vidx[i] = (uint32_t)i;
+      vcs[i] = cand_str[freps[s] - 1];  // the term's pool string, so later passes skip two gathers
     }
     base += tot;
     __syncthreads();
@@ -1447,10 +1449,10 @@ __global__ __launch_bounds__(256) void k_final_compact(const unsigned long long 
 // key word w (units 4w..4w+3, big-endian, zero padded) of the term at each order position
 // (cpw units of ub bits per word: 4 x 16 in general, 9 x 7 when every unit is
 // ASCII -- unit order is code order either way, so fewer words to sort)
-__global__ void k_term_word(const uint32_t *order, int64_t V, const uint32_t *vslot, const unsigned long long *freps,
-                            const uint64_t *cand_str, const uint16_t *pool, int w, int cpw, int ub, uint64_t *key) {
+__global__ void k_term_word(const uint32_t *order, int64_t V, const uint64_t *vcs, const uint16_t *pool, int w,
+                            int cpw, int ub, uint64_t *key) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t cs = cand_str[freps[vslot[order[i]]] - 1];
+    uint64_t cs = vcs[order[i]];
     const uint16_t *u = pool + (cs >> 16);
     int l = (int)(cs & 0xFFFF);
     uint64_t k = 0;
@@ -1503,21 +1505,19 @@ __global__ void k_final_fixup(uint32_t *order, int64_t V, const uint32_t *vslot,
 }
 
 // rank of every final slot; term lengths in rank order
-__global__ void k_final_rank(const uint32_t *order, int64_t V, const uint32_t *vslot,
-                             const unsigned long long *freps, const uint64_t *cand_str, int32_t *rank_of_slot,
-                             int64_t *term_len) {
+__global__ void k_final_rank(const uint32_t *order, int64_t V, const uint32_t *vslot, const uint64_t *vcs,
+                             int32_t *rank_of_slot, int64_t *term_len) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t s = vslot[order[i]];
-    rank_of_slot[s] = (int32_t)i;
-    term_len[i] = (int64_t)(cand_str[freps[s] - 1] & 0xFFFF);
+    const uint32_t o = order[i];
+    rank_of_slot[vslot[o]] = (int32_t)i;
+    term_len[i] = (int64_t)(vcs[o] & 0xFFFF);
   }
 }
 
-__global__ void k_final_gather(const uint32_t *order, int64_t V, const uint32_t *vslot,
-                               const unsigned long long *freps, const uint64_t *cand_str, const uint16_t *pool,
+__global__ void k_final_gather(const uint32_t *order, int64_t V, const uint64_t *vcs, const uint16_t *pool,
                                const int64_t *term_off, uint16_t *term_chars) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t cs = cand_str[freps[vslot[order[i]]] - 1];
+    uint64_t cs = vcs[order[i]];
     const uint16_t *w = pool + (cs >> 16);
     int l = (int)(cs & 0xFFFF);
     for (int k = 0; k < l; k++) term_chars[term_off[i] + k] = w[k];
@@ -2537,7 +2537,7 @@ enum {
   W_TOK, W_NTOK, W_RKEYS, W_RREPS, W_POOL, W_CKEY, W_CSTR, W_NOUT, W_LONG, W_FKEYS, W_FREPS, W_CFINAL,
   W_VSLOT, W_KHI, W_KLO, W_VIDX, W_T0, W_T1, W_T2, W_T3, W_RAWTERM, W_MULTI, W_PERM, W_PREC, W_PTERM, W_PVAL,
   W_MAXNOUT, W_SS, W_SE, W_SC, W_RLIST, W_RFLAG, W_POFF, W_OVFKEY, W_FREC, W_LT, W_RADIX, W_NTOK2, W_BIGL2,
-  W_BIGCAP, W_SEGB,
+  W_BIGCAP, W_SEGB, W_VCS,
   W_NSLOTS
 };
 constexpr int kBuildWs = 64;  // build slots live at ctx->ws[64..127]
@@ -2874,8 +2874,9 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
                        freps, fcap - 1, cand_final, ovf, maxlen);
   uint32_t *vslot = W[W_VSLOT].as<uint32_t>(ncand + 1);
   uint32_t *vidx = W[W_VIDX].as<uint32_t>(ncand + 1);
+  uint64_t *vcs = W[W_VCS].as<uint64_t>(ncand + 1);
   hipLaunchKernelGGL(k_final_compact, dim3(grid_for((int64_t)fcap)), dim3(256), 0, st, fkeys, freps, fcap - 1,
-                     co.cand_str, co.pool, cnt + 1, vslot, vidx);
+                     co.cand_str, co.pool, cnt + 1, vslot, vidx, vcs);
   SME_CHECK_LAUNCH();
   unsigned long long hv[13];
   SME_HIP(hipMemcpyAsync(hv, cnt, sizeof hv, hipMemcpyDeviceToHost, st));
@@ -2907,8 +2908,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     uint32_t *ord_a = vidx, *ord_b = order;
     size_t tbb = 0;
     for (int w = nwords - 1; w >= 0; w--) {
-      hipLaunchKernelGGL(k_term_word, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V, vslot, freps, co.cand_str,
-                         co.pool, w, cpw, ub, kw);
+      hipLaunchKernelGGL(k_term_word, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V, vcs, co.pool, w, cpw, ub, kw);
       SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, kw, kw2, ord_a, ord_b, (int)V, 0, kbits, st));
       SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, kw, kw2, ord_a, ord_b, (int)V, 0, kbits, st));
       std::swap(ord_a, ord_b);
@@ -2919,15 +2919,14 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       hipLaunchKernelGGL(k_final_fixup, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, freps, co.cand_str,
                          co.pool);
     int64_t *tlen = W[W_T0].as<int64_t>(V + 1);
-    hipLaunchKernelGGL(k_final_rank, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, freps, co.cand_str,
-                       rank_of_slot, tlen);
+    hipLaunchKernelGGL(k_final_rank, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, vcs, rank_of_slot, tlen);
     SME_HIP(hipMemsetAsync(tlen + V, 0, sizeof(int64_t), st));
     SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, tlen, term_off, (int)V + 1, st));
     SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, tlen, term_off, (int)V + 1, st));
     int64_t tchars = d2h(term_off + V, st);
     uint16_t *term_chars = ix->d_term_chars.as<uint16_t>(tchars + 1);
-    hipLaunchKernelGGL(k_final_gather, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, freps, co.cand_str,
-                       co.pool, term_off, term_chars);
+    hipLaunchKernelGGL(k_final_gather, dim3(grid_for(V)), dim3(256), 0, st, order, V, vcs, co.pool, term_off,
+                       term_chars);
     SME_CHECK_LAUNCH();
   } else {
     SME_HIP(hipMemsetAsync(term_off, 0, sizeof(int64_t), st));
