@@ -2243,22 +2243,63 @@ __global__ void k_gram_ids(const uint64_t *k, const uint32_t *incl, int64_t P, i
 // Segmented counting sort: the term CSR already delimits the segments and tf is a
 // small integer, so one read + one write per posting replaces a full radix sort.
 // ============================================================================
+constexpr int kTfTiny = 8;      // segments up to this: one thread each (insertion sort in registers)
 constexpr int kTfSmall = 64;    // segments up to one wave chunk: rank by lane compares
 constexpr int kTfMedium = 8192; // up to this: 4-wave blocks; beyond: 16-wave blocks
 constexpr int kTfSortMaxTf = 1023;  // LDS counters (max_tf + 1) x 16 x 4 B <= 64 KiB; above: radix sort
 
-// segments of length <= kTfSmall: one wave each; output rank of lane i =
-// #{j : tf_j > tf_i} + #{j < i : tf_j == tf_i}
-__global__ __launch_bounds__(256) void k_tfsort_small(const int64_t *__restrict__ off, int64_t V,
+// segments of length <= kTfTiny (every docid term, most rare words): one thread
+// each, a stable insertion sort by tf desc in registers
+__global__ __launch_bounds__(256) void k_tfsort_tiny(const int64_t *__restrict__ off, int64_t V,
+                                                     const int32_t *__restrict__ docno_d,
+                                                     const int32_t *__restrict__ tf_d, int32_t *docno_o,
+                                                     int32_t *tf_o) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = off[s];
+    const int n = (int)(off[s + 1] - b);
+    if (n > kTfTiny || n == 0) continue;
+    int32_t t[kTfTiny], d[kTfTiny];
+#pragma unroll
+    for (int j = 0; j < kTfTiny; j++) {
+      t[j] = j < n ? tf_d[b + j] : INT_MIN;  // INT_MIN: padding sinks to the end
+      d[j] = j < n ? docno_d[b + j] : 0;
+    }
+#pragma unroll
+    for (int j = 1; j < kTfTiny; j++) {  // stable: an item passes only strictly smaller tfs
+#pragma unroll
+      for (int k = j; k > 0; k--) {
+        if (t[k - 1] < t[k]) {
+          const int32_t x = t[k - 1], y = d[k - 1];
+          t[k - 1] = t[k];
+          d[k - 1] = d[k];
+          t[k] = x;
+          d[k] = y;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kTfTiny; j++)
+      if (j < n) {
+        docno_o[b + j] = d[j];
+        tf_o[b + j] = t[j];
+      }
+  }
+}
+
+// segments of length in (kTfTiny, kTfSmall] (from a class list): one wave each;
+// output rank of lane i = #{j : tf_j > tf_i} + #{j < i : tf_j == tf_i}
+__global__ __launch_bounds__(256) void k_tfsort_small(const int64_t *__restrict__ off,
+                                                      const int32_t *__restrict__ seg,
+                                                      const unsigned long long *__restrict__ nseg,
                                                       const int32_t *__restrict__ docno_d,
                                                       const int32_t *__restrict__ tf_d, int32_t *docno_o,
                                                       int32_t *tf_o) {
   const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  for (int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); s < V; s += nw) {
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6), ns = (int64_t)*nseg;
+  for (int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); q < ns; q += nw) {
+    const int64_t s = seg[q];
     const int64_t b = off[s];
     const int n = (int)(off[s + 1] - b);
-    if (n > kTfSmall || n == 0) continue;  // wave-uniform
     const bool v = lane < n;
     const int32_t t = v ? tf_d[b + lane] : 0, d = v ? docno_d[b + lane] : 0;
     int r = 0;
@@ -2363,23 +2404,24 @@ constexpr int kTfTile = 4096;
 // one global atomic per block and list; list order is free (segments are
 // independent and their output ranges fixed)
 __global__ __launch_bounds__(256) void k_tf_classify(const int64_t *__restrict__ off, int64_t V, int32_t *med,
-                                                     int32_t *large, unsigned long long *ctr) {
-  __shared__ unsigned int s_n[2];
-  __shared__ unsigned long long s_b[2];
+                                                     int32_t *large, int32_t *small, unsigned long long *ctr) {
+  __shared__ unsigned int s_n[3];
+  __shared__ unsigned long long s_b[3];
   for (int64_t s0 = (int64_t)blockIdx.x * 256; s0 < V; s0 += (int64_t)gridDim.x * 256) {  // block-uniform
     const int64_t s = s0 + threadIdx.x;
     const int64_t n = s < V ? off[s + 1] - off[s] : 0;
-    const bool is_l = n > kTfMedium, is_m = n > kTfSmall && !is_l;
-    if (threadIdx.x < 2) s_n[threadIdx.x] = 0;
+    const int cls = n > kTfMedium ? 1 : n > kTfSmall ? 0 : n > kTfTiny ? 2 : -1;  // ctr index
+    if (threadIdx.x < 3) s_n[threadIdx.x] = 0;
     __syncthreads();
-    unsigned int pm = 0, pl = 0;
-    if (is_m) pm = atomicAdd(&s_n[0], 1u);
-    if (is_l) pl = atomicAdd(&s_n[1], 1u);
+    unsigned int pos = 0;
+    if (cls >= 0) pos = atomicAdd(&s_n[cls], 1u);
     __syncthreads();
-    if (threadIdx.x < 2) s_b[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&ctr[threadIdx.x], (unsigned long long)s_n[threadIdx.x]) : 0ull;
+    if (threadIdx.x < 3)
+      s_b[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&ctr[threadIdx.x], (unsigned long long)s_n[threadIdx.x]) : 0ull;
     __syncthreads();
-    if (is_m) med[s_b[0] + pm] = (int32_t)s;
-    if (is_l) large[s_b[1] + pl] = (int32_t)s;
+    if (cls == 0) med[s_b[0] + pos] = (int32_t)s;
+    if (cls == 1) large[s_b[1] + pos] = (int32_t)s;
+    if (cls == 2) small[s_b[2] + pos] = (int32_t)s;
     __syncthreads();
   }
 }
@@ -3337,15 +3379,18 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   int32_t *docno_o = ix->d_docno_o.as<int32_t>(PP + 1), *tf_o = ix->d_tf_o.as<int32_t>(PP + 1);
   if (PP > 0 && max_tf <= kTfSortMaxTf) {
     // segmented counting sort over the term CSR (no full-width key sort)
-    hipLaunchKernelGGL(k_tfsort_small, dim3(grid_for(Vi * 64, 256, 8192)), dim3(256), 0, st, off, Vi, docno_d, tf_d,
-                       docno_o, tf_o);
+    hipLaunchKernelGGL(k_tfsort_tiny, dim3(grid_for(Vi)), dim3(256), 0, st, off, Vi, docno_d, tf_d, docno_o, tf_o);
     // medium and large segments as lists (a grid-stride walk over all V terms costs a
     // dependent offset load per term and block)
-    int64_t *ntl = W[W_FKEYS].as<int64_t>(2 * (Vi + 1)), *toff = W[W_FREPS].as<int64_t>(Vi + 1);
-    int32_t *seg_med = reinterpret_cast<int32_t *>(ntl + Vi + 1), *seg_large = seg_med + Vi;
-    unsigned long long *nseg = cnt + 28;  // [0] medium, [1] large
-    SME_HIP(hipMemsetAsync(nseg, 0, 2 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_tf_classify, dim3(grid_for(Vi)), dim3(256), 0, st, off, Vi, seg_med, seg_large, nseg);
+    int64_t *ntl = W[W_FKEYS].as<int64_t>(3 * (Vi + 1)), *toff = W[W_FREPS].as<int64_t>(Vi + 1);
+    int32_t *seg_med = reinterpret_cast<int32_t *>(ntl + Vi + 1), *seg_large = seg_med + Vi,
+            *seg_small = seg_large + Vi;
+    unsigned long long *nseg = cnt + 28;  // [0] medium, [1] large, [2] small
+    SME_HIP(hipMemsetAsync(nseg, 0, 3 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_tf_classify, dim3(grid_for(Vi)), dim3(256), 0, st, off, Vi, seg_med, seg_large, seg_small,
+                       nseg);
+    hipLaunchKernelGGL(k_tfsort_small, dim3(grid_for(Vi * 64, 256, 8192)), dim3(256), 0, st, off, seg_small, nseg + 2,
+                       docno_d, tf_d, docno_o, tf_o);
     const size_t lds4 = (size_t)(max_tf + 1) * 4 * sizeof(int32_t);
     hipLaunchKernelGGL(k_tfsort_block<4>, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(Vi, 1), 4096)),
                        dim3(256), lds4, st, off, Vi, docno_d, tf_d, docno_o, tf_o, seg_med, nseg, max_tf);
