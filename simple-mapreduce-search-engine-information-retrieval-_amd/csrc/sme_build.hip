@@ -2245,7 +2245,8 @@ __global__ void k_gram_ids(const uint64_t *k, const uint32_t *incl, int64_t P, i
 // ============================================================================
 constexpr int kTfTiny = 8;      // segments up to this: one thread each (insertion sort in registers)
 constexpr int kTfSmall = 64;    // segments up to one wave chunk: rank by lane compares
-constexpr int kTfMedium = 8192; // up to this: 4-wave blocks; beyond: 16-wave blocks
+constexpr int kTfWave = 512;    // up to this: one-wave blocks (no cross-wave barriers)
+constexpr int kTfMedium = 8192; // up to this: 4-wave blocks; beyond: tiles
 constexpr int kTfSortMaxTf = 1023;  // LDS counters (max_tf + 1) x 16 x 4 B <= 64 KiB; above: radix sort
 
 // segments of length <= kTfTiny (every docid term, most rare words): one thread
@@ -2404,24 +2405,26 @@ constexpr int kTfTile = 4096;
 // one global atomic per block and list; list order is free (segments are
 // independent and their output ranges fixed)
 __global__ __launch_bounds__(256) void k_tf_classify(const int64_t *__restrict__ off, int64_t V, int32_t *med,
-                                                     int32_t *large, int32_t *small, unsigned long long *ctr) {
-  __shared__ unsigned int s_n[3];
-  __shared__ unsigned long long s_b[3];
+                                                     int32_t *large, int32_t *small, int32_t *wave,
+                                                     unsigned long long *ctr) {
+  __shared__ unsigned int s_n[4];
+  __shared__ unsigned long long s_b[4];
   for (int64_t s0 = (int64_t)blockIdx.x * 256; s0 < V; s0 += (int64_t)gridDim.x * 256) {  // block-uniform
     const int64_t s = s0 + threadIdx.x;
     const int64_t n = s < V ? off[s + 1] - off[s] : 0;
-    const int cls = n > kTfMedium ? 1 : n > kTfSmall ? 0 : n > kTfTiny ? 2 : -1;  // ctr index
-    if (threadIdx.x < 3) s_n[threadIdx.x] = 0;
+    const int cls = n > kTfMedium ? 1 : n > kTfWave ? 0 : n > kTfSmall ? 3 : n > kTfTiny ? 2 : -1;  // ctr index
+    if (threadIdx.x < 4) s_n[threadIdx.x] = 0;
     __syncthreads();
     unsigned int pos = 0;
     if (cls >= 0) pos = atomicAdd(&s_n[cls], 1u);
     __syncthreads();
-    if (threadIdx.x < 3)
+    if (threadIdx.x < 4)
       s_b[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&ctr[threadIdx.x], (unsigned long long)s_n[threadIdx.x]) : 0ull;
     __syncthreads();
     if (cls == 0) med[s_b[0] + pos] = (int32_t)s;
     if (cls == 1) large[s_b[1] + pos] = (int32_t)s;
     if (cls == 2) small[s_b[2] + pos] = (int32_t)s;
+    if (cls == 3) wave[s_b[3] + pos] = (int32_t)s;
     __syncthreads();
   }
 }
@@ -3384,16 +3387,18 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     // dependent offset load per term and block)
     int64_t *ntl = W[W_FKEYS].as<int64_t>(3 * (Vi + 1)), *toff = W[W_FREPS].as<int64_t>(Vi + 1);
     int32_t *seg_med = reinterpret_cast<int32_t *>(ntl + Vi + 1), *seg_large = seg_med + Vi,
-            *seg_small = seg_large + Vi;
-    unsigned long long *nseg = cnt + 28;  // [0] medium, [1] large, [2] small
-    SME_HIP(hipMemsetAsync(nseg, 0, 3 * sizeof(unsigned long long), st));
+            *seg_small = seg_large + Vi, *seg_wave = seg_small + Vi;
+    unsigned long long *nseg = cnt + 28;  // [0] medium, [1] large, [2] small, [3] wave-sized
+    SME_HIP(hipMemsetAsync(nseg, 0, 4 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_tf_classify, dim3(grid_for(Vi)), dim3(256), 0, st, off, Vi, seg_med, seg_large, seg_small,
-                       nseg);
+                       seg_wave, nseg);
     hipLaunchKernelGGL(k_tfsort_small, dim3(grid_for(Vi * 64, 256, 8192)), dim3(256), 0, st, off, seg_small, nseg + 2,
                        docno_d, tf_d, docno_o, tf_o);
     const size_t lds4 = (size_t)(max_tf + 1) * 4 * sizeof(int32_t);
     hipLaunchKernelGGL(k_tfsort_block<4>, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(Vi, 1), 4096)),
                        dim3(256), lds4, st, off, Vi, docno_d, tf_d, docno_o, tf_o, seg_med, nseg, max_tf);
+    hipLaunchKernelGGL(k_tfsort_block<1>, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(Vi, 1), 32768)),
+                       dim3(64), lds4 / 4, st, off, Vi, docno_d, tf_d, docno_o, tf_o, seg_wave, nseg + 3, max_tf);
     // large segments: tiles spread over the whole chip
     hipLaunchKernelGGL(k_tf_ntiles, dim3(grid_for(Vi + 1)), dim3(256), 0, st, off, seg_large, nseg + 1, Vi, ntl);
     size_t tbb = 0;
