@@ -2466,7 +2466,19 @@ __global__ __launch_bounds__(256) void k_tf_tile_count(const int64_t *__restrict
     const int64_t b = off[s] + (tau - toff[q]) * kTfTile, e = min(off[s + 1], b + (int64_t)kTfTile);
     for (int j = lane; j < F; j += 64) hw[j] = 0;
     __builtin_amdgcn_wave_barrier();
-    for (int64_t i = b + lane; i < e; i += 64) atomicAdd(&hw[max_tf - tf_d[i]], 1);
+    // per 64-posting chunk: one LDS add per distinct tf (ballot groups) -- most
+    // postings have tf 1, and per-lane atomics on that one counter serialise
+    for (int64_t c = b; c < e; c += 64) {
+      const bool v = c + lane < e;
+      const int32_t t = v ? tf_d[c + lane] : -1;
+      uint64_t pend = __ballot(v);
+      while (pend) {
+        const int32_t tv = __shfl(t, __ffsll((unsigned long long)pend) - 1, 64);
+        const uint64_t m = __ballot(t == tv);
+        if (lane == 0) hw[max_tf - tv] += __popcll(m);
+        pend &= ~m;
+      }
+    }
     __builtin_amdgcn_wave_barrier();
     for (int j = lane; j < F; j += 64) tcnt[tau * F + j] = hw[j];
     __builtin_amdgcn_wave_barrier();
