@@ -26,13 +26,17 @@
 namespace sme {
 namespace {
 
-constexpr int kRsNT = 1024;                 // threads per block (16 waves)
+#ifndef SME_RSNT
+#define SME_RSNT 512
+#endif
+constexpr int kRsNT = SME_RSNT;             // threads per block (8 waves: two blocks per CU overlap their phases)
 constexpr int kRsWaves = kRsNT / 64;
 constexpr int kRsIPL = 16;                  // items per lane
-constexpr int kRsTile = kRsNT * kRsIPL;     // 16384 items per tile
+constexpr int kRsTile = kRsNT * kRsIPL;     // items per tile
 constexpr int kRsWaveItems = 64 * kRsIPL;   // 1024 contiguous items per wave
 constexpr int kRsMaxBits = 11;
 constexpr int kRsMaxBins = 1 << kRsMaxBits;
+constexpr int kRsBPT = kRsMaxBins / kRsNT;  // digits per thread in the scatter's tile scan
 constexpr int kRsGroups = 256;              // tile groups of the column scan
 
 // Gather mode (first pass after the single-pass aggregation): pair x of the
@@ -60,22 +64,25 @@ __device__ __forceinline__ int64_t gather_pos(const Gather &g, int64_t x, int64_
 // A wave's 1024 items span a few records: lane j loads record rec0 + j's pair
 // start and region delta into LDS once, so the per-item walk reads LDS and the
 // item loads are not held behind dependent global loads (vmcnt is in order).
-// Walks past 64 records fall back to the global walk.
+// Walks past kGRec records fall back to the global walk.
+constexpr int kGRec = 48;  // (LDS: two 512-thread scatter blocks per CU)
 __device__ __forceinline__ int64_t gather_table(const Gather &g, int64_t x0, int lane, int64_t *gx, int64_t *gdl) {
   const int64_t rec0 = g.crec[x0 >> 10];
   const int64_t r = rec0 + lane;
-  gx[lane] = r <= g.nrec ? g.xoff[r] : INT64_MAX;
-  gdl[lane] = r < g.nrec ? g.reg[r] - g.xoff[r] : 0;
-  if (lane == 0) gx[64] = rec0 + 64 <= g.nrec ? g.xoff[rec0 + 64] : INT64_MAX;
+  if (lane < kGRec) {
+    gx[lane] = r <= g.nrec ? g.xoff[r] : INT64_MAX;
+    gdl[lane] = r < g.nrec ? g.reg[r] - g.xoff[r] : 0;
+  }
+  if (lane == 0) gx[kGRec] = rec0 + kGRec <= g.nrec ? g.xoff[rec0 + kGRec] : INT64_MAX;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   return rec0;
 }
 __device__ __forceinline__ int64_t gather_at(const Gather &g, int64_t x, int &j, const int64_t *gx, const int64_t *gdl,
                                              int64_t rec0) {
-  while (j < 63 && x >= gx[j + 1]) j++;
+  while (j < kGRec - 1 && x >= gx[j + 1]) j++;
   if (x < gx[j + 1]) return x + gdl[j];
-  int64_t rec = rec0 + 63, nx = g.xoff[rec + 1], dl = g.reg[rec] - g.xoff[rec];
+  int64_t rec = rec0 + kGRec - 1, nx = g.xoff[rec + 1], dl = g.reg[rec] - g.xoff[rec];
   return gather_pos(g, x, rec, nx, dl);
 }
 __global__ void k_rs_chunk_rec(const int64_t *__restrict__ xoff, int64_t nrec, int64_t P, int64_t *__restrict__ crec) {
@@ -101,7 +108,7 @@ __global__ __launch_bounds__(kRsNT) void k_rs_count(const uint32_t *__restrict__
   const uint32_t mask = (uint32_t)nbins - 1u;
   const int64_t n = min((int64_t)kRsTile, P - t0);
   if (g.reg != nullptr) {
-    __shared__ int64_t gx_all[kRsWaves][65], gdl_all[kRsWaves][64];
+    __shared__ int64_t gx_all[kRsWaves][kGRec + 1], gdl_all[kRsWaves][kGRec];
     const int lane = tid & 63, w = tid >> 6;
     const int64_t wb = t0 + (int64_t)w * kRsWaveItems;
     if (wb < P) {
@@ -243,7 +250,7 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
   const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t k[kRsIPL], v[kRsIPL], pos[kRsIPL];
   if (g.reg != nullptr) {
-    __shared__ int64_t gx_all[kRsWaves][65], gdl_all[kRsWaves][64];
+    __shared__ int64_t gx_all[kRsWaves][kGRec + 1], gdl_all[kRsWaves][kGRec];
     int64_t rec0 = 0;
     if (wb < n) rec0 = gather_table(g, t0 + wb, lane, gx_all[w], gdl_all[w]);
     int j = 0;
@@ -289,16 +296,18 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
   __syncthreads();
   // 2. tile slot of each (wave, digit): digits in order, waves in order
   {
-    const int b0 = 2 * tid;
-    uint32_t t0c = 0, t1c = 0;
-    if (b0 < nbins) {
+    const int b0 = kRsBPT * tid;  // this thread's digits b0 .. b0 + kRsBPT - 1
+    uint32_t tc[kRsBPT];
+    uint32_t s2 = 0;
 #pragma unroll
-      for (int x = 0; x < kRsWaves; x++) {
-        t0c += wc[x * kRsMaxBins + b0];
-        t1c += wc[x * kRsMaxBins + b0 + 1];
+    for (int q = 0; q < kRsBPT; q++) {
+      tc[q] = 0;
+      if (b0 + q < nbins) {
+#pragma unroll
+        for (int x = 0; x < kRsWaves; x++) tc[q] += wc[x * kRsMaxBins + b0 + q];
       }
+      s2 += tc[q];
     }
-    const uint32_t s2 = t0c + t1c;
     uint32_t incl = s2;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(incl, o, 64);
@@ -308,18 +317,19 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
     __syncthreads();
     uint32_t ex = incl - s2;
     for (int j = 0; j < w; j++) ex += ws[j];
-    if (b0 < nbins) {
-      uint32_t r0 = ex, r1 = ex + t0c;
-      gd[b0] = offs[tile * nbins + b0] - r0;
-      gd[b0 + 1] = offs[tile * nbins + b0 + 1] - r1;
 #pragma unroll
-      for (int x = 0; x < kRsWaves; x++) {
-        const uint32_t c0 = wc[x * kRsMaxBins + b0], c1 = wc[x * kRsMaxBins + b0 + 1];
-        wc[x * kRsMaxBins + b0] = (uint16_t)r0;
-        wc[x * kRsMaxBins + b0 + 1] = (uint16_t)r1;
-        r0 += c0;
-        r1 += c1;
+    for (int q = 0; q < kRsBPT; q++) {
+      if (b0 + q < nbins) {
+        uint32_t r = ex;
+        gd[b0 + q] = offs[tile * nbins + b0 + q] - r;
+#pragma unroll
+        for (int x = 0; x < kRsWaves; x++) {
+          const uint32_t c = wc[x * kRsMaxBins + b0 + q];
+          wc[x * kRsMaxBins + b0 + q] = (uint16_t)r;
+          r += c;
+        }
       }
+      ex += tc[q];
     }
   }
   __syncthreads();

@@ -120,7 +120,7 @@ def test_build_big_records_interleaved(sme, synth):
 def test_build_many_tiny_records(sme):
     """Thousands of records with 0-3 words (a few pairs each, some only the
     docid): a wave's 1024 pairs of the term sort's gather pass span hundreds of
-    records, past its 64-record LDS table (the global walk takes over)."""
+    records, past its 48-record LDS table (the global walk takes over)."""
     rng = random.Random(11)
     docs, ids = [], []
     for i in range(3000):
