@@ -2541,10 +2541,14 @@ __global__ __launch_bounds__(256) void k_tf_tile_place(const int64_t *__restrict
     const int64_t b = sb + (tau - toff[q]) * kTfTile, e = min(off[s + 1], b + (int64_t)kTfTile);
     for (int j = lane; j < F; j += 64) hw[j] = tcnt[tau * F + j];
     __builtin_amdgcn_wave_barrier();
+    // the next chunk's (tf, docno) are loaded before this chunk's placement
+    int32_t tn = b + lane < e ? tf_d[b + lane] : -1, dnx = b + lane < e ? docno_d[b + lane] : 0;
     for (int64_t c = b; c < e; c += 64) {
-      const int64_t i = c + lane;
-      const bool v = i < e;
-      const int32_t t = v ? tf_d[i] : -1, d = v ? docno_d[i] : 0;
+      const bool v = c + lane < e;
+      const int32_t t = tn, d = dnx;
+      const int64_t in = c + 64 + lane;
+      tn = in < e ? tf_d[in] : -1;
+      dnx = in < e ? docno_d[in] : 0;
       uint64_t pend = __ballot(v);
       while (pend) {
         const int32_t tv = __shfl(t, __ffsll((unsigned long long)pend) - 1, 64);
