@@ -160,7 +160,18 @@ def main():
     N, V, P = ix.N, ix.V, ix.P
     t_max = dt
     tot_bytes = nbytes
+    df_ex = None
     if dist is not None:
+        # true-df exchange, once per index, untimed: fingerprint
+        # all_gather + unique + df all_reduce over RCCL (dist.global_df_index)
+        D2 = importlib.import_module(PKG + ".dist")
+        df_ex = {}
+        barrier()
+        t_ex = time.perf_counter()
+        D2.global_df_index(ix, timings=df_ex)
+        barrier()
+        df_ex["total_ms"] = round((time.perf_counter() - t_ex) * 1e3, 3)
+        df_ex = {k2: (round(v, 3) if isinstance(v, float) else v) for k2, v in df_ex.items()}
         tt = torch.tensor([dt, float(nbytes), float(N), float(V), float(P)], dtype=torch.float64, device="cuda")
         ts = [torch.zeros_like(tt) for _ in range(world)]
         dist.all_gather(ts, tt)
@@ -212,6 +223,8 @@ def main():
     }
     if query is not None:
         result["query"] = query
+    if df_ex is not None:
+        result["df_exchange_untimed"] = df_ex
     qinternal = None
     if query is not None:
         qinternal = (query.pop("_terms"), query.pop("_qoff"), query.pop("_out"))
@@ -252,13 +265,17 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     out_d = torch.empty((a.queries, k), dtype=torch.int32, device="cuda")
     out_s = torch.empty((a.queries, k), dtype=torch.float64, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
+    # query-side heavy rows of the index: built once per index (like the
+    # reference's forward-index job), outside the per-batch timing, reported
+    qidx_ms = ix.prepare_queries(stream)
 
     def qstep():
         ix.query_topk_device(d_terms.data_ptr(), d_qoff.data_ptr(), a.queries, k, out_d.data_ptr(), out_s.data_ptr(),
                              stream)
         if dist is not None:
-            # per-shard top-k lists -> global top-k (RCCL all-gather + merge, dist.merge_topk)
-            return importlib.import_module(PKG + ".dist").merge_topk(out_d, out_s, k)
+            # per-shard top-k lists -> global top-k of the queries this rank owns
+            # (RCCL query-owner all_to_all + merge, dist.merge_topk_owner)
+            return importlib.import_module(PKG + ".dist").merge_topk_owner(out_d, out_s, k)
         return out_d
 
     qstep()
@@ -307,9 +324,12 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     qtr = pmc_traffic(kname, a, detail=True)
     return {"metric": "top-%d queries/sec" % k, "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
             "terms_per_query": "U{2..8} drawn by df (seed %d)" % a.cfg["qseed"], "ms_per_batch": round(dt * 1e3, 3),
-            "prep_ms": qp_ms, "_terms": terms, "_qoff": qoff, "_out": (out_d, out_s),
-            "prep_what": "per batch, inside ms_per_batch: skip table (distinct batch terms x 1024-doc tiles), dense "
-                         "u8 tf + impact rows of terms with df >= span/32, heaviest-term query order",
+            "prep_ms": qp_ms, "query_index_build_ms": round(qidx_ms, 3),
+            "query_index_what": "once per index, not per batch: tf byte rows + 16/1024-doc block maxima of the "
+                                "terms with df >= span/32 (sme_index_prepare_queries)",
+            "_terms": terms, "_qoff": qoff, "_out": (out_d, out_s),
+            "prep_what": "per batch, inside ms_per_batch: skip table (distinct batch terms x 1024-doc tiles), "
+                         "impact tables of the batch terms, heaviest-term query order",
             "roofline": {"bound": "hbm", "kernel": kname, "kernel_ms": qk_ms,
                          "achieved": round(alg / t_k / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(alg / t_k / 1e9 / HBM_PEAK_GBS, 6), "traffic": qtr[0],
@@ -334,13 +354,12 @@ def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank):
     same = ~newt[1:ix.P]
     out["reduce_order"] = bool((((tf[1:] <= tf[:-1]) | ~same).all()) and
                                (((tf[1:] != tf[:-1]) | (dn[1:] > dn[:-1]) | ~same).all()))
-    del tf, dn
     # query-side CSR: docnos strictly ascending per term
     o2, dd, _ = ix.weights()
     out["docno_order"] = bool(np.array_equal(o2, off) and ((dd[1:] > dd[:-1]) | ~same).all())
     del dd, same, newt
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     if rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         blob, voff = synth.make_vocab(a.vocab, a.cfg["seed"])
         nv = int(O.lib().or_count_distinct_terms(blob, voff.ctypes.data, a.vocab))
@@ -355,22 +374,29 @@ def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank):
         base = (out_d[:nq].cpu().numpy(), out_s[:nq].cpu().numpy()) if hasattr(out_d, "cpu") else None
         d1, s1 = ix.query_topk(t_s, q_s, k)
         ok = base is None or (np.array_equal(base[0], d1) and np.array_equal(base[1], s1))
-        for env in ({"SME_QDENSE": "0"}, {"SME_QUERY_KERNEL": "stream"}):
-            if "SME_QUERY_KERNEL" in env and k > 32:
+        for opts in ({"heavy_div": 0}, {"query_kernel": 1}):
+            if "query_kernel" in opts and k > 32:
                 continue
-            old = {n: os.environ.get(n) for n in env}
-            os.environ.update(env)
             try:
+                for n, v in opts.items():
+                    ix.ctx.set_option(n, v)
                 d2, s2 = ix.query_topk(t_s, q_s, k)
             finally:
-                for n, v in old.items():
-                    if v is None:
-                        del os.environ[n]
-                    else:
-                        os.environ[n] = v
+                ix.ctx.set_option("heavy_div", 32)
+                ix.ctx.set_option("query_kernel", 0)
             ok = ok and np.array_equal(d1, d2) and np.array_equal(s1, s2)
         out["query_sample_kernels_agree"] = bool(ok)
         out["query_sample"] = nq
+        # the batch's first queries against a numpy restatement of rank() over the
+        # index's own postings (tests/common.np_rank; docnos + fp64 score bits)
+        import common
+        nr = min(100, nq)
+        good = True
+        for q in range(nr):
+            rd, rs = common.np_rank(off, dn, tf, terms[qoff[q]:qoff[q + 1]].tolist(), ix.N, k)
+            good = good and d1[q, :len(rd)].tolist() == rd and s1[q, :len(rd)].tolist() == rs
+        out["query_sample_vs_np_rank"] = bool(good)
+        out["query_sample_np_rank"] = nr
     return out
 
 

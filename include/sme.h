@@ -69,6 +69,19 @@ const char *sme_version(void);
 int sme_create(const sme_config *cfg, sme_ctx **out);
 void sme_destroy(sme_ctx *ctx);
 
+/* Path options of a context (no reference counterpart: the reference has one
+ * code path).  Every value gives bit-identical results; the options exist so
+ * tests can hold each device path to the others and benches can sweep them.
+ *   "query_kernel"  0 block-max pruned scoring (default), 1 streaming k_query (k <= 32)
+ *   "heavy_div"     heavy tf rows for terms with df >= docno span / div (default 32; 0 none)
+ *   "seed_tiles"    best-bound tiles scored before the sweep, 0..8 (default 4)
+ *   "query_order"   1 heaviest-term query order (default), 0 batch order
+ *   "agg_two_pass"  1 count + emit aggregation passes (default 0: single pass)
+ *   "tok_grid"      tokenizer workgroups, >= 1 (default 4096)
+ *   "raw_load_pct"  raw-vocabulary table load of the next build, 10..90 (default 40)
+ * Unknown names and out-of-range values are SME_EINVAL. */
+int sme_set_option(sme_ctx *ctx, const char *name, int64_t value);
+
 /* Docno mapping file bytes: int32 N, then N x writeUTF(docid), docids sorted
  * (TrecDocnoMapping.writeDocnoData format).  Uploaded once; docno lookup is
  * Arrays.binarySearch over {"", docids...} on the device. */
@@ -165,6 +178,13 @@ int sme_lookup_terms(sme_index *ix, const uint8_t *terms, const int64_t *offs, i
  * docno -1 / score 0 when fewer than k documents match. */
 int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq,
                    int k, int32_t *out_docno, double *out_score);
+
+/* Query-side structures of an index (the role the reference's forward index,
+ * BuildIntDocVectorsForwardIndex.java:84-158, plays for rank()): heavy-term tf
+ * rows and block maxima for the block-max scorer.  Built once per index (tf
+ * based: sme_index_reweight keeps them); sme_query_topk* builds them on first
+ * use when this was not called.  *ms (may be NULL) gets the device time. */
+int sme_index_prepare_queries(sme_index *ix, void *stream, float *ms);
 
 /* Same with all arrays already in device memory (timed path). */
 int sme_query_topk_device(sme_index *ix, const int32_t *d_term_ids, const int64_t *d_q_offsets,

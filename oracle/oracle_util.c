@@ -196,6 +196,56 @@ static void push_cp(jstr *out, unsigned cp) {
 
 /* String.toLowerCase(): per code point full lowercase mapping.  Final sigma is
  * mapped context-free to U+03C3 (parity unpinned, see gen_unicase.py). */
+/* code point ending at / starting at unit index i (surrogate pairs joined) */
+static unsigned cp_before(const uint16_t *a, int i, int *w) {
+  if (i >= 2 && is_lo(a[i - 1]) && is_hi(a[i - 2])) {
+    *w = 2;
+    return 0x10000 + (((unsigned)a[i - 2] - 0xD800) << 10) + ((unsigned)a[i - 1] - 0xDC00);
+  }
+  *w = 1;
+  return a[i - 1];
+}
+static unsigned cp_at(const uint16_t *a, int n, int i, int *w) {
+  if (is_hi(a[i]) && i + 1 < n && is_lo(a[i + 1])) {
+    *w = 2;
+    return 0x10000 + (((unsigned)a[i] - 0xD800) << 10) + ((unsigned)a[i + 1] - 0xDC00);
+  }
+  *w = 1;
+  return a[i];
+}
+static int in_ranges(const unsigned (*r)[2], int nr, unsigned cp) {
+  int lo = 0, hi = nr - 1;
+  while (lo <= hi) {
+    int m = (lo + hi) >> 1;
+    if (cp < r[m][0]) hi = m - 1;
+    else if (cp > r[m][1]) lo = m + 1;
+    else return 1;
+  }
+  return 0;
+}
+/* Final_Sigma context of U+03A3 at unit i of a[0..n): String.toLowerCase gives
+ * U+03C2 there (ConditionalSpecialCasing; Unicode rule, see tools/gen_unicase.py):
+ * a cased letter before it (case-ignorables skipped), none after it. */
+static int final_sigma(const uint16_t *a, int n, int i) {
+  int j = i, w;
+  unsigned c = 0;
+  int found = 0;
+  while (j > 0) {
+    c = cp_before(a, j, &w);
+    j -= w;
+    if (!in_ranges(UNISIGMA_CI, UNISIGMA_CI_N, c)) {
+      found = 1;
+      break;
+    }
+  }
+  if (!found || !in_ranges(UNISIGMA_CASED, UNISIGMA_CASED_N, c)) return 0;
+  for (j = i + 1; j < n; j += w) {
+    c = cp_at(a, n, j, &w);
+    if (!in_ranges(UNISIGMA_CI, UNISIGMA_CI_N, c)) return !in_ranges(UNISIGMA_CASED, UNISIGMA_CASED_N, c);
+  }
+  return 1;
+}
+
 void java_tolower(const uint16_t *a, int n, jstr *out) {
   for (int i = 0; i < n; i++) {
     unsigned cp = a[i];
@@ -204,7 +254,9 @@ void java_tolower(const uint16_t *a, int n, jstr *out) {
       cp = 0x10000 + (((unsigned)a[i] - 0xD800) << 10) + ((unsigned)a[i + 1] - 0xDC00);
       w = 2;
     }
-    if (cp < 0x80) {
+    if (cp == 0x03A3 && final_sigma(a, n, i)) {
+      js_push(out, 0x03C2);
+    } else if (cp < 0x80) {
       js_push(out, (uint16_t)((cp >= 'A' && cp <= 'Z') ? cp + 32 : cp));
     } else {
       const unicase_ent *e = unicase_find(cp);

@@ -44,7 +44,8 @@ EXPORTS = [
     "sme_index_device_arrays", "sme_index_term", "sme_tokenize", "sme_lookup_terms", "sme_query_topk",
     "sme_query_topk_device", "sme_last_build_profile", "sme_index_reweight", "sme_number_documents",
     "sme_build_chargram", "sme_build_chargram_device", "sme_chargram_partition_text", "sme_chargram_stats",
-    "sme_split_points", "sme_split_points_device", "sme_index_term_fingerprints",
+    "sme_split_points", "sme_split_points_device", "sme_index_term_fingerprints", "sme_set_option",
+    "sme_index_prepare_queries",
 ]
 
 
@@ -88,6 +89,8 @@ def lib():
     L.sme_index_term_fingerprints.argtypes = [vp, vp, vp]
     L.sme_split_points.argtypes = [vp, C.c_char_p, sz, C.c_int, C.POINTER(C.c_uint64)]
     L.sme_split_points_device.argtypes = [vp, vp, sz, C.c_int, vp, C.POINTER(C.c_uint64)]
+    L.sme_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
+    L.sme_index_prepare_queries.argtypes = [vp, vp, C.POINTER(C.c_float)]
     L.sme_synth_free.argtypes = [vp]
     L.sme_synth_free.restype = None
     _lib = L
@@ -167,6 +170,10 @@ class Context:
 
     def __del__(self):
         self.close()
+
+    def set_option(self, name, value):
+        """sme_set_option: a result-preserving path option (include/sme.h)."""
+        _check(lib().sme_set_option(self._h, name.encode(), int(value)))
 
     def load_docno_mapping(self, mapping_bytes):
         _check(lib().sme_load_docno_mapping(self._h, mapping_bytes, len(mapping_bytes)))
@@ -311,6 +318,13 @@ class Index:
                                     dn.ctypes.data_as(C.POINTER(C.c_int32)),
                                     sc.ctypes.data_as(C.POINTER(C.c_double))))
         return dn[:nq], sc[:nq]
+
+    def prepare_queries(self, stream=None):
+        """Build the query-side heavy rows now (else the first query batch does);
+        returns their device build time in ms."""
+        ms = C.c_float(0.0)
+        _check(lib().sme_index_prepare_queries(self._h, C.c_void_p(stream or 0), C.byref(ms)))
+        return ms.value
 
     def reweight(self, n_global, d_df_global=None, stream=None):
         """TF-IDF weights with all-reduced N (and df) of a doc-sharded index."""

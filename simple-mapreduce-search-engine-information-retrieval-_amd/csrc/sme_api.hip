@@ -159,6 +159,40 @@ int sme_create(const sme_config *cfg, sme_ctx **out) {
   });
 }
 
+int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
+  return guard([&] {
+    if (!cx || !name) throw sme::Error(SME_EINVAL, "null argument");
+    const std::string n(name);
+    auto range = [&](int64_t lo, int64_t hi) {
+      if (v < lo || v > hi) throw sme::Error(SME_EINVAL, "option " + n + " out of range");
+    };
+    if (n == "query_kernel") {
+      range(0, 1);
+      cx->opt_query_kernel = v;
+    } else if (n == "heavy_div") {
+      range(0, int64_t(1) << 40);
+      cx->opt_heavy_div = v;
+    } else if (n == "seed_tiles") {
+      range(0, 8);
+      cx->opt_seed_tiles = v;
+    } else if (n == "query_order") {
+      range(0, 1);
+      cx->opt_query_order = v;
+    } else if (n == "agg_two_pass") {
+      range(0, 1);
+      cx->opt_agg_two_pass = v;
+    } else if (n == "tok_grid") {
+      range(1, int64_t(1) << 30);
+      cx->opt_tok_grid = v;
+    } else if (n == "raw_load_pct") {
+      range(10, 90);
+      cx->opt_raw_load_pct = v;
+    } else {
+      throw sme::Error(SME_EINVAL, "unknown option " + n);
+    }
+  });
+}
+
 static void ctx_release(sme_ctx *cx) {
   (void)hipSetDevice(cx->device);
   (void)hipDeviceSynchronize();
@@ -434,6 +468,16 @@ int sme_lookup_terms(sme_index *ix, const uint8_t *terms, const int64_t *offs, i
   });
 }
 
+int sme_index_prepare_queries(sme_index *ix, void *stream, float *ms) {
+  return guard([&] {
+    if (!ix) throw sme::Error(SME_EINVAL, "null index");
+    if (ix->job != 0) throw sme::Error(SME_EINVAL, "not a TermKGramDocIndexer index");
+    set_device(ix->ctx);
+    sme::prepare_queries(ix, stream_of(ix->ctx, stream));
+    if (ms) *ms = ix->q_prep_ms;
+  });
+}
+
 int sme_query_topk_device(sme_index *ix, const int32_t *d_term_ids, const int64_t *d_q_offsets, int nq, int k,
                           int32_t *d_out_docno, double *d_out_score, void *stream) {
   return guard([&] {
@@ -500,7 +544,8 @@ int sme_last_build_profile(const sme_ctx *cx, const char **json) {
       os << (i ? "," : "") << "\"" << cx->last_profile[i].first << "\":" << cx->last_profile[i].second;
     if (cx->last_query_ms >= 0) os << (cx->last_profile.empty() ? "" : ",") << "\"query_kernel\":" << cx->last_query_ms;
     if (cx->last_query_ms >= 0) os << ",\"query_prep\":" << cx->last_query_prep_ms;
-    if (cx->last_query_ms >= 0) os << ",\"query_kernel_name\":\"" << (cx->last_query_tiled ? "k_query_imp" : "k_query") << "\"";
+    if (cx->last_query_ms >= 0) os << ",\"query_index\":" << cx->last_query_index_ms;
+    if (cx->last_query_ms >= 0) os << ",\"query_kernel_name\":\"" << (cx->last_query_tiled ? "k_query_bm" : "k_query") << "\"";
     os << "}";
     const_cast<sme_ctx *>(cx)->profile_json = os.str();
     *json = cx->profile_json.c_str();

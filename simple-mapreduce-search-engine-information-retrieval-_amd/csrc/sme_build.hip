@@ -2800,12 +2800,16 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
         // events bracket exactly this launch: "tok_kernel" is the dominant kernel's
         // duration that bench.py reports against the HBM roofline
         prof.mark("tok_setup");
-        const char *tg = getenv("SME_TOKGRID");
-        const int64_t tgrid = std::min<int64_t>(nF, tg ? atoll(tg) : 4096), rpb = (nF + tgrid - 1) / tgrid;
-        // SME_TOKEXP (timing experiments only, wrong results): 1 no signatures / probes, 2 no token stores
-        const char *tx = getenv("SME_TOKEXP");
+        const int64_t tgrid = std::max<int64_t>(1, std::min<int64_t>(nF, cx->opt_tok_grid)),
+                      rpb = (nF + tgrid - 1) / tgrid;
+        int tokexp = 0;
+#ifdef SME_EXPERIMENTS
+        // SME_TOKEXP (timing experiments, experiment builds only; wrong results):
+        // 1 no signatures / probes, 2 no token stores
+        if (const char *tx = getenv("SME_TOKEXP")) tokexp = atoi(tx);
+#endif
         hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)((nF + rpb - 1) / rpb)), dim3(kTokNT), 0, st, t, (int64_t)n, rs,
-                           re, frec, nF, rpb, tok, ntok, tb, tx ? atoi(tx) : 0);
+                           re, frec, nF, rpb, tok, ntok, tb, tokexp);
         SME_CHECK_LAUNCH();
         prof.mark("tok_kernel");
       }
@@ -2848,10 +2852,9 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   }
   const int64_t nraw = d2h(d_nsel, st);
   // next build's raw table: load <= 40 % (fewer probe collisions: c2 tokenizes in 9.2 ms at 8 M
-  // slots vs 10.0 ms at 4 M; SME_RAWLOAD = percent, experiments)
+  // slots vs 10.0 ms at 4 M; option raw_load_pct)
   {
-    const char *rl = getenv("SME_RAWLOAD");
-    const uint64_t pct = rl ? std::max(10, std::min(90, atoi(rl))) : 40;
+    const uint64_t pct = (uint64_t)std::max<int64_t>(10, std::min<int64_t>(90, cx->opt_raw_load_pct));
     cx->raw_cap_hint = next_pow2(std::max<uint64_t>(1ull << 20, (uint64_t)nraw * 100 / pct + 1));
   }
   int64_t *poff = W[W_POFF].as<int64_t>(nraw + 1);
@@ -3077,7 +3080,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   // single pass: the term sort's first pass reads pair x from the region of its record
   const int64_t *sort_reg = nullptr, *sort_xoff = nullptr;
   int64_t sort_nrec = 0;
-  if (K == 1 && want_packed && !getenv("SME_AGG2")) {
+  if (K == 1 && want_packed && !cx->opt_agg_two_pass) {
     // single-pass aggregation: record regions sized by ntok * max_nout
     int64_t *reg = W[W_T2].as<int64_t>(nR + 1), *reg_off = W[W_SEGB].as<int64_t>(nR + 1);
     SME_HIP(hipMemsetAsync(cnt + 24, 0, 4 * sizeof(unsigned long long), st));

@@ -28,8 +28,18 @@ struct sme_ctx {
   std::vector<std::pair<std::string, float>> last_profile;
   std::vector<uint8_t> mapping_out;  // last sme_number_documents result
   float last_query_ms = -1.0f;  // device time of the last query kernel launch
-  float last_query_prep_ms = -1.0f;  // skip-table preparation before it (wave kernel only)
-  bool last_query_tiled = false;  // which scoring kernel it was (k_query_tiled / k_query)
+  float last_query_prep_ms = -1.0f;  // per-batch tables before it (skip / impact tables, query order)
+  float last_query_index_ms = -1.0f;  // one-time heavy-row build of the index it ran on (prepare_queries)
+  bool last_query_tiled = false;  // which scoring kernel it was (k_query_bm / k_query)
+  // Path options (sme_set_option).  Every setting gives identical results; they
+  // exist so tests can hold each path to the others and benches can sweep them.
+  int64_t opt_query_kernel = 0;   // "query_kernel": 0 block-max (auto), 1 streaming k_query
+  int64_t opt_heavy_div = 32;     // "heavy_div": heavy rows for terms with df >= span / div (0: none)
+  int64_t opt_seed_tiles = 4;     // "seed_tiles": best-bound tiles scored before the sweep (0..8)
+  int64_t opt_query_order = 1;    // "query_order": 1 heaviest-term query order, 0 batch order
+  int64_t opt_agg_two_pass = 0;   // "agg_two_pass": 1 = count + emit aggregation passes
+  int64_t opt_tok_grid = 4096;    // "tok_grid": tokenizer workgroups (>= 1)
+  int64_t opt_raw_load_pct = 40;  // "raw_load_pct": raw-vocabulary table load of the next build (10..90)
   // indexes borrow the context (its pool, workspace, stream): sme_destroy defers
   // the delete until the last index is freed, whatever order a host frees them in
   int live_indexes = 0;
@@ -76,13 +86,21 @@ struct sme_index {
   std::vector<int32_t> h_gram;
   std::vector<uint8_t> h_term_tmp;
   bool h_terms_ready = false;
+  // query-side heavy rows (prepare_queries, sme_query.hip): tf byte rows, 16-doc
+  // and 1024-doc block maxima of the terms covering >= 1/div of the docno span
+  sme::DevBuf d_hrow_of;  // int32 [V] heavy row or -1
+  sme::DevBuf d_heavy;    // u8 [H][T * 1024] tf | [H][T * 64] bm16 | [H][T] bm1k
+  const uint8_t *q_tfrow = nullptr, *q_bm16 = nullptr, *q_bm1k = nullptr;
+  int64_t q_T = 0, q_H = 0, q_div = -1;
+  bool q_ready = false;
+  float q_prep_ms = 0.0f;
   // stage timings of the build that produced this index (ms)
   std::vector<std::pair<std::string, float>> profile;
   ~sme_index() { ctx->live_indexes--; }  // members (pooled buffers) are released after this body
   explicit sme_index(sme_ctx *c) : ctx(c) {
     c->live_indexes++;
     for (sme::DevBuf *b : {&d_term_off, &d_term_chars, &d_off, &d_docno_d, &d_tf_d, &d_w, &d_idf, &d_lut, &d_gram, &d_docno_o,
-                           &d_tf_o, &d_rec_docno, &d_ser})
+                           &d_tf_o, &d_rec_docno, &d_ser, &d_hrow_of, &d_heavy})
       b->pool = &c->pool;
   }
 };
@@ -139,6 +157,7 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
 size_t term_sort_scratch(int64_t P);
 void serialize_index(sme_index *ix, hipStream_t st);
 void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t st);
+void prepare_queries(sme_index *ix, hipStream_t st);
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k,
                 int32_t *d_out_docno, double *d_out_score, hipStream_t st);
 void tokenize_string(sme_ctx *cx, const uint8_t *h_utf8, size_t n, std::vector<std::vector<uint16_t>> &out,

@@ -240,55 +240,150 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
 }
 
 
-
 // ---------------------------------------------------------------------------
-// Tiled, impact-gated scoring (default path).
+// Block-max pruned scoring (default path), k_query_bm.
 //
-// The docno axis is cut into tiles of kWTile documents from the index's
-// smallest docno.  Per batch: a skip table gives, for every DISTINCT batch term
-// and every tile, the term's first posting in the tile; terms covering >= 1/div
-// of the docno span (the Zipf head) also get two dense byte rows, the tf of
-// every document and its IMPACT q = floor(w * alpha) + 1 (w = lut[tf] * idf, the
-// exact fp64 weight; 0 where absent), alpha = 253.5 / (largest weight of any
-// batch term), so q <= 255 and q >= 1 exactly where the term occurs.
+// The docno axis is cut into tiles of kQT = 1024 documents from the index's
+// smallest docno, each tile into 64 blocks of 16 documents (lane l of a wave
+// owns block l).  Two structures bound what a document can score:
 //
-// One wave per query sweeps the tiles.  Per tile it sums the impacts of its
-// terms into packed u16 lanes (A(d) = sum_j q_j(d) is an integer, order-free:
-// dense terms by two byte permutes + adds per dword of four documents, posting
-// terms by LDS atomic adds).  Since q_j > w_j * alpha, A(d) > alpha * R(d) where
-// R is the real sum of d's weights, so a document whose fp64 score S(d) can
-// reach the current k-th best score th has A(d) >= gate = floor(alpha * th *
-// (1 - 2^-40)) (the factor absorbs every rounding).  Only
-// those candidates are scored exactly: S(d) = the left-to-right fp64 sum of
-// lut[tf] * idf over the query's terms in token order (tf from the dense tf row
-// or a binary search of the tile's postings), bit-identical to the reference's
-// `score += (1 + Math.log(tf)) * idf` (IntDocVectorsForwardIndex.java:197-213).
+//  * index-resident HEAVY rows (prepare_queries, built once per index, tf-based
+//    so they survive sme_index_reweight): for every term whose postings cover
+//    >= 1/div of the docno span (the Zipf head) and whose tf never exceeds 255,
+//    its tf byte of every document (0 where absent), the largest tf of every
+//    16-document block (bm16) and of every tile (bm1k);
+//  * per batch, for every DISTINCT batch term: a skip table (its first posting
+//    in every tile) and an impact table q(tf) = floor(w(tf) * alpha) + 1,
+//    w(tf) = lut[tf] * idf the exact fp64 weight, alpha = 253.5 / (largest
+//    weight of any batch term), so 1 <= q <= 254 where the term occurs.
+//
+// q is monotone in tf, so the impact of a block's (tile's) largest tf bounds
+// every document in it, and for a "sparse" term (no heavy row) the impact of
+// its largest tf (the first posting of the reduce-order CSR) bounds every
+// posting.  A(d) = sum_j q_j(tf_j(d)) > alpha * R(d) (R the real sum of d's
+// weights), so a document whose fp64 score can reach the current k-th best
+// score th has A(d) >= gate = floor(alpha * th * (1 - 2^-40)) + 1 (the factor
+// absorbs every rounding of S(d) vs R(d) and of the product).
+//
+// One wave per query:
+//  1. seed: tile upper bounds UB(x) = sum_heavy q(bm1k) + sum_sparse [postings
+//     in x] * q(maxtf) of every tile; the best `nseed` tiles are scored first,
+//     so th (and the gate) start near their final values;
+//  2. sweep: tiles in docno order, skipped when UB(x) < gate; a visited tile
+//     gets block bounds (heavy bm16 + the block's largest exact sparse sum; the
+//     sparse terms' postings of the tile are added into LDS), blocks below the
+//     gate are dropped, the rest get exact per-document A(d) (heavy tf bytes
+//     through the LDS impact tables), and documents with A(d) >= gate are
+//     scored exactly: the left-to-right fp64 sum of lut[tf] * idf over the
+//     query's terms in token order, bit-identical to the reference's
+//     `score += (1 + Math.log(tf)) * idf` (IntDocVectorsForwardIndex.java:197-213).
 // Candidates that beat th go to a per-wave LDS buffer of C entries; when it
 // fills, a bitonic sort (score desc, docno asc) keeps the best k and raises th.
+// The order tiles are visited in does not matter: `better` compares (score,
+// docno) completely, and th / the gate only ever rise.
 // ---------------------------------------------------------------------------
-#ifndef SME_QTB
-#define SME_QTB 10
-#endif
-constexpr int kWBits = SME_QTB;     // tile = 2^kWBits documents
-constexpr int kWTile = 1 << kWBits;
-constexpr int kDPL = kWTile / 64;   // documents per lane in a tile (16 at 1024)
-constexpr int kIMaxTerms = 64;      // lane j holds query term j
-constexpr int kWLut = 256;          // 1 + ln(tf) for tf < 256 from LDS
-constexpr int kTfRows = 4;          // LDS tf rows per tile (terms beyond: dense row bytes / binary search)
-static_assert(kDPL % 16 == 0 && kDPL <= 32, "tile must be 1024 or 2048 documents");
+constexpr int kQB = 10;
+constexpr int kQT = 1 << kQB;   // documents per tile
+constexpr int kQBlk = kQT / 64;  // documents per block (one lane per block)
+constexpr int kIMaxTerms = 64;   // lane j holds query term j
+constexpr int kHSlots = 16;      // heavy terms per query with an LDS impact table (more: posting path)
+constexpr int kSRows = 4;        // LDS tf rows per tile for sparse terms (more: binary search)
+constexpr int kMaxSeed = 8;
+static_assert(kQBlk == 16, "one uint4 of tf bytes per lane and heavy term");
 
 __device__ __forceinline__ uint32_t impact(double l, double widf, double alpha) {
   return (uint32_t)floor(__dmul_rn(__dmul_rn(l, widf), alpha)) + 1u;
 }
 __device__ __forceinline__ double rld(double v, int l) { return __longlong_as_double(rl64(__double_as_longlong(v), l)); }
-__device__ __forceinline__ uint32_t pkmax_u16(uint32_t a, uint32_t b) {
-  const uint32_t lo = max(a & 0xFFFFu, b & 0xFFFFu), hi = max(a >> 16, b >> 16);
-  return lo | (hi << 16);
-}
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t max_u8x4(uint32_t w) {
+  return max(max(w & 0xFFu, (w >> 8) & 0xFFu), max((w >> 16) & 0xFFu, w >> 24));
+}
 
+// ---- index-resident heavy rows (prepare_queries) ----------------------------
+__global__ void k_heavy_flags(const int64_t *off, const int32_t *tf_o, int64_t V, int64_t span, int64_t div,
+                              int32_t *flag) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t df = off[t + 1] - off[t];
+    flag[t] = (div > 0 && df > 0 && df * div >= span && tf_o[off[t]] <= 255) ? 1 : 0;
+  }
+}
+__global__ void k_heavy_rows(const int32_t *flag, const int32_t *scan, int64_t V, int64_t cap, const int64_t *off,
+                             int32_t *hrow_of, int32_t *hterm, int64_t *hdf) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t r = scan[t];
+    if (flag[t] && r < cap) {
+      hrow_of[t] = r;
+      hterm[r] = (int32_t)t;
+      hdf[r] = off[t + 1] - off[t];
+    } else {
+      hrow_of[t] = -1;
+    }
+  }
+}
+// tf byte of every heavy posting at docno - dmin of its row, over the heavy
+// rows' postings as one flat list (chunks of kSkipChunk) so a head term's
+// million postings spread over the whole chip
+constexpr int kSkipChunk = 2048;
+__global__ __launch_bounds__(256) void k_heavy_fill(const int64_t *hpre, int64_t H, const int32_t *hterm,
+                                                    const int64_t *off, const int32_t *docno, const int32_t *tf,
+                                                    int64_t dmin, int64_t stride, uint8_t *tfrow) {
+  const int64_t total = hpre[H];
+  for (int64_t x0 = (int64_t)blockIdx.x * kSkipChunk; x0 < total; x0 += (int64_t)gridDim.x * kSkipChunk) {
+    const int64_t x1 = x0 + kSkipChunk < total ? x0 + kSkipChunk : total;
+    int64_t lo = 0, hi = H;  // row of x0: hpre[lo] <= x0 < hpre[hi]
+    while (hi - lo > 1) {
+      const int64_t m = (lo + hi) >> 1;
+      if (hpre[m] <= x0) lo = m;
+      else hi = m;
+    }
+    int64_t row = lo, rb = hpre[row], re = hpre[row + 1], b = off[hterm[row]];
+    for (int64_t x = x0 + threadIdx.x; x < x1; x += blockDim.x) {
+      while (x >= re) {
+        row++;
+        rb = re;
+        re = hpre[row + 1];
+        b = off[hterm[row]];
+      }
+      const int64_t p = b + (x - rb);
+      tfrow[row * stride + ((int64_t)docno[p] - dmin)] = (uint8_t)tf[p];
+    }
+  }
+}
+// bm16[i] = largest tf byte of 16-document block i (flat over all rows: a row is
+// T * 64 blocks, its tf row T * 64 * 16 bytes, so the indexing is the same)
+__global__ void k_heavy_bm16(const uint4 *tfrow, int64_t n, uint8_t *bm16) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 v = tfrow[i];
+    bm16[i] = (uint8_t)max(max(max_u8x4(v.x), max_u8x4(v.y)), max(max_u8x4(v.z), max_u8x4(v.w)));
+  }
+}
+// bm1k[i] = largest of the 64 block maxima of tile i
+__global__ void k_heavy_bm1k(const uint4 *bm16, int64_t n, uint8_t *bm1k) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint4 v = bm16[4 * i + c];
+      m = max(m, max(max(max_u8x4(v.x), max_u8x4(v.y)), max(max_u8x4(v.z), max_u8x4(v.w))));
+    }
+    bm1k[i] = (uint8_t)m;
+  }
+}
+
+// ---- per-batch tables --------------------------------------------------------
 __global__ void k_mark_terms(const int32_t *terms, int64_t n, int64_t V, int32_t *mark) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t t = terms[i];
@@ -315,7 +410,6 @@ __global__ void k_max_qlen(const int64_t *qoff, int nq, int *mx) {
 // table starts as "infinity" with sk[row][T] = df; every posting that opens a
 // tile writes its index there (a change point), and a backward min-scan per
 // row fills the gaps (k_skip_suffix).
-constexpr int kSkipChunk = 2048;  // postings per block in k_skip_fill
 __global__ __launch_bounds__(256) void k_skip_fill(const int64_t *rpre, int64_t nrows, const int32_t *term_of_row,
                                                    const int64_t *off, const int32_t *docno, int64_t dmin, int64_t T,
                                                    int32_t *sk) {
@@ -338,8 +432,8 @@ __global__ __launch_bounds__(256) void k_skip_fill(const int64_t *rpre, int64_t 
       }
       const int64_t i = x - rb, n = re - rb;
       int32_t *r = sk + row * (T + 1);
-      const int64_t j = ((int64_t)docno[b + i] - dmin) >> kWBits;
-      const int64_t jp = i == 0 ? -1 : (((int64_t)docno[b + i - 1] - dmin) >> kWBits);
+      const int64_t j = ((int64_t)docno[b + i] - dmin) >> kQB;
+      const int64_t jp = i == 0 ? -1 : (((int64_t)docno[b + i - 1] - dmin) >> kQB);
       if (jp < j) r[j] = (int32_t)i;
       if (i == n - 1) r[T] = (int32_t)n;
     }
@@ -372,26 +466,18 @@ __global__ void k_skip_zero_rows(const int64_t *rdf, int64_t nrows, int64_t T, i
     if (rdf[r] == 0)
       for (int64_t j = threadIdx.x; j <= T; j += blockDim.x) sk[r * (T + 1) + j] = 0;
 }
-
-// Per batch row: the largest weight of the term (its max tf is the first
-// posting of the reduce-order CSR, tf desc) folded into wmax (non-negative
-// doubles order like their bit patterns), and whether the term gets dense rows:
-// postings covering >= 1/div of the docno span, every tf <= 255.  A row costs
-// span bytes against >= 8 B x span / div of (docno, tf) postings.
-__global__ void k_row_stats(const int32_t *term_of_row, const int64_t *rdf, int64_t nrows, const int64_t *off,
-                            const int32_t *tf_o, const double *lut, const double *idf, int64_t span, int64_t div,
-                            int32_t *flag, unsigned long long *wmax_bits) {
+// largest weight of any batch term (its max tf is the first posting of the
+// reduce-order CSR, tf desc), as bits (non-negative doubles order like them)
+__global__ void k_row_wmax(const int32_t *term_of_row, const int64_t *rdf, int64_t nrows, const int64_t *off,
+                           const int32_t *tf_o, const double *lut, const double *idf, unsigned long long *wmax_bits) {
   unsigned long long wm = 0;
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows + 1; r += (int64_t)gridDim.x * blockDim.x) {
-    int32_t fl = 0;
-    if (r < nrows && rdf[r] > 0) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
+    if (rdf[r] > 0) {
       const int32_t t = term_of_row[r];
-      const int32_t mt = tf_o[off[t]];
-      const unsigned long long wb = (unsigned long long)__double_as_longlong(__dmul_rn(lut[mt], idf[t]));
+      const unsigned long long wb =
+          (unsigned long long)__double_as_longlong(__dmul_rn(lut[tf_o[off[t]]], idf[t]));
       wm = wb > wm ? wb : wm;
-      fl = (div > 0 && rdf[r] * div >= span && mt <= 255) ? 1 : 0;
     }
-    flag[r] = fl;
   }
   for (int o = 32; o > 0; o >>= 1) {
     const unsigned long long u = __shfl_xor(wm, o, 64);
@@ -399,51 +485,17 @@ __global__ void k_row_stats(const int32_t *term_of_row, const int64_t *rdf, int6
   }
   if ((threadIdx.x & 63) == 0 && wm) atomicMax(wmax_bits, wm);
 }
-__global__ void k_dense_rows(const int32_t *flag, const int32_t *scan, int64_t nrows, int64_t cap, int32_t *drow) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
-    drow[r] = (flag[r] && scan[r] < cap) ? scan[r] : -1;
-}
-// Within a tile a dense row is stored lane-major: byte kDPL * l + b holds
-// document 64 b + l, so lane l's kDPL-byte load carries the documents it owns.
-__device__ __forceinline__ int64_t dense_pos(int64_t x) {
-  const int64_t r = x & (kWTile - 1);
-  return (x - r) + kDPL * (r & 63) + (r >> 6);
-}
-// tf and impact bytes at docno - dmin for every posting of a dense row, over the
-// batch rows' postings as one flat list (chunks of kSkipChunk, like k_skip_fill)
-// so a head term's million postings spread over the whole chip
-__global__ __launch_bounds__(256) void k_dense_fill(const int64_t *rpre, int64_t nrows, const int32_t *drow,
-                                                    const int32_t *term_of_row, const int64_t *off,
-                                                    const int32_t *docno, const int32_t *tf, const double *lut,
-                                                    const double *idf, const unsigned long long *wmax_bits,
-                                                    int64_t dmin, int64_t stride, uint8_t *dtf, uint8_t *dq) {
+// impact table of every batch row: q(tf) for tf < 256 (0 for tf = 0; tf above
+// the index's largest tf never occurs)
+__global__ void k_row_qlut(const int32_t *term_of_row, int64_t nrows, const double *lut, int max_tf,
+                           const double *idf, const unsigned long long *wmax_bits, uint8_t *qlut) {
   const double wmax = __longlong_as_double((long long)*wmax_bits);
   const double alpha = wmax > 0.0 ? 253.5 / wmax : 1.0;
-  const int64_t total = rpre[nrows];
-  for (int64_t x0 = (int64_t)blockIdx.x * kSkipChunk; x0 < total; x0 += (int64_t)gridDim.x * kSkipChunk) {
-    const int64_t x1 = x0 + kSkipChunk < total ? x0 + kSkipChunk : total;
-    int64_t lo = 0, hi = nrows;  // row of x0
-    while (hi - lo > 1) {
-      const int64_t m = (lo + hi) >> 1;
-      if (rpre[m] <= x0) lo = m;
-      else hi = m;
-    }
-    int64_t row = lo, rb = rpre[row], re = rpre[row + 1];
-    for (int64_t x = x0 + threadIdx.x; x < x1; x += blockDim.x) {
-      while (x >= re) {
-        row++;
-        rb = re;
-        re = rpre[row + 1];
-      }
-      const int32_t d = drow[row];
-      if (d < 0) continue;
-      const int32_t t = term_of_row[row];
-      const int64_t p = off[t] + (x - rb);
-      const int32_t f = tf[p];  // <= 255 (k_row_stats)
-      const int64_t pos = (int64_t)d * stride + dense_pos((int64_t)docno[p] - dmin);
-      dtf[pos] = (uint8_t)f;
-      dq[pos] = (uint8_t)impact(lut[f], idf[t], alpha);
-    }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nrows * 256;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int f = (int)(i & 255);
+    const int32_t t = term_of_row[i >> 8];
+    qlut[i] = (uint8_t)(f == 0 ? 0u : f <= max_tf ? impact(lut[f], idf[t], alpha) : 255u);
   }
 }
 
@@ -497,69 +549,98 @@ __device__ __forceinline__ void wave_sort(double *s, int32_t *d, int n) {
     }
 }
 
+struct QBmArgs {
+  const int64_t *off;     // postings per term (docno-sorted CSR; also the reduce-order CSR's offsets)
+  const int32_t *docno;   // docno-ascending postings
+  const int32_t *tf;
+  const int32_t *tf_o;    // reduce order: tf_o[off[t]] is term t's largest tf
+  const double *lut;      // 1 + ln(tf)
+  const double *idf;
+  int64_t V;
+  const int32_t *row_of;  // term -> batch row
+  const int32_t *sk;      // skip table [rows][T + 1]
+  const uint8_t *qlut;    // impact tables [rows][256]
+  const int32_t *hrow_of;  // term -> heavy row or -1 (nullptr: no heavy rows)
+  const uint8_t *tfrow;   // [H][T * kQT]
+  const uint8_t *bm16;    // [H][T * 64]
+  const uint8_t *bm1k;    // [H][T]
+  int64_t dmin, T;
+  const int32_t *terms;
+  const int64_t *qoff;
+  const int32_t *qorder;
+  int nq, k, nseed;
+  int32_t *out_d;
+  double *out_s;
+  const unsigned long long *wmax_bits;
+  unsigned long long *stats;  // SME_EXPERIMENTS builds only (else nullptr)
+};
+
 template <int C>
-__global__ __launch_bounds__(64) void k_query_imp(
-    const int64_t *__restrict__ off, const int32_t *__restrict__ docno, const int32_t *__restrict__ tf,
-    const double *__restrict__ lut, int max_tf, const double *__restrict__ idf, int64_t V,
-    const int32_t *__restrict__ row_of, const int32_t *__restrict__ sk, int64_t dmin, int64_t T,
-    const int32_t *__restrict__ terms, const int64_t *__restrict__ qoff, const int32_t *__restrict__ qorder, int nq,
-    int k, int32_t *out_d, double *out_s, const uint8_t *__restrict__ dtf, const uint8_t *__restrict__ dq,
-    const int32_t *__restrict__ drow, int64_t dstride, const unsigned long long *__restrict__ wmax_bits, int sh,
-    unsigned long long *stats, int exper) {
-  __shared__ uint32_t lacc[kDPL / 2 * 64];  // posting terms' impact sums, u16 pairs (documents 128 m + l, + 64)
+__global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
+  __shared__ uint8_t s_qlut[kHSlots * 256];  // impact tables of the query's heavy terms
+  __shared__ uint32_t lacc[kQT];             // sparse terms' impact sums of the tile's documents
+  __shared__ uint8_t trow[kSRows * kQT];     // tf bytes of the tile for the first kSRows sparse terms
   __shared__ double bs[C];
   __shared__ int32_t bd[C];
-  __shared__ double s_lut[kWLut];
-  // tf bytes of the tile for the first kTfRows query terms with postings in it
-  // (lane-major like the dense rows), read when candidates are scored exactly
-  __shared__ uint8_t trow[kTfRows * kWTile];
-  __shared__ uint32_t s_big;  // slots whose term has a tf > 255 in the tile
+  __shared__ uint32_t s_big;  // sparse slots whose term has a tf > 255 in the tile
   const int lane = threadIdx.x;
-  for (int j = lane; j < kWLut; j += 64) s_lut[j] = (j >= 1 && j <= max_tf) ? lut[j] : 0.0;
-  const double wmax = __longlong_as_double((long long)*wmax_bits);
-  // dense impacts are bytes at scale alpha; posting terms' impacts and the
-  // gate use alpha * 2^sh (the dense sums are shifted by sh before the gate)
+  const double wmax = __longlong_as_double((long long)*a.wmax_bits);
   const double alpha = wmax > 0.0 ? 253.5 / wmax : 1.0;
-  const double alpha_s = __dmul_rn(alpha, (double)(1 << sh));
-  __syncthreads();
+  const int64_t T = a.T, span = T << kQB;
   // queries in `qorder` (heaviest terms first) are dealt in 8 contiguous slices,
   // slice x to the blocks b with b % 8 == x, which share an XCD and its L2
-  const int slice = (nq + 7) >> 3;
+  const int slice = (a.nq + 7) >> 3;
   for (int qi = blockIdx.x; qi < 8 * slice; qi += gridDim.x) {
     const int pos = (qi & 7) * slice + (qi >> 3);
-    if (pos >= nq) continue;
-    const int q = qorder ? qorder[pos] : pos;
-    const int64_t q0 = qoff[q];
-    const int nt = (int)(qoff[q + 1] - q0);  // <= kIMaxTerms (host checked)
-    // lane j < nt holds term j: postings base, df, idf, skip row, dense rows
+    if (pos >= a.nq) continue;
+    const int q = a.qorder ? a.qorder[pos] : pos;
+    const int64_t q0 = a.qoff[q];
+    const int nt = (int)(a.qoff[q + 1] - q0);  // <= kIMaxTerms (host checked)
+    // lane j < nt holds token j: postings base, df, idf, batch row, heavy row,
+    // impact of its largest tf
     int64_t mb = 0;
-    int32_t mdf = 0;
+    int32_t mdf = 0, brow = 0, hr = -1;
     double midf = 0.0;
-    const int32_t *mrow = sk;
-    int32_t nx = 0x7FFFFFFF;
-    int64_t mdr = -1;
+    uint32_t qmx = 0;
     if (lane < nt) {
-      const int32_t t = terms[q0 + lane];
-      if (t >= 0 && t < V) {  // unknown (-1) and out-of-range ids are skipped
-        mb = off[t];
-        mdf = (int32_t)(off[t + 1] - mb);
-        midf = idf[t];
-        mrow = sk + (int64_t)row_of[t] * (T + 1);
+      const int32_t t = a.terms[q0 + lane];
+      if (t >= 0 && t < a.V) {  // unknown (-1) and out-of-range ids are skipped
+        mb = a.off[t];
+        mdf = (int32_t)(a.off[t + 1] - mb);
+        midf = a.idf[t];
+        brow = a.row_of[t];
         if (mdf > 0) {
-          nx = (int32_t)(((int64_t)docno[mb] - dmin) >> kWBits);
-          if (drow != nullptr) mdr = drow[row_of[t]];
+          if (a.hrow_of) hr = a.hrow_of[t];
+          const int32_t mt = a.tf_o[mb];
+          qmx = mt <= 255 ? a.qlut[(int64_t)brow * 256 + mt] : impact(a.lut[mt], midf, alpha);
         }
       }
     }
-    const bool isd = mdr >= 0;
-    const uint64_t dmask = (uint64_t)__ballot(isd);
-    const int64_t mro = isd ? mdr * dstride : 0;  // this lane's dense row offset (impact / tf rows)
+    // heavy terms: the first kHSlots tokens with a heavy row (slot = rank); the
+    // rest, and every term without one, are "sparse" (postings + skip table)
+    const uint64_t hcand = (uint64_t)__ballot(hr >= 0);
+    const uint32_t hslot = lane_prefix(hcand);
+    const bool ish = hr >= 0 && hslot < (uint32_t)kHSlots;
+    const uint64_t hm = (uint64_t)__ballot(ish);
+    const uint64_t sm = (uint64_t)__ballot(lane < nt && mdf > 0 && !ish);
+    const int32_t *mrow = a.sk + (int64_t)brow * (T + 1);
+    const int64_t h1k = ish ? (int64_t)hr * T : 0, h16 = ish ? (int64_t)hr * (T << 6) : 0,
+                  htf = ish ? (int64_t)hr * span : 0;
+    for (uint64_t m = hm; m; m &= m - 1) {
+      const int j = (int)__builtin_ctzll(m);
+      const int s = __popcll(hm & ((1ull << j) - 1));
+      const int r = __builtin_amdgcn_readlane(brow, j);
+      reinterpret_cast<uint32_t *>(s_qlut)[s * 64 + lane] =
+          reinterpret_cast<const uint32_t *>(a.qlut + (int64_t)r * 256)[lane];
+    }
+    __syncthreads();
+
     int cnt = 0;  // buffer fill (wave-uniform)
-    uint32_t st_tiles = 0, st_gated = 0, st_cand = 0, st_comp = 0, st_sparse = 0;  // SME_QSTATS
     bool th_ok = false;
     double th_s = 0.0;
     int32_t th_d = 0;
     uint32_t gate = 1;  // touched documents only until k of them are held
+    uint32_t st_tiles = 0, st_blocks = 0, st_cand = 0, st_comp = 0;
     // sort the buffer, keep the best k, raise th and the gate
     auto compact = [&]() {
       st_comp++;
@@ -571,257 +652,332 @@ __global__ __launch_bounds__(64) void k_query_imp(
       }
       __syncthreads();
       wave_sort(bs, bd, n2);
-      cnt = min(cnt, k);
-      if (cnt >= k) {
+      cnt = min(cnt, a.k);
+      if (cnt >= a.k) {
         th_ok = true;
-        th_s = bs[k - 1];
-        th_d = bd[k - 1];
-        const double g = floor(__dmul_rn(__dmul_rn(th_s, alpha_s), 1.0 - 0x1p-40));
-        gate = g > 1.0 ? (uint32_t)g : 1u;
+        th_s = bs[a.k - 1];
+        th_d = bd[a.k - 1];
+        const double g = floor(__dmul_rn(__dmul_rn(th_s, alpha), 1.0 - 0x1p-40));
+        gate = g >= 0.0 ? (uint32_t)g + 1u : 1u;
       }
     };
-    int32_t tile = nx;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) tile = min(tile, __shfl_xor(tile, o, 64));
-    int32_t mc = 0, me = 0;
-    if (tile != 0x7FFFFFFF && lane < nt && mdf > 0) {
-      mc = mrow[tile];
-      me = mrow[tile + 1];
-    }
-    while (tile != 0x7FFFFFFF) {  // wave-uniform
-      // loads for the next step overlap this tile's work: the next tile of this
-      // term, and (for the common case that it is tile + 1) its range end
-      nx = 0x7FFFFFFF;
-      int32_t me1 = 0;
-      if (lane < nt && me < mdf) {
-        nx = (int32_t)(((int64_t)docno[mb + me] - dmin) >> kWBits);
-        me1 = tile + 2 <= T ? mrow[tile + 2] : mdf;
-      } else if (lane < nt) {
-        me1 = mdf;
+    // upper bound of tile x (any lane, x < T): heavy tile maxima + sparse maxima
+    auto tile_ub = [&](int64_t x) -> uint32_t {
+      uint32_t u = 0;
+      for (uint64_t m = hm; m; m &= m - 1) {
+        const int j = (int)__builtin_ctzll(m);
+        const int s = __popcll(hm & ((1ull << j) - 1));
+        u += s_qlut[(s << 8) + a.bm1k[rl64(h1k, j) + x]];
       }
-      const int64_t dbase = dmin + ((int64_t)tile << kWBits);
-      const int64_t tbyte = (int64_t)tile << kWBits;
-      const uint64_t amask = (uint64_t)__ballot(lane < nt && me > mc);  // terms with postings in the tile
-      const uint64_t dm = amask & dmask, sm = amask & ~dmask;
-      uint64_t rmask = amask;  // the first kTfRows terms of amask own an LDS tf row (slot = rank in amask)
-#pragma unroll
-      for (int x = 0; x < kTfRows; x++) rmask &= rmask - 1;
-      rmask = amask & ~rmask;
-      const int64_t plo = mb + mc, phi = mb + me;  // this lane's term: postings in the tile
-      uint32_t a[kDPL / 2];
+      for (uint64_t m = sm; m; m &= m - 1) {
+        const int j = (int)__builtin_ctzll(m);
+        const int32_t *row = a.sk + (int64_t)__builtin_amdgcn_readlane(brow, j) * (T + 1);
+        if (row[x] < row[x + 1]) u += (uint32_t)__builtin_amdgcn_readlane((int)qmx, j);
+      }
+      return u;
+    };
+    // score tile x (wave-uniform)
+    auto tile = [&](int64_t x) {
       st_tiles++;
-      // dense terms: kDPL impact bytes per lane, four terms' loads in flight;
-      // the first four are issued before the posting pass so both overlap
-      uint64_t dmr = dm;
-      auto dense_load = [&](uint4 (&v)[4][kDPL / 16]) {
+      const int64_t dbase = a.dmin + (x << kQB);
+      int32_t mc = 0, me = 0;  // this lane's sparse term: postings in the tile (term-relative)
+      if ((sm >> lane) & 1) {
+        mc = mrow[x];
+        me = mrow[x + 1];
+      }
+      const uint64_t spm = (uint64_t)__ballot(me > mc);
+      // block bounds from the heavy rows
+      uint32_t hub = 0;
+      for (uint64_t m = hm; m; m &= m - 1) {
+        const int j = (int)__builtin_ctzll(m);
+        const int s = __popcll(hm & ((1ull << j) - 1));
+        hub += s_qlut[(s << 8) + a.bm16[rl64(h16, j) + (x << 6) + lane]];
+      }
+      const uint32_t sub = wave_sum_u32(((spm >> lane) & 1) ? qmx : 0u);
+      if (wave_max_u32(hub) + sub < gate) return;
+      uint32_t A[kQBlk];
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
-          if (dmr) {
-            const int j = (int)__builtin_ctzll(dmr);
-            dmr &= dmr - 1;
-            const uint8_t *pj = dq + rl64(mro, j) + tbyte + kDPL * lane;
+      for (int i = 0; i < kQBlk; i++) A[i] = 0;
+      uint64_t rmask = spm;  // the first kSRows sparse terms with postings own an LDS tf row (slot = rank)
 #pragma unroll
-            for (int c = 0; c < kDPL / 16; c++) v[g][c] = *reinterpret_cast<const uint4 *>(pj + 16 * c);
-          } else {
+      for (int s = 0; s < kSRows; s++) rmask &= rmask - 1;
+      rmask = spm & ~rmask;
+      uint32_t bigs = 0;
+      uint32_t smax = 0;
+      if (spm) {
+        uint4 *la = reinterpret_cast<uint4 *>(lacc + kQBlk * lane);
 #pragma unroll
-            for (int c = 0; c < kDPL / 16; c++) v[g][c] = make_uint4(0, 0, 0, 0);
-          }
-        }
-      };
-      auto dense_add = [&](const uint4 (&v)[4][kDPL / 16]) {
-#pragma unroll
-        for (int g = 0; g < 4; g++)
-#pragma unroll
-          for (int c = 0; c < kDPL / 16; c++) {
-            const uint32_t w4[4] = {v[g][c].x, v[g][c].y, v[g][c].z, v[g][c].w};
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-              a[8 * c + 2 * u] += __builtin_amdgcn_perm(0u, w4[u], 0x0C010C00u);
-              a[8 * c + 2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
-            }
-          }
-      };
-      uint4 v0[4][kDPL / 16];
-      dense_load(v0);
-      if (sm && !(exper & 2)) {
-        st_sparse++;
-        // posting terms: impacts added into LDS (order-free integer sums)
-#pragma unroll
-        for (int m = 0; m < kDPL / 2; m++) lacc[m * 64 + lane] = 0;
-        {
-          int sl = 0;
-          for (uint64_t m = rmask; m; m &= m - 1, sl++)
-            if ((sm >> __builtin_ctzll(m)) & 1)
-#pragma unroll
-              for (int c = 0; c < kDPL / 16; c++)
-                *reinterpret_cast<uint4 *>(trow + (sl << kWBits) + kDPL * lane + 16 * c) = make_uint4(0, 0, 0, 0);
-        }
+        for (int c = 0; c < kQBlk / 4; c++) la[c] = make_uint4(0, 0, 0, 0);
+        for (int s = 0; s < __popcll(rmask); s++)
+          *reinterpret_cast<uint4 *>(trow + (s << kQB) + kQBlk * lane) = make_uint4(0, 0, 0, 0);
         if (lane == 0) s_big = 0;
         __syncthreads();
-        // the tile's postings of all posting terms as one list, 256 per step:
-        // entry x belongs to the last term j of sm with pre_j <= x
-        const int32_t cj = ((sm >> lane) & 1) ? me - mc : 0;
+        // the tile's postings of all sparse terms as one list, 256 per step:
+        // entry e belongs to the last term j of spm with pre_j <= e
+        const int32_t cj = ((spm >> lane) & 1) ? me - mc : 0;
         const int32_t incl = wave_incl_sum(cj), prej = incl - cj;
         const int32_t total = __shfl(incl, 63, 64);
-        for (int32_t x0 = 0; x0 < total; x0 += 256) {
-          const int nu = min(4, (total - x0 + 63) >> 6);  // 64-entry chunks in this step (wave-uniform)
-          int32_t dv[4], fv[4], sv[4];
+        const int64_t plo = mb + mc;
+        for (int32_t e0 = 0; e0 < total; e0 += 256) {
+          const int nu = min(4, (total - e0 + 63) >> 6);  // 64-entry chunks in this step (wave-uniform)
+          int32_t dv[4], fv[4], sv[4], rv[4];
           double wv[4];
 #pragma unroll
           for (int u = 0; u < 4; u++) {
             dv[u] = 0;
             fv[u] = 0;
             wv[u] = 0.0;
-            sv[u] = kTfRows;
+            sv[u] = kSRows;
+            rv[u] = 0;
             if (u < nu) {
-              const int32_t x = x0 + 64 * u + lane;
+              const int32_t e = e0 + 64 * u + lane;
               int64_t pb = 0;
               double wj = 0.0;
-              int sj = kTfRows;
-              for (uint64_t m = sm; m; m &= m - 1) {
+              int sj = kSRows, rj = 0;
+              for (uint64_t m = spm; m; m &= m - 1) {
                 const int j = (int)__builtin_ctzll(m);
                 const int32_t pj = __builtin_amdgcn_readlane(prej, j);
-                if (x >= pj) {
+                if (e >= pj) {
                   pb = rl64(plo, j) - pj;
                   wj = rld(midf, j);
-                  sj = ((rmask >> j) & 1) ? __popcll(amask & ((1ull << j) - 1)) : kTfRows;
+                  rj = __builtin_amdgcn_readlane(brow, j);
+                  sj = ((rmask >> j) & 1) ? __popcll(spm & ((1ull << j) - 1)) : kSRows;
                 }
               }
-              if (x < total) {
-                dv[u] = docno[pb + x];
-                fv[u] = tf[pb + x];
+              if (e < total) {
+                dv[u] = a.docno[pb + e];
+                fv[u] = a.tf[pb + e];
               }
               wv[u] = wj;
               sv[u] = sj;
+              rv[u] = rj;
             }
           }
 #pragma unroll
           for (int u = 0; u < 4; u++) {
             if (fv[u] == 0) continue;
             const int r = (int)((int64_t)dv[u] - dbase);
-            if (sv[u] < kTfRows) {
-              trow[(sv[u] << kWBits) + kDPL * (r & 63) + (r >> 6)] = (uint8_t)(fv[u] > 255 ? 0 : fv[u]);
+            if (sv[u] < kSRows) {
+              trow[(sv[u] << kQB) + r] = (uint8_t)(fv[u] > 255 ? 0 : fv[u]);
               if (fv[u] > 255) atomicOr(&s_big, 1u << sv[u]);
             }
-            const double l = fv[u] < kWLut ? s_lut[fv[u]] : lut[fv[u]];
-            atomicAdd(&lacc[((r >> 7) << 6) | (r & 63)], impact(l, wv[u], alpha_s) << (((r >> 6) & 1) << 4));
+            const uint32_t qv =
+                fv[u] <= 255 ? (uint32_t)a.qlut[(int64_t)rv[u] * 256 + fv[u]] : impact(a.lut[fv[u]], wv[u], alpha);
+            atomicAdd(&lacc[r], qv);
           }
         }
         __syncthreads();
+#pragma unroll
+        for (int c = 0; c < kQBlk / 4; c++) {
+          const uint4 v = la[c];
+          A[4 * c] = v.x;
+          A[4 * c + 1] = v.y;
+          A[4 * c + 2] = v.z;
+          A[4 * c + 3] = v.w;
+          smax = max(smax, max(max(v.x, v.y), max(v.z, v.w)));
+        }
+        bigs = s_big;
       }
+      const bool pass = hub + smax >= gate;
+      if (__ballot(pass) == 0) return;
+      st_blocks++;
+      uint32_t cm = 0;  // candidate documents of this lane's block
+      if (pass) {
+        for (uint64_t m = hm; m; m &= m - 1) {
+          const int j = (int)__builtin_ctzll(m);
+          const int s = __popcll(hm & ((1ull << j) - 1));
+          const uint4 v = *reinterpret_cast<const uint4 *>(a.tfrow + rl64(htf, j) + (x << kQB) + kQBlk * lane);
+          const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int m = 0; m < kDPL / 2; m++) a[m] = 0;
-      dense_add(v0);
-      while (dmr) {
-        uint4 v[4][kDPL / 16];
-        dense_load(v);
-        dense_add(v);
+          for (int i = 0; i < kQBlk; i++) A[i] += s_qlut[(s << 8) + ((w4[i >> 2] >> ((i & 3) << 3)) & 0xFFu)];
+        }
+#pragma unroll
+        for (int i = 0; i < kQBlk; i++)
+          if (A[i] >= gate) cm |= 1u << i;
       }
-      // A = (dense sums << sh) + posting-term sums: u16 fields never carry
-      // (host: 255 * 2^sh * terms <= 65535)
-#pragma unroll
-      for (int m = 0; m < kDPL / 2; m++) a[m] = (a[m] << sh) + (sm && !(exper & 2) ? lacc[m * 64 + lane] : 0u);
-      // gate: most tiles hold no document whose impact sum reaches it
-      uint32_t mx = a[0];
-#pragma unroll
-      for (int m = 1; m < kDPL / 2; m++) mx = pkmax_u16(mx, a[m]);
-      if (!(exper & 1) && __ballot(max(mx & 0xFFFFu, mx >> 16) >= gate) != 0) {
-        uint32_t cm = 0;
-#pragma unroll
-        for (int b = 0; b < kDPL; b++)
-          if (((a[b >> 1] >> ((b & 1) << 4)) & 0xFFFFu) >= gate) cm |= 1u << b;
-        st_gated++;
-        if (stats) st_cand += (uint32_t)__popc(cm);
-        // dense terms that own a tf row: copy the tile's tf bytes
-        {
-          int sl = 0;
-          for (uint64_t m = rmask; m; m &= m - 1, sl++) {
+      if (a.stats) st_cand += (uint32_t)__popc(cm);
+      const uint64_t amask = hm | spm;  // terms that can contribute, in token order
+      for (;;) {
+        const bool have = cm != 0;
+        if (__ballot(have) == 0) break;  // wave-uniform
+        double S = 0.0;
+        int32_t d = 0x7FFFFFFF;
+        bool keep = false;
+        if (have) {
+          const int b = (int)__builtin_ctz(cm);
+          cm &= cm - 1;
+          const int r = kQBlk * lane + b;
+          d = (int32_t)(dbase + r);
+          // exact score: query-token order, fp64, as rank() accumulates it
+          for (uint64_t m = amask; m; m &= m - 1) {
             const int j = (int)__builtin_ctzll(m);
-            if (!((dmask >> j) & 1)) continue;
-            const uint8_t *pj = dtf + rl64(mro, j) + tbyte + kDPL * lane;
-#pragma unroll
-            for (int c = 0; c < kDPL / 16; c++)
-              *reinterpret_cast<uint4 *>(trow + (sl << kWBits) + kDPL * lane + 16 * c) =
-                  *reinterpret_cast<const uint4 *>(pj + 16 * c);
-          }
-        }
-        __syncthreads();
-        const uint32_t bigs = sm ? s_big : 0u;
-        for (;;) {
-          const bool have = cm != 0;
-          if (__ballot(have) == 0) break;  // wave-uniform
-          double S = 0.0;
-          int32_t d = 0x7FFFFFFF;
-          bool keep = false;
-          if (have) {
-            const int b = (int)__builtin_ctz(cm);
-            cm &= cm - 1;
-            d = (int32_t)(dbase + ((b << 6) | lane));
-            // exact score: query-token order, fp64, as rank() accumulates it
-            int sl = 0;
-            for (uint64_t m = amask; m; m &= m - 1, sl++) {
-              const int j = (int)__builtin_ctzll(m);
-              int f = 0;
-              if (sl < kTfRows && !((bigs >> sl) & 1)) {
-                f = trow[(sl << kWBits) + kDPL * lane + b];
-              } else if ((dmask >> j) & 1) {
-                f = dtf[rl64(mro, j) + tbyte + kDPL * lane + b];
+            int f = 0;
+            if ((hm >> j) & 1) {
+              f = a.tfrow[rl64(htf, j) + (x << kQB) + r];
+            } else {
+              const int sl = ((rmask >> j) & 1) ? __popcll(spm & ((1ull << j) - 1)) : kSRows;
+              if (sl < kSRows && !((bigs >> sl) & 1)) {
+                f = trow[(sl << kQB) + r];
               } else {
-                int64_t lo = rl64(plo, j);
-                const int64_t e = rl64(phi, j);
+                const int64_t base = rl64(mb, j);
+                int64_t lo = base + __builtin_amdgcn_readlane(mc, j);
+                const int64_t e = base + __builtin_amdgcn_readlane(me, j);
                 int64_t hi = e;
                 while (lo < hi) {
                   const int64_t mid = (lo + hi) >> 1;
-                  if (docno[mid] < d) lo = mid + 1;
+                  if (a.docno[mid] < d) lo = mid + 1;
                   else hi = mid;
                 }
-                if (lo < e && docno[lo] == d) f = tf[lo];
+                if (lo < e && a.docno[lo] == d) f = a.tf[lo];
               }
-              if (f != 0) S = __dadd_rn(S, __dmul_rn(f < kWLut ? s_lut[f] : lut[f], rld(midf, j)));
             }
-            keep = !th_ok || better(S, d, th_s, th_d);
+            if (f != 0) S = __dadd_rn(S, __dmul_rn(a.lut[f], rld(midf, j)));
           }
-          const uint64_t km = (uint64_t)__ballot(keep);
-          if (keep) {
-            const int pos = cnt + (int)lane_prefix(km);
-            bs[pos] = S;
-            bd[pos] = d;
+          keep = !th_ok || better(S, d, th_s, th_d);
+        }
+        const uint64_t km = (uint64_t)__ballot(keep);
+        if (keep) {
+          const int p = cnt + (int)lane_prefix(km);
+          bs[p] = S;
+          bd[p] = d;
+        }
+        cnt += __popcll(km);
+        if (cnt > C - 64) compact();
+      }
+    };
+
+    if (nt > 0 && (hm | sm)) {
+      // 1. seed tiles: the best tile bound of every lane's column, then the
+      //    nseed best of those
+      int64_t seed[kMaxSeed];
+      int ns = 0;
+      if (a.nseed > 0) {
+        uint32_t bu = 0;
+        int64_t bx = -1;
+        for (int64_t x0 = 0; x0 < T; x0 += 64) {
+          const int64_t x = x0 + lane;
+          const uint32_t u = x < T ? tile_ub(x) : 0u;
+          if (u > bu) {
+            bu = u;
+            bx = x;
           }
-          cnt += __popcll(km);
-          if (cnt > C - 64) compact();
+        }
+        for (; ns < a.nseed && ns < kMaxSeed; ns++) {
+          const uint32_t top = wave_max_u32(bu);
+          if (top == 0) break;
+          const uint64_t wm = (uint64_t)__ballot(bu == top);
+          const int wl = (int)__builtin_ctzll(wm);
+          seed[ns] = rl64(bx, wl);
+          if (lane == wl) bu = 0;
+        }
+        for (int s = 0; s < ns; s++) tile(seed[s]);
+      }
+      // 2. sweep in docno order
+      for (int64_t x0 = 0; x0 < T; x0 += 64) {
+        const int64_t x = x0 + lane;
+        uint32_t u = 0;
+        if (x < T) {
+          bool seeded = false;
+          for (int s = 0; s < ns; s++) seeded |= seed[s] == x;
+          if (!seeded) u = tile_ub(x);
+        }
+        uint64_t vm = (uint64_t)__ballot(u >= gate && u > 0);
+        while (vm) {
+          const int j = (int)__builtin_ctzll(vm);
+          vm &= vm - 1;
+          if ((uint32_t)__builtin_amdgcn_readlane((int)u, j) >= gate) tile(x0 + j);
         }
       }
-      int32_t nt_ = nx;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) nt_ = min(nt_, __shfl_xor(nt_, o, 64));
-      if (nt_ == tile + 1) {
-        mc = me;
-        me = me1;
-      } else if (nt_ != 0x7FFFFFFF && lane < nt && mdf > 0) {
-        mc = mrow[nt_];
-        me = mrow[nt_ + 1];
-      }
-      tile = nt_;
     }
     __syncthreads();
     compact();
-    if (stats) {
+    if (a.stats) {
       uint32_t c = st_cand;
       for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
       if (lane == 0) {
-        atomicAdd(stats + 0, (unsigned long long)st_tiles);
-        atomicAdd(stats + 1, (unsigned long long)st_gated);
-        atomicAdd(stats + 2, (unsigned long long)c);
-        atomicAdd(stats + 3, (unsigned long long)st_comp);
-        atomicAdd(stats + 4, (unsigned long long)st_sparse);
+        atomicAdd(a.stats + 0, (unsigned long long)st_tiles);
+        atomicAdd(a.stats + 1, (unsigned long long)st_blocks);
+        atomicAdd(a.stats + 2, (unsigned long long)c);
+        atomicAdd(a.stats + 3, (unsigned long long)st_comp);
       }
     }
-    for (int r = lane; r < k; r += 64) {
-      out_d[(int64_t)q * k + r] = r < cnt ? bd[r] : -1;
-      out_s[(int64_t)q * k + r] = r < cnt ? bs[r] : 0.0;
+    for (int r = lane; r < a.k; r += 64) {
+      a.out_d[(int64_t)q * a.k + r] = r < cnt ? bd[r] : -1;
+      a.out_s[(int64_t)q * a.k + r] = r < cnt ? bs[r] : 0.0;
     }
     __syncthreads();
   }
+}
+
+// Index-resident heavy rows (see k_query_bm): built once per index and heavy
+// threshold; tf-based, so TF-IDF reweighting keeps them.
+void prepare_queries(sme_index *ix, hipStream_t st) {
+  sme_ctx *cx = ix->ctx;
+  const int64_t div = cx->opt_heavy_div;
+  if (ix->q_ready && ix->q_div == div) return;
+  hipEvent_t e0, e1;
+  SME_HIP(hipEventCreate(&e0));
+  SME_HIP(hipEventCreate(&e1));
+  SME_HIP(hipEventRecord(e0, st));
+  ix->q_H = 0;
+  ix->q_T = (ix->V > 0 && ix->P > 0 && ix->dmax >= ix->dmin) ? ((ix->dmax - ix->dmin) >> kQB) + 1 : 0;
+  const int64_t V = ix->V, T = ix->q_T;
+  if (T > 0 && div > 0) {
+    auto &W = cx->ws;
+    const int64_t *off = (const int64_t *)ix->d_off.p;
+    const int64_t span = ix->dmax - ix->dmin + 1, stride = T << kQB;
+    int32_t *flag = W[36].as<int32_t>(V + 1), *scan = W[37].as<int32_t>(V + 1);
+    SME_HIP(hipMemsetAsync(flag + V, 0, sizeof(int32_t), st));
+    const unsigned gV = (unsigned)std::min<int64_t>((V + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_heavy_flags, dim3(gV), dim3(256), 0, st, off, (const int32_t *)ix->d_tf_o.p, V, span, div,
+                       flag);
+    size_t tbb = 0;
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, flag, scan, (int)V + 1, st));
+    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, flag, scan, (int)V + 1, st));
+    int32_t nh = 0;
+    SME_HIP(hipMemcpyAsync(&nh, scan + V, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    // memory budget for the rows: 1/8 of the device's free memory, at most 16 GB
+    size_t fr = 0, tot = 0;
+    SME_HIP(hipMemGetInfo(&fr, &tot));
+    const double per_row = (double)stride + (double)(T << 6) + (double)T;
+    const int64_t cap = (int64_t)(std::min<double>((double)fr / 8.0, 16e9) / per_row);
+    const int64_t H = std::min<int64_t>(nh, cap);
+    int32_t *hrow_of = ix->d_hrow_of.as<int32_t>(V);
+    int32_t *hterm = W[38].as<int32_t>(H + 1);
+    int64_t *hdf = W[39].as<int64_t>(H + 1), *hpre = W[40].as<int64_t>(H + 1);
+    hipLaunchKernelGGL(k_heavy_rows, dim3(gV), dim3(256), 0, st, flag, scan, V, H, off, hrow_of, hterm, hdf);
+    SME_CHECK_LAUNCH();
+    if (H > 0) {
+      SME_HIP(hipMemsetAsync(hdf + H, 0, sizeof(int64_t), st));
+      SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, hdf, hpre, (int)H + 1, st));
+      SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, hdf, hpre, (int)H + 1, st));
+      uint8_t *buf = ix->d_heavy.as<uint8_t>((size_t)H * (size_t)per_row + 64);
+      uint8_t *tfrow = buf, *bm16 = buf + H * stride, *bm1k = bm16 + H * (T << 6);
+      SME_HIP(hipMemsetAsync(tfrow, 0, (size_t)(H * stride), st));
+      hipLaunchKernelGGL(k_heavy_fill, dim3(16384), dim3(256), 0, st, hpre, H, hterm, off,
+                         (const int32_t *)ix->d_docno_d.p, (const int32_t *)ix->d_tf_d.p, ix->dmin, stride, tfrow);
+      const int64_t n16 = H * (T << 6), n1k = H * T;
+      hipLaunchKernelGGL(k_heavy_bm16, dim3((unsigned)std::min<int64_t>((n16 + 255) / 256, 1 << 16)), dim3(256), 0,
+                         st, (const uint4 *)tfrow, n16, bm16);
+      hipLaunchKernelGGL(k_heavy_bm1k, dim3((unsigned)std::min<int64_t>((n1k + 255) / 256, 1 << 16)), dim3(256), 0,
+                         st, (const uint4 *)bm16, n1k, bm1k);
+      SME_CHECK_LAUNCH();
+      ix->q_tfrow = tfrow;
+      ix->q_bm16 = bm16;
+      ix->q_bm1k = bm1k;
+    }
+    ix->q_H = H;
+  }
+  SME_HIP(hipEventRecord(e1, st));
+  SME_HIP(hipEventSynchronize(e1));
+  float ms = 0;
+  SME_HIP(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  ix->q_prep_ms = ms;
+  ix->q_div = div;
+  ix->q_ready = true;
 }
 
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k, int32_t *d_out_docno,
@@ -829,7 +985,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   if (k < 1) throw Error(SME_EINVAL, "k must be >= 1");
   if (k > 448) throw Error(SME_ELIMIT, "top-k with k > 448");
   if (nq <= 0) return;
-  auto &W = ix->ctx->ws;
+  sme_ctx *cx = ix->ctx;
+  auto &W = cx->ws;
   int *err = W[63].as<int>(4);
   unsigned long long *wmax = reinterpret_cast<unsigned long long *>(err + 2);
   SME_HIP(hipMemsetAsync(err, 0, 4 * sizeof(int), st));
@@ -839,18 +996,17 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   const double *lut = (const double *)ix->d_lut.p;
   const double *idf = (const double *)ix->d_idf.p;
   const int64_t V = ix->V;
+  // the block-max path unless a query is longer than kIMaxTerms or the batch's
+  // skip table would be unreasonably large; option query_kernel = 1 forces the
+  // streaming kernel (tests run both)
+  bool tiled = V > 0 && ix->P > 0 && ix->dmax >= ix->dmin && cx->opt_query_kernel != 1;
+  if (tiled) prepare_queries(ix, st);  // once per index (timed separately: q_prep_ms)
   hipEvent_t ep;
   SME_HIP(hipEventCreate(&ep));
   SME_HIP(hipEventRecord(ep, st));
-  // Tiled path unless a query is longer than kIMaxTerms or the batch's skip
-  // table would be unreasonably large; SME_QUERY_KERNEL=stream forces the
-  // streaming kernel (tests run both).
-  const char *force = getenv("SME_QUERY_KERNEL");
-  bool tiled = V > 0 && ix->P > 0 && ix->dmax >= ix->dmin && !(force && strcmp(force, "stream") == 0);
-  const int64_t T = tiled ? ((ix->dmax - ix->dmin) >> kWBits) + 1 : 0;
-  const int32_t *row_of = nullptr, *sk = nullptr, *drow = nullptr;
-  const uint8_t *dtf = nullptr, *dq = nullptr;
-  int64_t dstride = 0;
+  const int64_t T = tiled ? ix->q_T : 0;
+  const int32_t *row_of = nullptr, *sk = nullptr;
+  const uint8_t *qlut = nullptr;
   int h_mx = 0;
   if (tiled) {
     hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
@@ -860,7 +1016,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     SME_HIP(hipStreamSynchronize(st));
     tiled = h_mx <= kIMaxTerms;
     if (tiled) {
-      // distinct batch terms -> rows of the skip table
+      // distinct batch terms -> rows of the skip and impact tables
       int32_t *mark = W[55].as<int32_t>(V + 1), *rowo = W[56].as<int32_t>(V + 1);
       SME_HIP(hipMemsetAsync(mark, 0, (V + 1) * sizeof(int32_t), st));
       if (nterm > 0)
@@ -868,7 +1024,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
                            d_terms, nterm, V, mark);
       size_t tbb = 0;
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, mark, rowo, (int)V + 1, st));
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, mark, rowo, (int)V + 1, st));
+      SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, mark, rowo, (int)V + 1, st));
       int32_t nrows32 = 0;
       SME_HIP(hipMemcpyAsync(&nrows32, rowo + V, sizeof(int32_t), hipMemcpyDeviceToHost, st));
       SME_HIP(hipStreamSynchronize(st));
@@ -878,7 +1034,9 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       } else {
         row_of = rowo;
         int32_t *skw = W[60].as<int32_t>(std::max<int64_t>(nrows, 1) * (T + 1));
+        uint8_t *ql = W[44].as<uint8_t>(std::max<int64_t>(nrows, 1) * 256);
         sk = skw;
+        qlut = ql;
         if (nrows > 0) {
           int32_t *tor = W[57].as<int32_t>(nrows + 1);
           int64_t *rdf = W[58].as<int64_t>(nrows + 1), *rpre = W[59].as<int64_t>(nrows + 1);
@@ -886,93 +1044,84 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           hipLaunchKernelGGL(k_term_rows, dim3(gV), dim3(256), 0, st, mark, rowo, V, off, tor, rdf);
           SME_HIP(hipMemsetAsync(rdf + nrows, 0, sizeof(int64_t), st));
           SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, rdf, rpre, (int)nrows + 1, st));
-          SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, rdf, rpre, (int)nrows + 1, st));
+          SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, rdf, rpre, (int)nrows + 1, st));
           SME_HIP(hipMemsetAsync(skw, 0x7F, (size_t)nrows * (T + 1) * sizeof(int32_t), st));
           hipLaunchKernelGGL(k_skip_zero_rows, dim3((unsigned)std::min<int64_t>(nrows, 4096)), dim3(256), 0, st, rdf,
                              nrows, T, skw);
           hipLaunchKernelGGL(k_skip_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T, skw);
           hipLaunchKernelGGL(k_skip_suffix, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 16384)), dim3(256), 0,
                              st, nrows, T, skw);
-          // largest weight of the batch (impact scale) and the dense-row terms
-          // (SME_QDENSE=div, 0 = posting path only; tests run several)
-          const char *ed = getenv("SME_QDENSE");
-          const int64_t ddiv = ed ? atoll(ed) : 32;
-          const int64_t span = ix->dmax - ix->dmin + 1, stride = T << kWBits;
-          int32_t *flag = W[53].as<int32_t>(nrows + 1), *dscan = W[54].as<int32_t>(nrows + 1);
-          const unsigned gR = (unsigned)std::min<int64_t>((nrows + 256) / 256, 8192);
-          hipLaunchKernelGGL(k_row_stats, dim3(gR), dim3(256), 0, st, tor, rdf, nrows, off,
-                             (const int32_t *)ix->d_tf_o.p, lut, idf, span, ddiv, flag, wmax);
+          const unsigned gR = (unsigned)std::min<int64_t>((nrows + 255) / 256, 8192);
+          hipLaunchKernelGGL(k_row_wmax, dim3(gR), dim3(256), 0, st, tor, rdf, nrows, off,
+                             (const int32_t *)ix->d_tf_o.p, lut, idf, wmax);
+          hipLaunchKernelGGL(k_row_qlut, dim3((unsigned)std::min<int64_t>(nrows, 16384)), dim3(256), 0, st, tor, nrows,
+                             lut, ix->max_tf, idf, (const unsigned long long *)wmax, ql);
           SME_CHECK_LAUNCH();
-          if (ddiv > 0) {
-            const int64_t cap = std::max<int64_t>(1, (int64_t)2e9 / stride);
-            SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, flag, dscan, (int)nrows + 1, st));
-            SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tbb), tbb, flag, dscan, (int)nrows + 1, st));
-            int32_t ndense = 0;
-            SME_HIP(hipMemcpyAsync(&ndense, dscan + nrows, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-            SME_HIP(hipStreamSynchronize(st));
-            const int64_t nd = std::min<int64_t>(ndense, cap);
-            if (nd > 0) {
-              int32_t *drw = W[62].as<int32_t>(nrows);
-              uint8_t *dns = W[61].as<uint8_t>(2 * nd * stride);
-              SME_HIP(hipMemsetAsync(dns, 0, (size_t)(2 * nd * stride), st));
-              hipLaunchKernelGGL(k_dense_rows, dim3(gR), dim3(256), 0, st, flag, dscan, nrows, cap, drw);
-              hipLaunchKernelGGL(k_dense_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, drw, tor, off, dn, tf, lut,
-                                 idf, wmax, ix->dmin, stride, dns, dns + nd * stride);
-              SME_CHECK_LAUNCH();
-              dtf = dns;
-              dq = dns + nd * stride;
-              drow = drw;
-              dstride = stride;
-            }
-          }
         }
       }
     }
   }
   if (!tiled && k > 32) throw Error(SME_ENOTIMPL, "top-k with k > 32 for queries of more than 64 terms");
-  int sh = 0;
   const int32_t *qord = nullptr;
-  if (tiled) {
-    // impact shift: 255 * 2^sh * (terms per query) <= 65535 keeps the u16 sums exact
-    sh = 0;
-    while (sh < 5 && 255 * (2 << sh) * std::max(h_mx, 1) <= 65535) sh++;
-    // heaviest-term query order (SME_QORDER=0: batch order)
-    const char *eo = getenv("SME_QORDER");
-    if (!(eo && atoi(eo) == 0)) {
-      uint64_t *qk = W[46].as<uint64_t>(2 * (size_t)nq);
-      int32_t *qi = W[45].as<int32_t>(2 * (size_t)nq);
-      hipLaunchKernelGGL(k_query_keys, dim3(std::min((nq + 255) / 256, 4096)), dim3(256), 0, st, d_terms, d_qoff, nq, off,
-                         V, qk, qi);
-      size_t tbb = 0;
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, qk, qk + nq, qi, qi + nq, nq, 0, 64, st));
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(ix->ctx->cub_tmp.get(tbb), tbb, qk, qk + nq, qi, qi + nq, nq, 0, 64,
-                                                 st));
-      qord = qi + nq;
-    }
+  if (tiled && cx->opt_query_order) {
+    // heaviest-term query order
+    uint64_t *qk = W[46].as<uint64_t>(2 * (size_t)nq);
+    int32_t *qi = W[45].as<int32_t>(2 * (size_t)nq);
+    hipLaunchKernelGGL(k_query_keys, dim3(std::min((nq + 255) / 256, 4096)), dim3(256), 0, st, d_terms, d_qoff, nq, off,
+                       V, qk, qi);
+    size_t tbb = 0;
+    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, qk, qk + nq, qi, qi + nq, nq, 0, 64, st));
+    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cx->cub_tmp.get(tbb), tbb, qk, qk + nq, qi, qi + nq, nq, 0, 64, st));
+    qord = qi + nq;
   }
   // events on the launch stream bracket the scoring kernel (bench.py roofline)
   hipEvent_t e0, e1;
   SME_HIP(hipEventCreate(&e0));
   SME_HIP(hipEventCreate(&e1));
   SME_HIP(hipEventRecord(e0, st));
-  const char *ex = getenv("SME_QEXP");  // timing experiments only (wrong results): 1 no candidates, 2 no postings
-  const int qexp = ex ? atoi(ex) : 0;
   unsigned long long *qstats = nullptr;
+#ifdef SME_EXPERIMENTS
   const char *eq = getenv("SME_QSTATS");
   if (eq && atoi(eq)) {
     qstats = reinterpret_cast<unsigned long long *>(W[47].as<uint64_t>(8));
     SME_HIP(hipMemsetAsync(qstats, 0, 8 * sizeof(uint64_t), st));
   }
+#endif
   if (tiled) {
+    QBmArgs qa;
+    qa.off = off;
+    qa.docno = dn;
+    qa.tf = tf;
+    qa.tf_o = (const int32_t *)ix->d_tf_o.p;
+    qa.lut = lut;
+    qa.idf = idf;
+    qa.V = V;
+    qa.row_of = row_of;
+    qa.sk = sk;
+    qa.qlut = qlut;
+    qa.hrow_of = ix->q_H > 0 ? (const int32_t *)ix->d_hrow_of.p : nullptr;
+    qa.tfrow = ix->q_tfrow;
+    qa.bm16 = ix->q_bm16;
+    qa.bm1k = ix->q_bm1k;
+    qa.dmin = ix->dmin;
+    qa.T = T;
+    qa.terms = d_terms;
+    qa.qoff = d_qoff;
+    qa.qorder = qord;
+    qa.nq = nq;
+    qa.k = k;
+    qa.nseed = (int)std::max<int64_t>(0, std::min<int64_t>(cx->opt_seed_tiles, kMaxSeed));
+    qa.out_d = d_out_docno;
+    qa.out_s = d_out_score;
+    qa.wmax_bits = (const unsigned long long *)wmax;
+    qa.stats = qstats;
     const unsigned wgrid = (unsigned)std::min<int64_t>(8 * (((int64_t)nq + 7) / 8), 1 << 30);
-#define SME_QI(C)                                                                                                \
-  hipLaunchKernelGGL(k_query_imp<C>, dim3(wgrid), dim3(64), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, row_of, sk, \
-                     ix->dmin, T, d_terms, d_qoff, qord, nq, k, d_out_docno, d_out_score, dtf, dq, drow, dstride,    \
-                     (const unsigned long long *)wmax, sh, qstats, qexp)
-    if (k <= 64) SME_QI(128);
-    else if (k <= 192) SME_QI(256);
-    else SME_QI(512);
-#undef SME_QI
+    if (k <= 64)
+      hipLaunchKernelGGL(k_query_bm<128>, dim3(wgrid), dim3(64), 0, st, qa);
+    else if (k <= 192)
+      hipLaunchKernelGGL(k_query_bm<256>, dim3(wgrid), dim3(64), 0, st, qa);
+    else
+      hipLaunchKernelGGL(k_query_bm<512>, dim3(wgrid), dim3(64), 0, st, qa);
   } else if (k <= 16) {
     const unsigned grid = (unsigned)std::min(nq, 1 << 20);
     hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
@@ -990,21 +1139,22 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   float ms = 0, pms = 0;
   SME_HIP(hipEventElapsedTime(&ms, e0, e1));
   SME_HIP(hipEventElapsedTime(&pms, ep, e0));
-  ix->ctx->last_query_ms = ms;
-  ix->ctx->last_query_prep_ms = pms;
+  cx->last_query_ms = ms;
+  cx->last_query_prep_ms = pms;
+  cx->last_query_index_ms = tiled ? ix->q_prep_ms : 0.0f;
   (void)hipEventDestroy(ep);
-  ix->ctx->last_query_tiled = tiled;
+  cx->last_query_tiled = tiled;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   if (qstats) {
     uint64_t h[8];
     SME_HIP(hipMemcpy(h, qstats, sizeof h, hipMemcpyDeviceToHost));
-    fprintf(stderr, "SME_QSTATS tiles=%llu gated=%llu candidates=%llu compactions=%llu sparse_tiles=%llu\n",
-            (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
-            (unsigned long long)h[4]);
+    fprintf(stderr, "SME_QSTATS tiles=%llu blocks_gated=%llu candidates=%llu compactions=%llu\n",
+            (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3]);
   }
   if (h_err) throw Error(SME_ELIMIT, "a query has more than 128 terms");
 }
+
 
 // ---------------------------------------------------------------------------
 // processContent on one string (query parsing), single lane

@@ -116,6 +116,54 @@ __device__ __forceinline__ const unicase_ent *unicase_lookup(uint32_t cp) {
   return nullptr;
 }
 
+__device__ __forceinline__ bool in_cp_ranges(const unsigned int (*r)[2], int nr, uint32_t cp) {
+  int lo = 0, hi = nr - 1;
+  while (lo <= hi) {
+    const int m = (lo + hi) >> 1;
+    if (cp < r[m][0])
+      hi = m - 1;
+    else if (cp > r[m][1])
+      lo = m + 1;
+    else
+      return true;
+  }
+  return false;
+}
+// Final_Sigma context of U+03A3 at unit i of a[0..n) (String.toLowerCase ->
+// U+03C2, ConditionalSpecialCasing): a cased letter before it with only
+// case-ignorables between, and no cased letter after it (case-ignorables
+// skipped).  Tables from tools/gen_unicase.py.
+__device__ inline bool final_sigma(const uint16_t *a, int n, int i) {
+  int j = i;
+  uint32_t c = 0;
+  bool found = false;
+  while (j > 0) {
+    if (j >= 2 && a[j - 1] >= 0xDC00 && a[j - 1] <= 0xDFFF && a[j - 2] >= 0xD800 && a[j - 2] <= 0xDBFF) {
+      c = 0x10000 + ((uint32_t)(a[j - 2] - 0xD800) << 10) + (a[j - 1] - 0xDC00u);
+      j -= 2;
+    } else {
+      c = a[j - 1];
+      j -= 1;
+    }
+    if (!in_cp_ranges(UNISIGMA_CI, UNISIGMA_CI_N, c)) {
+      found = true;
+      break;
+    }
+  }
+  if (!found || !in_cp_ranges(UNISIGMA_CASED, UNISIGMA_CASED_N, c)) return false;
+  for (j = i + 1; j < n;) {
+    if (a[j] >= 0xD800 && a[j] <= 0xDBFF && j + 1 < n && a[j + 1] >= 0xDC00 && a[j + 1] <= 0xDFFF) {
+      c = 0x10000 + ((uint32_t)(a[j] - 0xD800) << 10) + (a[j + 1] - 0xDC00u);
+      j += 2;
+    } else {
+      c = a[j];
+      j += 1;
+    }
+    if (!in_cp_ranges(UNISIGMA_CI, UNISIGMA_CI_N, c)) return !in_cp_ranges(UNISIGMA_CASED, UNISIGMA_CASED_N, c);
+  }
+  return true;
+}
+
 // Appends lower(a[0..n)) to out (capacity cap); returns new length or -1 on overflow.
 __device__ inline int java_lower(const uint16_t *a, int n, uint16_t *out, int cap) {
   int k = 0;
@@ -126,7 +174,10 @@ __device__ inline int java_lower(const uint16_t *a, int n, uint16_t *out, int ca
       cp = 0x10000 + ((cp - 0xD800) << 10) + (a[i + 1] - 0xDC00u);
       w = 2;
     }
-    if (cp < 0x80) {
+    if (cp == 0x03A3 && final_sigma(a, n, i)) {
+      if (k >= cap) return -1;
+      out[k++] = 0x03C2;
+    } else if (cp < 0x80) {
       if (k >= cap) return -1;
       out[k++] = (uint16_t)((cp >= 'A' && cp <= 'Z') ? cp + 32 : cp);
     } else {

@@ -16,8 +16,9 @@ the small global statistics and the query results:
                    returned per LOCAL term for sme_index_reweight
   global_df_index  the same for a libsme shard, keyed by 128-bit device term
                    fingerprints (all_gather + torch.unique, no host strings)
-  merge_topk       per-shard top-k -> global top-k, (score desc, docno asc)
-                   (all_gather of Q x k x (4 + 8) B)
+  merge_topk_owner per-shard top-k -> global top-k of the queries a rank owns
+                   (query-owner all_to_all of Q x k x (4 + 8) B, score desc,
+                   docno asc); merge_topk also all_gathers the merged slices
 
 Exactness: with docids unique across shards (every synthetic corpus), the sharded
 result equals the single-index result bit for bit: a document's score only uses its
@@ -132,18 +133,44 @@ def global_df(local_df, l2g, n_global_terms, group=None):
     return g[torch.from_numpy(l2g).to(dev)] if len(l2g) else g[:0]
 
 
-def global_df_index(ix, group=None):
+def _hip_d2d(dst, src, nbytes, stream):
+    import ctypes as C
+    h = C.CDLL("libamdhip64.so")
+    h.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+    rc = h.hipMemcpyAsync(C.c_void_p(dst), C.c_void_p(src), nbytes, 3, C.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError("hipMemcpyAsync failed: %d" % rc)
+
+
+def global_df_index(ix, group=None, timings=None):
     """All-reduced df per LOCAL term of a libsme shard index, as a CUDA int64 tensor
     ready for sme_index_reweight: shards agree on terms through their 128-bit device
     fingerprints (sme_index_term_fingerprints), gathered and deduplicated with
-    torch.unique on the collective's device -- no term strings on the host."""
+    torch.unique on the collective's device -- no term strings on the host, and the
+    shard's df comes from its device offsets (never through host memory).
+
+    Everything runs on torch's current stream (the fingerprints and the offsets copy
+    are issued on it), and the stream is synchronized before returning, so the
+    result is ready for a reweight on any stream.  `timings` (a dict) receives the
+    wall ms of the fingerprint, gather, unique and reduce steps."""
+    import time
     dev = _dev(group)
     world = dist.get_world_size(group)
     V = int(ix.V)
-    fp = torch.zeros((max(V, 1), 2), dtype=torch.int64, device="cuda")
+    cs = torch.cuda.current_stream()
+    t0 = time.perf_counter()
+    fp = torch.empty((max(V, 1), 2), dtype=torch.int64, device="cuda")
+    offs = torch.empty(V + 1, dtype=torch.int64, device="cuda")
     if V:
-        ix.term_fingerprints(fp.data_ptr())
+        ix.term_fingerprints(fp.data_ptr(), cs.cuda_stream)  # every row written
+        o_ptr, _, _ = ix.device_arrays()
+        _hip_d2d(offs.data_ptr(), o_ptr, 8 * (V + 1), cs.cuda_stream)
+    else:
+        offs.zero_()
+    df = (offs[1:] - offs[:-1]).to(dev)
     fp = fp[:V].to(dev)
+    cs.synchronize()
+    t1 = time.perf_counter()
     n = torch.tensor([V], dtype=torch.int64, device=dev)
     ns = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(ns, n, group=group)
@@ -151,34 +178,45 @@ def global_df_index(ix, group=None):
     m = max(max(ns), 1)
     pad = torch.zeros((m, 2), dtype=torch.int64, device=dev)
     pad[:V] = fp
-    outs = [torch.zeros_like(pad) for _ in range(world)]
+    outs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(outs, pad, group=group)
     allfp = torch.cat([o[:c] for o, c in zip(outs, ns)], 0)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t2 = time.perf_counter()
     uniq, inv = torch.unique(allfp, dim=0, return_inverse=True)
     r = dist.get_rank(group)
     mine = inv[sum(ns[:r]):sum(ns[:r]) + V]
-    df = torch.from_numpy(np.diff(ix.offsets())).to(dev)
     g = torch.zeros(uniq.shape[0], dtype=torch.int64, device=dev)
     if V:
         g.index_add_(0, mine, df)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t3 = time.perf_counter()
     dist.all_reduce(g, group=group)
-    return g[mine].to("cuda").contiguous()
+    out = g[mine].to("cuda").contiguous()
+    torch.cuda.current_stream().synchronize()
+    t4 = time.perf_counter()
+    if timings is not None:
+        timings.update(fingerprints_ms=(t1 - t0) * 1e3, all_gather_ms=(t2 - t1) * 1e3, unique_ms=(t3 - t2) * 1e3,
+                       all_reduce_ms=(t4 - t3) * 1e3, local_terms=V, gathered_terms=int(allfp.shape[0]),
+                       global_terms=int(uniq.shape[0]))
+    return out
 
 
-def merge_topk(docno, score, k, group=None):
-    """docno int32 [Q, k] (-1 pads), score float64 [Q, k] torch tensors of this
-    shard -> global (docno, score) [Q, k]: score desc, docno asc."""
-    world = dist.get_world_size(group)
-    gs = [torch.empty_like(score) for _ in range(world)]
-    gd = [torch.empty_like(docno) for _ in range(world)]
-    dist.all_gather(gs, score, group=group)
-    dist.all_gather(gd, docno, group=group)
-    s = torch.cat(gs, 1)
-    d = torch.cat(gd, 1).to(torch.int64)
+def owner_bounds(nq, world):
+    """Query-owner split: rank r merges queries [b[r], b[r+1])."""
+    return [nq * r // world for r in range(world + 1)]
+
+
+def _merge_rows(s, d, k):
+    """rows of candidate (score, docno) lists -> the best k per row, (score desc,
+    docno asc); docno -1 pads."""
+    d = d.to(torch.int64)
     valid = d >= 0
     s = torch.where(valid, s, torch.full_like(s, -float("inf")))
     d = torch.where(valid, d, torch.full_like(d, 1 << 40))
-    # (score desc, docno asc): stable sort by docno, then stable sort by -score
+    # stable sort by docno, then stable sort by -score
     i1 = torch.argsort(d, dim=1, stable=True)
     s1, d1 = torch.gather(s, 1, i1), torch.gather(d, 1, i1)
     i2 = torch.argsort(-s1, dim=1, stable=True)[:, :k]
@@ -186,3 +224,45 @@ def merge_topk(docno, score, k, group=None):
     pad = out_d >= (1 << 40)
     return (torch.where(pad, torch.full_like(out_d, -1), out_d).to(torch.int32),
             torch.where(pad, torch.zeros_like(out_s), out_s))
+
+
+def merge_topk_owner(docno, score, k, group=None):
+    """Query-owner merge: docno int32 [Q, k] (-1 pads), score float64
+    [Q, k] of this shard -> (q0, q1, docno [q1-q0, k], score [q1-q0, k]), the global
+    top-k of the queries this rank owns.  One all_to_all moves every shard's lists
+    of query q to q's owner (Q x k x 12 B per rank in all), and each rank sorts only
+    its Q/W queries' W x k candidates."""
+    world, r = dist.get_world_size(group), dist.get_rank(group)
+    nq = docno.shape[0]
+    b = owner_bounds(nq, world)
+    my = b[r + 1] - b[r]
+    ins = [(b[i + 1] - b[i]) * k for i in range(world)]
+    rs = torch.empty(world * my * k, dtype=score.dtype, device=score.device)
+    rd = torch.empty(world * my * k, dtype=docno.dtype, device=docno.device)
+    dist.all_to_all_single(rs, score.contiguous().reshape(-1), [my * k] * world, ins, group=group)
+    dist.all_to_all_single(rd, docno.contiguous().reshape(-1), [my * k] * world, ins, group=group)
+    s = rs.reshape(world, my, k).permute(1, 0, 2).reshape(my, world * k)
+    d = rd.reshape(world, my, k).permute(1, 0, 2).reshape(my, world * k)
+    md, ms = _merge_rows(s, d, k)
+    return b[r], b[r + 1], md, ms
+
+
+def merge_topk(docno, score, k, group=None):
+    """Global (docno, score) [Q, k] on every rank: the query-owner merge, then an
+    all_gather of the merged slices (Q x k x 12 B, not W x Q x k)."""
+    world = dist.get_world_size(group)
+    nq = docno.shape[0]
+    q0, q1, md, ms = merge_topk_owner(docno, score, k, group)
+    b = owner_bounds(nq, world)
+    m = max(b[i + 1] - b[i] for i in range(world))
+    pd = torch.full((m, k), -1, dtype=md.dtype, device=md.device)
+    ps = torch.zeros((m, k), dtype=ms.dtype, device=ms.device)
+    pd[:q1 - q0] = md
+    ps[:q1 - q0] = ms
+    gd = [torch.empty_like(pd) for _ in range(world)]
+    gs = [torch.empty_like(ps) for _ in range(world)]
+    dist.all_gather(gd, pd, group=group)
+    dist.all_gather(gs, ps, group=group)
+    out_d = torch.cat([x[:b[i + 1] - b[i]] for i, x in enumerate(gd)], 0)
+    out_s = torch.cat([x[:b[i + 1] - b[i]] for i, x in enumerate(gs)], 0)
+    return out_d, out_s

@@ -120,3 +120,38 @@ def canon_digest(buf):
             h.update(buf[i:i + 8 + rl])
         i += 8 + rl
     return h.hexdigest()
+
+
+def np_rank(off, dn, tf, terms_q, N, k, idf_mode=0, df=None):
+    """rank() of IntDocVectorsForwardIndex (C/sa/edu/kaust/fwindex/
+    IntDocVectorsForwardIndex.java:192-223) restated with numpy over a CSR (any
+    posting order per term): for each query token in order, every posting adds
+    (1 + ln tf) * log10(N / df) to its document's score -- one fp64 add per token
+    and document, so a dense accumulator reproduces the JVM's sequential sum bit
+    for bit (the first add is 0.0 + w = w).  1 + ln tf comes from libm log
+    (math.log), as the device's shared LUT does.  Top-k by (score desc, docno
+    asc).  Size-independent: used at full c2 size where the C oracle is too slow."""
+    import math
+    import numpy as np
+    if not len(terms_q):
+        return [], []
+    dmin = min(int(dn[off[t]:off[t + 1]].min()) for t in terms_q if off[t + 1] > off[t]) \
+        if any(off[t + 1] > off[t] for t in terms_q) else 0
+    dmax = max(int(dn[off[t]:off[t + 1]].max()) for t in terms_q if off[t + 1] > off[t]) \
+        if any(off[t + 1] > off[t] for t in terms_q) else -1
+    if dmax < dmin:
+        return [], []
+    acc = np.zeros(dmax - dmin + 1, np.float64)
+    hit = np.zeros(dmax - dmin + 1, bool)
+    mt = max(int(tf[off[t]:off[t + 1]].max()) for t in terms_q if off[t + 1] > off[t])
+    lut = np.array([0.0] + [1.0 + math.log(float(i)) for i in range(1, mt + 1)], np.float64)
+    for t in terms_q:
+        sd = 1 if idf_mode == 0 else int(df[t])
+        idf = math.log10(float(N // sd))
+        d = dn[off[t]:off[t + 1]].astype(np.int64) - dmin
+        acc[d] += lut[tf[off[t]:off[t + 1]]] * idf
+        hit[d] = True
+    docs = np.nonzero(hit)[0]
+    sc = acc[docs]
+    order = np.lexsort((docs, -sc))[:k]
+    return (docs[order] + dmin).tolist(), sc[order].tolist()

@@ -54,6 +54,8 @@ def main():
         for k in (10, 100):
             dn, sc = ix.query_topk(ids, qoff, k)
             md, ms = D.merge_topk(torch.from_numpy(dn), torch.from_numpy(sc), k)
+            q0, q1, od, osc = D.merge_topk_owner(torch.from_numpy(dn), torch.from_numpy(sc), k)
+            assert torch.equal(od, md[q0:q1]) and torch.equal(osc, ms[q0:q1])
             for q, tl in enumerate(queries):
                 rd, rs = full.query(tl, k, idf_mode, 0)
                 assert md[q, :len(rd)].tolist() == rd, (k, q, tl)

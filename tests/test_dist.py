@@ -83,6 +83,9 @@ def _worker(rank, world, port, idf_mode, out_dir):
         for q, tq in enumerate(queries):
             dn[q], sc[q] = _shard_scores(tq, local, N, df_of, idf_mode, k)
         md, ms = D.merge_topk(torch.from_numpy(dn), torch.from_numpy(sc), k)
+        q0, q1, od, osc = D.merge_topk_owner(torch.from_numpy(dn), torch.from_numpy(sc), k)
+        assert (q0, q1) == tuple(D.owner_bounds(len(queries), world)[rank:rank + 2])
+        assert torch.equal(od, md[q0:q1]) and torch.equal(osc, ms[q0:q1])  # the owner's slice
         for q, tq in enumerate(queries):
             rd, rs = full.query(tq, k, idf_mode, 0)
             assert md[q, :len(rd)].tolist() == rd, (q, tq)
@@ -93,10 +96,10 @@ def _worker(rank, world, port, idf_mode, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("idf_mode", [0, 1])
-def test_two_shards_gloo(tmp_path, idf_mode):
-    mp.spawn(_worker, args=(2, _free_port(), idf_mode, str(tmp_path)), nprocs=2, join=True)
-    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
+@pytest.mark.parametrize("idf_mode,world", [(0, 2), (1, 2), (0, 3)])
+def test_two_shards_gloo(tmp_path, idf_mode, world):
+    mp.spawn(_worker, args=(world, _free_port(), idf_mode, str(tmp_path)), nprocs=world, join=True)
+    assert all((tmp_path / ("ok%d" % r)).exists() for r in range(world))
 
 
 def test_cuts_own_every_record_and_quirks():

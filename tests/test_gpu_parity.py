@@ -177,31 +177,31 @@ def test_queries_vs_oracle(sme, synth, idf_mode):
         assert (dn[q, k:] == -1).all()
 
 
-def _query_env(ix, terms, qoff, k, **env):
-    old = {n: os.environ.get(n) for n in env}
-    os.environ.update({n: str(v) for n, v in env.items()})
+def _query_opts(ix, terms, qoff, k, **opts):
+    """Query with context path options set (sme_set_option), then restore the defaults."""
+    defaults = {"query_kernel": 0, "heavy_div": 32, "seed_tiles": 4, "query_order": 1}
     try:
+        for n, v in opts.items():
+            ix.ctx.set_option(n, v)
         return ix.query_topk(terms, qoff, k)
     finally:
-        for n, v in old.items():
-            if v is None:
-                del os.environ[n]
-            else:
-                os.environ[n] = v
+        for n in opts:
+            ix.ctx.set_option(n, defaults[n])
 
 
 def _query_both_kernels(ix, terms, qoff, k):
-    """Default tiled scoring (impact-gated, dense rows for terms covering >= 1/4
-    of the docno span), the tiled kernel on postings only, every term on dense
-    rows, only full-span terms dense, and the streaming kernel (k <= 32): all
-    identical bits."""
+    """Default block-max scoring (heavy rows for terms covering >= 1/32 of the
+    docno span, 4 seed tiles), the same on postings only, every term heavy, only
+    full-span terms heavy, no seed tiles, batch query order, and the streaming
+    kernel (k <= 32): all identical bits."""
     dn, sc = ix.query_topk(terms, qoff, k)
-    envs = [{"SME_QDENSE": 0}, {"SME_QDENSE": 1 << 30}, {"SME_QDENSE": 1}]
+    variants = [{"heavy_div": 0}, {"heavy_div": 1 << 30}, {"heavy_div": 1}, {"seed_tiles": 0},
+                {"seed_tiles": 8, "query_order": 0}]
     if k <= 32:
-        envs.append({"SME_QUERY_KERNEL": "stream"})
-    for env in envs:
-        dn2, sc2 = _query_env(ix, terms, qoff, k, **env)
-        assert np.array_equal(dn, dn2) and np.array_equal(sc, sc2), env
+        variants.append({"query_kernel": 1})
+    for v in variants:
+        dn2, sc2 = _query_opts(ix, terms, qoff, k, **v)
+        assert np.array_equal(dn, dn2) and np.array_equal(sc, sc2), v
     return dn, sc
 
 
@@ -226,13 +226,21 @@ def test_queries_multi_tile(sme, synth):
             rd, rs = ref.query(tl, 10, 0, 0)
             assert dn[q, :len(rd)].tolist() == rd, q
             assert np.array_equal(sc[q, :len(rd)], np.array(rs)), q
-    # a 20-term query in the batch: whole batch through the streaming kernel
-    long_terms = np.concatenate([tu[:ou[3]], np.arange(20, dtype=np.int32)])
-    long_off = np.concatenate([ou[:4], [ou[3] + 20]]).astype(np.int64)
-    dn, sc = ix.query_topk(long_terms, long_off, 10)
-    tl = [names[t] for t in range(20)]
-    rd, rs = ref.query(tl, 10, 0, 0)
-    assert dn[3, :len(rd)].tolist() == rd and np.array_equal(sc[3, :len(rd)], np.array(rs))
+    # 64-term queries stay on the block-max kernel (more than its 16 heavy
+    # slots: the rest take the posting path); the heaviest terms repeated push
+    # every impact sum towards 64 x 254.  A 65-term query sends the whole batch
+    # to the streaming kernel.
+    heavy = np.argsort(-df, kind="stable")[:8].astype(np.int32)
+    for nlong in (64, 65):
+        q64 = np.concatenate([np.repeat(heavy, 4), np.arange(nlong - 32, dtype=np.int32)])
+        long_terms = np.concatenate([tu[:ou[3]], q64])
+        long_off = np.concatenate([ou[:4], [ou[3] + nlong]]).astype(np.int64)
+        dn, sc = ix.query_topk(long_terms, long_off, 10)
+        assert ix.ctx.last_build_profile()["query_kernel_name"] == ("k_query_bm" if nlong == 64 else "k_query")
+        for q in range(4):
+            tl = [names[t] for t in long_terms[long_off[q]:long_off[q + 1]] if t >= 0]
+            rd, rs = ref.query(tl, 10, 0, 0)
+            assert dn[q, :len(rd)].tolist() == rd and np.array_equal(sc[q, :len(rd)], np.array(rs)), (nlong, q)
 
 
 def test_queries_dense_rows(sme, synth):

@@ -8,8 +8,12 @@
   tools/gen_scale_golden.py): per-partition record digests, N / V / P / sum tf,
   and top-10 / top-100 query results -- docnos identical, fp64 scores bit-equal --
   for c3-drawn (by df), uniform and true-df-mode queries.
-* c2 full size (1M docs) is checked by size-independent properties in
-  test_c2_full_properties.
+* c2 full size (1M docs, BASELINE configs[1]) in test_c2_full_properties:
+  size-independent properties of the built index (sum tf = tokens + docid
+  tokens, offsets monotone, reduce order (tf desc, docno asc), docno order of
+  the query CSR) and c3-drawn queries over it (configs[2]'s distribution)
+  checked against a numpy restatement of rank() over the index's own postings
+  (tests/common.py np_rank), docnos and fp64 score bits.
 """
 import json
 import os
@@ -76,3 +80,33 @@ def test_scale_build_and_queries(sme, synth, name):
         corpus, ctx, ix = _build(sme, synth, g, idf_mode=1)
         for group in groups:
             _check_queries(ix, group)
+
+
+def test_c2_full_properties(sme, synth):
+    import common
+    n, V, seed, lo, hi = 1_000_000, 1 << 20, 42, 400, 600
+    corpus = sme.DeviceCorpus(n, V=V, seed=seed, len_lo=lo, len_hi=hi)
+    ctx = sme.Context(1, 1, 0)
+    ctx.load_docno_mapping(synth.mapping_bytes(n))
+    ix = ctx.build_device(corpus.ptr, corpus.nbytes)
+    corpus.close()
+    assert ix.N == n
+    off, dn, tf, df = ix.csr()
+    lens = synth.doc_lengths(0, n, seed, lo, hi)
+    assert int(tf.astype(np.int64).sum()) == int(lens.sum()) + n  # every token + the docid term (T7)
+    assert off[0] == 0 and off[-1] == ix.P and (np.diff(off) >= 1).all()
+    newt = np.zeros(ix.P, bool)
+    newt[off[:-1]] = True
+    same = ~newt[1:]
+    assert (((tf[1:] <= tf[:-1]) | ~same).all())  # tf desc inside a term
+    assert (((tf[1:] != tf[:-1]) | (dn[1:] > dn[:-1]) | ~same).all())  # then docno asc
+    o2, dd, _ = ix.weights()
+    assert np.array_equal(o2, off) and ((dd[1:] > dd[:-1]) | ~same).all()
+    del dd, newt, same
+    terms, qoff = synth.queries_by_df(df, 300, seed=7)
+    for k in (10, 100):
+        got_d, got_s = ix.query_topk(terms, qoff, k)
+        for q in range(0, 300, 3 if k == 10 else 15):
+            rd, rs = common.np_rank(off, dn, tf, terms[qoff[q]:qoff[q + 1]].tolist(), ix.N, k)
+            assert got_d[q, :len(rd)].tolist() == rd, (k, q)
+            assert got_s[q, :len(rd)].tolist() == rs, (k, q)  # fp64 bit-equal

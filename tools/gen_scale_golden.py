@@ -11,10 +11,14 @@ device against them:
            df + 200 uniform, top-10; 200 top-100; 200 in true-df idf mode).
   c5shard  100,000 docs of the c5 distribution (V_w = 30,000, 40-72 tokens,
            seed 9), R = 1: digests and 500 top-100 queries drawn by df.
+  c4multi  60,000 docs of the c4 distribution (V_w = 2^22, 200-360 tokens,
+           seed 44), the whole corpus as ONE index: the reference of the
+           4-shard multi-rank test (600 + 100 uniform top-10 queries in
+           reference idf mode, 300 top-10 and 100 top-100 in true-df mode).
 
 Queries are stored as term strings; expected results as docnos and the fp64
 scores' hex (bit-exact comparison).  Run from the repo root:
-    python tools/gen_scale_golden.py [c2shard|c5shard ...]
+    python tools/gen_scale_golden.py [c2shard|c5shard|c4multi ...]
 """
 import hashlib
 import importlib
@@ -38,6 +42,11 @@ CONFIGS = {
                              ("df", 200, 27, 10, 1)]),
     "c5shard": dict(n=100000, V=30000, seed=9, lo=40, hi=72, R=1,
                     queries=[("df", 500, 9, 100, 0), ("df", 100, 19, 10, 1)]),
+    # c4 distribution, 4 doc shards of 15,000 docs (tests/test_dist_gpu.py: four
+    # rank processes, fingerprint df all-reduce, reweight, query-owner merge)
+    "c4multi": dict(n=60000, V=1 << 22, seed=44, lo=200, hi=360, R=1,
+                    queries=[("df", 600, 7, 10, 0), ("uniform", 100, 8, 10, 0), ("df", 300, 27, 10, 1),
+                             ("df", 100, 17, 100, 1)]),
 }
 
 
@@ -74,4 +83,4 @@ def main(names):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or list(CONFIGS))
+    main(sys.argv[1:] or ["c2shard", "c5shard"])
