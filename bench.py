@@ -72,6 +72,7 @@ def parse():
     p.add_argument("--cpu-ref-queries", type=int, default=50, help="queries timed with the ref-faithful rank()")
     p.add_argument("--cpu-opt-queries", type=int, default=20000, help="queries timed with the cpu-opt rank()")
     p.add_argument("--no-query", action="store_true")
+    p.add_argument("--no-e2e", action="store_true", help="skip the untimed host-to-host end-to-end stage")
     a = p.parse_args()
     cfg = dict(CONFIGS[a.config])
     for key in ("docs", "vocab", "queries"):
@@ -223,6 +224,14 @@ def main():
     }
     if query is not None:
         result["query"] = query
+    # calibration: the achievable HBM rate of a streaming copy on this device,
+    # reported beside the 8 TB/s spec every frac above is priced against
+    cal = C.c_double()
+    if L.sme_hbm_copy_bench(local, 4 << 30, 10, C.byref(cal)) == 0:
+        result["roofline"]["peak_measured_copy"] = round(cal.value, 1)
+        result["roofline"]["frac_of_measured"] = (round(tok_gbs / cal.value, 5) if tok_gbs else None)
+        result["hbm_copy_GBps"] = {"value": round(cal.value, 1), "what": "sme_hbm_copy_bench: 4 GiB device copy, "
+                                   "16-byte nontemporal loads/stores, read + write bytes / kernel time (x10)"}
     if df_ex is not None:
         result["df_exchange_untimed"] = df_ex
     qinternal = None
@@ -230,12 +239,23 @@ def main():
         qinternal = (query.pop("_terms"), query.pop("_qoff"), query.pop("_out"))
     if not a.no_checks:
         result["checks"] = post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank)
-        result["stage_ms"]["serialize_records_untimed"] = serialize_stage(ix)
+        result["stage_ms"]["serialize_records_untimed"] = serialize_stage(ix, torch)
+    cpu_full = None
+    if rank == 0 and a.cpu_docs > 0 and a.config == "c2" and qinternal is not None:
+        cpu_full = cpu_query_full(ix, qinternal, a)
+    if not a.no_e2e and world == 1:
+        ix.close()
+        ix = None
+        gc.collect()
+        result["end_to_end_ms"] = end_to_end_stage(sme, ctx, d_corpus.value, nbytes, torch)
     if rank == 0 and a.cpu_docs > 0 and a.config == "c2":
         result["cpu_baseline"] = cpu_baseline(synth, a)
+        if cpu_full is not None:
+            result["cpu_baseline"]["cpu_opt"].update(cpu_full)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    ix.close()
+    if ix is not None:
+        ix.close()
     ctx.close()
     L.sme_synth_free(d_corpus)
     if dist is not None:
@@ -400,12 +420,69 @@ def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank):
     return out
 
 
-def serialize_stage(ix):
-    """I9: the partition records (device serializer + copy to the host), untimed."""
+def serialize_stage(ix, torch):
+    """I9: the partition records, untimed, as its own stage: the device serializer
+    (k_ser_*, HIP events) and the copy of the concatenated record stream to host
+    memory -- pinned (the drop-in's direct ByteBuffer case: one DMA) and pageable
+    (through the library's pinned staging)."""
+    offs, dev_ms = ix.serialize()
+    total = int(offs[-1])
+    host = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
     t0 = time.perf_counter()
-    n = sum(len(ix.partition_records(p)) for p in range(ix.ctx.num_partitions))
-    return {"ms": round((time.perf_counter() - t0) * 1e3, 2), "bytes": n,
-            "what": "sme_index_partition_records for every partition (device k_ser_* + D2H), after the timed steps"}
+    n = ix.copy_records(-1, hv)
+    pin_ms = (time.perf_counter() - t0) * 1e3
+    del host, hv
+    page = np.empty(max(total, 1), np.uint8)
+    page[::4096] = 0  # pages touched once (first-touch faults are not the copy)
+    t0 = time.perf_counter()
+    ix.copy_records(-1, page)
+    page_ms = (time.perf_counter() - t0) * 1e3
+    del page
+    return {"device_ms": round(dev_ms, 3), "d2h_pinned_ms": round(pin_ms, 2), "d2h_pageable_ms": round(page_ms, 2),
+            "ms": round(dev_ms + pin_ms, 2), "bytes": n, "d2h_pinned_GBps": round(n / pin_ms / 1e6, 2),
+            "d2h_pageable_GBps": round(n / page_ms / 1e6, 2),
+            "what": "sme_index_serialize (device k_ser_* time) + sme_index_copy_records(-1) of every partition's "
+                    "records into pinned host memory; 'ms' = device + pinned copy, after the timed steps"}
+
+
+def end_to_end_stage(sme, ctx, d_corpus, nbytes, torch, reps=2):
+    """Host corpus -> part-file records on the host, untimed in the step: the
+    corpus sits in pinned host memory (the drop-in's direct ByteBuffer), then
+    sme_build_index (H2D + build) + sme_index_serialize + sme_index_copy_records
+    into pinned host memory.  Best of `reps` after one warm-up call."""
+    host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    _hip_copy(host.data_ptr(), d_corpus, nbytes, 2)
+    out = None
+    best = None
+    for i in range(reps + 1):
+        t0 = time.perf_counter()
+        ix = ctx.build_ptr(host.data_ptr(), nbytes)
+        t1 = time.perf_counter()
+        offs, dev_ms = ix.serialize()
+        if out is None:
+            out = torch.empty(max(int(offs[-1]), 1), dtype=torch.uint8, pin_memory=True)
+        n = ix.copy_records(-1, out.numpy())
+        t2 = time.perf_counter()
+        prof = ctx.last_build_profile()
+        ix.close()
+        if i > 0 and (best is None or t2 - t0 < best["ms"] / 1e3):
+            best = {"ms": round((t2 - t0) * 1e3, 2), "build_from_host_ms": round((t1 - t0) * 1e3, 2),
+                    "build_device_ms": prof.get("total"), "serialize_device_ms": round(dev_ms, 3),
+                    "serialize_and_d2h_ms": round((t2 - t1) * 1e3, 2), "record_bytes": n}
+    best["h2d_ms_est"] = round(best["build_from_host_ms"] - (best["build_device_ms"] or 0.0), 2)
+    best["GBps_text"] = round(nbytes / best["ms"] / 1e6, 2)
+    best["what"] = ("pinned host corpus -> sme_build_index (H2D + build + TF-IDF) -> sme_index_serialize -> "
+                    "sme_index_copy_records into pinned host memory; best of %d after a warm-up" % reps)
+    del host, out
+    return best
+
+
+def _hip_copy(dst, src, n, kind):
+    h = C.CDLL("libamdhip64.so")
+    h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    rc = h.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), n, kind)
+    assert rc == 0, rc
 
 
 def pmc_traffic(kernel, a, detail=False):
@@ -438,6 +515,36 @@ def _cpu_model():
     return None
 
 
+def cpu_threads():
+    """Threads the CPU legs use: OMP_NUM_THREADS when set (the GPU box sets it to
+    the CPU share it grants one GPU's job, 16), else every CPU this process may
+    run on (sched_getaffinity)."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    return env or aff, aff
+
+
+def cpu_query_full(ix, qinternal, a):
+    """cpu-opt rank() over the SAME full-size index as the GPU query batch: the
+    device-built CSR (held equal to the oracle's by the parity tests) wrapped as a
+    cpu-opt index, the first queries of the same c3 batch, all granted threads."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    terms, qoff, _ = qinternal
+    threads, _ = cpu_threads()
+    off, dn, tf, _ = ix.csr()
+    cix = O.CpuOptIndex.from_csr(ix.N, off, dn, tf)
+    nq = min(a.cpu_opt_queries, len(qoff) - 1)
+    _, _, dt = cix.query(terms[:qoff[nq]], qoff[:nq + 1], a.cfg["k"], 0, threads)
+    del cix, off, dn, tf
+    return {"query_qps_full_index": round(nq / dt, 1), "query_full_index_docs": ix.N,
+            "query_full_index_sample": "first %d queries of the GPU's c3 batch over the full %d-doc c2 index "
+                                       "(device-built CSR), %d threads, %.2f s" % (nq, ix.N, threads, dt)}
+
+
 def cpu_baseline(synth, a):
     """BASELINE.md section 2, on this box's host cores, bounded samples of the c2 / c3
     distributions (the oracle is the checker and the timed CPU port; the tests hold
@@ -449,8 +556,11 @@ def cpu_baseline(synth, a):
     `value` is the cpu-opt build rate (the honest CPU comparison)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    out = {"unit": "GB/s", "cores": threads, "kind": "port", "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
+    threads, aff = cpu_threads()
+    out = {"unit": "GB/s", "cores": threads, "kind": "port", "nproc": os.cpu_count(), "affinity_cpus": aff,
+           "cpu_model": _cpu_model(),
+           "cores_what": "threads used = OMP_NUM_THREADS (the GPU box's CPU share for one GPU's job; nproc "
+                         "shows the whole host) or the affinity set"}
     # ref-faithful build + rank() (indexOf scan) on a small sample
     n_ref = a.cpu_docs
     corpus = synth.gen_corpus(n_ref, V=a.vocab, seed=42, len_lo=400, len_hi=600)
@@ -489,8 +599,10 @@ def cpu_baseline(synth, a):
     out["value"] = round(len(corpus) / dt_opt / 1e9, 6)
     out["sample"] = ("cpu-opt (%d threads): build of %d docs (%d bytes) of c2 in %.1f s; %d c3-style top-10 queries "
                      "over that index in %.2f s" % (threads, n_opt, len(corpus), dt_opt, a.cpu_opt_queries, dt_q))
-    out["cpu_opt"] = {"build_GBps": out["value"], "query_qps": round(a.cpu_opt_queries / dt_q, 1),
-                      "query_index_docs": n_opt}
+    out["cpu_opt"] = {"build_GBps": out["value"], "build_GBps_per_thread": round(out["value"] / threads, 6),
+                      "query_qps": round(a.cpu_opt_queries / dt_q, 1), "query_index_docs": n_opt,
+                      "query_what": "query_qps: over the %d-doc sample index; query_qps_full_index: over the "
+                                    "GPU's full-size index" % n_opt}
     return out
 
 

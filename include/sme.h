@@ -49,7 +49,13 @@ extern "C" {
 #define SME_IDF_TRUE_DF 1   /* log10(N / df) with df = postings length, int division as the reference */
 
 /* tiebreak */
-#define SME_TIE_DOCNO 0 /* score desc, then docno asc (north-star contract) */
+#define SME_TIE_DOCNO 0     /* score desc, then docno asc (north-star contract) */
+#define SME_TIE_REFERENCE 1 /* score desc, then the reference's printed order: rank() appends
+                               candidates in first-encounter order (query token order, each term's
+                               postings tf desc / docno asc) and Collections.sort over DocScore
+                               (IntDocVectorsForwardIndex.java:195-215,363-365) is a stable sort by
+                               score desc (its merge sort only asks compareTo <= 0 / > 0, which is
+                               score order for finite scores), so equal scores keep that order */
 
 typedef struct sme_ctx sme_ctx;
 typedef struct sme_index sme_index;
@@ -143,6 +149,21 @@ int sme_index_stats(const sme_index *ix, uint64_t *N, uint64_t *V, uint64_t *P);
  * on the host and is owned by ix. */
 int sme_index_partition_records(sme_index *ix, int part, const uint8_t **buf, size_t *n);
 
+/* The device half of the same output (the serializer kernels k_ser_*, run once
+ * per index): part_offsets (R+1 host entries, may be NULL) gets the byte offset
+ * of every partition in the concatenated record stream (partition order), and
+ * *device_ms (may be NULL) the serializer's device time.  Replaces the reduce
+ * tasks' record writes, TermKGramDocIndexer.java:275 (SequenceFileOutputFormat)
+ * + TermDF.java:50-56 + ArrayListWritable.java:90-105. */
+int sme_index_serialize(sme_index *ix, uint64_t *part_offsets, float *device_ms);
+
+/* Copy the record bytes of partition `part` (part = -1: every partition, back
+ * to back in partition order) from HBM into caller memory dst of cap bytes;
+ * *n gets the bytes written.  Pinned dst (hipHostMalloc / hipHostRegister,
+ * e.g. a pinned direct ByteBuffer) is one DMA; pageable dst goes through the
+ * context's pinned staging buffers.  No intermediate host copy is kept. */
+int sme_index_copy_records(sme_index *ix, int part, void *dst, size_t cap, size_t *n);
+
 /* Host copies of the CSR in reduce-output order (tf desc, docno asc) over
  * terms in TermDF key order.  offsets has V+1 entries; true_df has V. */
 int sme_index_csr(sme_index *ix, const int64_t **offsets, const int32_t **docno,
@@ -178,6 +199,9 @@ int sme_lookup_terms(sme_index *ix, const uint8_t *terms, const int64_t *offs, i
  * docno -1 / score 0 when fewer than k documents match. */
 int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq,
                    int k, int32_t *out_docno, double *out_score);
+/* The same plus every result's tie word (see sme_query_topk_device_tie). */
+int sme_query_topk_tie(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq,
+                       int k, int32_t *out_docno, double *out_score, uint32_t *out_tie);
 
 /* Query-side structures of an index (the role the reference's forward index,
  * BuildIntDocVectorsForwardIndex.java:84-158, plays for rank()): heavy-term tf
@@ -189,6 +213,15 @@ int sme_index_prepare_queries(sme_index *ix, void *stream, float *ms);
 /* Same with all arrays already in device memory (timed path). */
 int sme_query_topk_device(sme_index *ix, const int32_t *d_term_ids, const int64_t *d_q_offsets,
                           int nq, int k, int32_t *d_out_docno, double *d_out_score, void *stream);
+
+/* The same plus the tie word of every result (d_out_tie[nq * k], 0xFFFFFFFF
+ * padding): 0 under SME_TIE_DOCNO; under SME_TIE_REFERENCE (first query token
+ * holding the document) << 24 | (2^24 - 1 - its tf).  Results of doc shards
+ * merge by (score desc, tie asc, docno asc) into the single index's order
+ * (dist.py merge_topk_owner). */
+int sme_query_topk_device_tie(sme_index *ix, const int32_t *d_term_ids, const int64_t *d_q_offsets,
+                              int nq, int k, int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie,
+                              void *stream);
 
 /* 128-bit fingerprint of every index term (two u64 per term into device memory
  * d_out[2 V]): equal term strings (k-grams) on different shards get equal
@@ -209,6 +242,10 @@ int sme_synth_corpus(int device, const uint8_t *vocab, const int64_t *vocab_off,
                      int64_t n_docs, int64_t d0, uint64_t seed, int len_lo, int len_hi, void **d_corpus,
                      size_t *nbytes);
 void sme_synth_free(void *d_corpus);
+
+/* Calibration (bench.py): achievable HBM bandwidth of a streaming device copy of
+ * `bytes` (x reps, after a warm-up); *gbps = read + write bytes / kernel time. */
+int sme_hbm_copy_bench(int device, size_t bytes, int reps, double *gbps);
 
 /* Timing of the last build, per stage, in milliseconds (device events on the
  * build stream), as a JSON object; "tok_kernel" brackets exactly the tokenizer

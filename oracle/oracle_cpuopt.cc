@@ -297,6 +297,21 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
 
 void or_cpuopt_free(void *h) { delete (CpuIndex *)h; }
 
+/* An index over given CSR arrays (reduce order, no term strings), so the cpu-opt
+ * rank() can be timed over an index too large to build on the CPU inside a bench
+ * (bench.py: the GPU-built full-size c2 index, held equal to the oracle's by the
+ * parity tests). */
+void *or_cpuopt_from_csr(int64_t N, int64_t V, const int64_t *off, const int32_t *docno, const int32_t *tf) {
+  CpuIndex *ix = new CpuIndex();
+  ix->N = N;
+  ix->V = V;
+  ix->off.assign(off, off + V + 1);
+  ix->P = ix->off[(size_t)V];
+  ix->docno.assign(docno, docno + ix->P);
+  ix->tf.assign(tf, tf + ix->P);
+  return ix;
+}
+
 void or_cpuopt_stats(const void *h, int64_t *N, int64_t *V, int64_t *P, double *build_s) {
   const CpuIndex *ix = (const CpuIndex *)h;
   *N = ix->N;

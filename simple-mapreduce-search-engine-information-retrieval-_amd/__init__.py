@@ -22,6 +22,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SME_LIB_PATH") or os.path.join(_HERE, "libsme.so")
 
 SME_IDF_REFERENCE = 0
+SME_TIE_DOCNO = 0      # score desc, docno asc (north star)
+SME_TIE_REFERENCE = 1  # score desc, then rank()'s printed order (first encounter; include/sme.h)
 SME_IDF_TRUE_DF = 1
 
 
@@ -40,12 +42,13 @@ _lib = None
 
 EXPORTS = [
     "sme_last_error", "sme_version", "sme_create", "sme_destroy", "sme_load_docno_mapping", "sme_build_index",
-    "sme_build_index_device", "sme_index_free", "sme_index_stats", "sme_index_partition_records", "sme_index_csr",
+    "sme_build_index_device", "sme_index_free", "sme_index_stats", "sme_index_partition_records", "sme_index_serialize",
+    "sme_index_copy_records", "sme_index_csr",
     "sme_index_device_arrays", "sme_index_term", "sme_tokenize", "sme_lookup_terms", "sme_query_topk",
-    "sme_query_topk_device", "sme_last_build_profile", "sme_index_reweight", "sme_number_documents",
+    "sme_query_topk_device", "sme_query_topk_device_tie", "sme_query_topk_tie", "sme_last_build_profile", "sme_index_reweight", "sme_number_documents",
     "sme_build_chargram", "sme_build_chargram_device", "sme_chargram_partition_text", "sme_chargram_stats",
     "sme_split_points", "sme_split_points_device", "sme_index_term_fingerprints", "sme_set_option",
-    "sme_index_prepare_queries",
+    "sme_index_prepare_queries", "sme_hbm_copy_bench",
 ]
 
 
@@ -70,6 +73,8 @@ def lib():
     L.sme_index_free.restype = None
     L.sme_index_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.sme_index_partition_records.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
+    L.sme_index_serialize.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_float)]
+    L.sme_index_copy_records.argtypes = [vp, C.c_int, vp, sz, C.POINTER(sz)]
     L.sme_index_csr.argtypes = [vp, C.POINTER(i64p), C.POINTER(i32p), C.POINTER(i32p), C.POINTER(i32p)]
     L.sme_index_device_arrays.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
     L.sme_index_term.argtypes = [vp, C.c_int64, C.POINTER(vp), C.POINTER(sz)]
@@ -77,6 +82,9 @@ def lib():
     L.sme_lookup_terms.argtypes = [vp, C.c_char_p, i64p, C.c_int, i32p]
     L.sme_query_topk.argtypes = [vp, i32p, i64p, C.c_int, C.c_int, i32p, C.POINTER(C.c_double)]
     L.sme_query_topk_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp]
+    L.sme_query_topk_device_tie.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, vp]
+    L.sme_query_topk_tie.argtypes = [vp, i32p, i64p, C.c_int, C.c_int, i32p, C.POINTER(C.c_double),
+                                     C.POINTER(C.c_uint32)]
     L.sme_last_build_profile.argtypes = [vp, C.POINTER(C.c_char_p)]
     L.sme_index_reweight.argtypes = [vp, C.c_int64, vp, vp]
     L.sme_number_documents.argtypes = [vp, C.c_char_p, sz, C.POINTER(vp), C.POINTER(sz)]
@@ -92,6 +100,7 @@ def lib():
     L.sme_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
     L.sme_index_prepare_queries.argtypes = [vp, vp, C.POINTER(C.c_float)]
     L.sme_synth_free.argtypes = [vp]
+    L.sme_hbm_copy_bench.argtypes = [C.c_int, sz, C.c_int, C.POINTER(C.c_double)]
     L.sme_synth_free.restype = None
     _lib = L
     return L
@@ -156,12 +165,13 @@ class TrecDocnoMapping:
 class Context:
     """One device context (sme_ctx): config + docno mapping + reusable HBM workspace."""
 
-    def __init__(self, k=1, num_partitions=1, idf_mode=SME_IDF_REFERENCE, device=0):
-        cfg = _Config(k, num_partitions, idf_mode, 0, device)
+    def __init__(self, k=1, num_partitions=1, idf_mode=SME_IDF_REFERENCE, device=0, tiebreak=SME_TIE_DOCNO):
+        cfg = _Config(k, num_partitions, idf_mode, tiebreak, device)
         h = C.c_void_p()
         _check(lib().sme_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self.k, self.num_partitions, self.idf_mode, self.device = k, num_partitions, idf_mode, device
+        self.tiebreak = tiebreak
 
     def close(self):
         if getattr(self, "_h", None):
@@ -188,6 +198,13 @@ class Context:
         """Build from host bytes (copied to HBM)."""
         h = C.c_void_p()
         _check(lib().sme_build_index(self._h, corpus, len(corpus), C.byref(h)))
+        return Index(h, self)
+
+    def build_ptr(self, host_ptr, nbytes):
+        """Build from nbytes of host memory at address host_ptr (pinned memory is
+        copied to HBM at DMA rate)."""
+        h = C.c_void_p()
+        _check(lib().sme_build_index(self._h, C.cast(C.c_void_p(host_ptr), C.c_char_p), nbytes, C.byref(h)))
         return Index(h, self)
 
     def build_device(self, d_ptr, nbytes, stream=None):
@@ -245,9 +262,34 @@ class Index:
         self.close()
 
     def partition_records(self, part):
-        p, n = C.c_void_p(), C.c_size_t()
-        _check(lib().sme_index_partition_records(self._h, part, C.byref(p), C.byref(n)))
-        return _host_bytes(p, n.value)
+        """Record bytes of reduce partition `part` (bytes; one D2H copy into them)."""
+        offs, _ = self.serialize()
+        out = bytearray(int(offs[part + 1] - offs[part]))
+        self.copy_records(part, out)
+        return bytes(out) if len(out) < (1 << 26) else out
+
+    def serialize(self):
+        """Device serialization of every partition (once per index):
+        (partition byte offsets [R+1] in the concatenated stream, k_ser_* device ms)."""
+        R = self.ctx.num_partitions
+        offs = (C.c_uint64 * (R + 1))()
+        ms = C.c_float()
+        _check(lib().sme_index_serialize(self._h, offs, C.byref(ms)))
+        return np.array(offs[:], dtype=np.int64), float(ms.value)
+
+    def copy_records(self, part, out):
+        """Copy partition `part`'s records (part = -1: all partitions back to back)
+        into `out` (a writable buffer: bytearray, numpy uint8 array, pinned torch
+        tensor's numpy view ...) straight from HBM; returns the byte count."""
+        n = C.c_size_t()
+        if hasattr(out, "ctypes"):
+            ptr, cap = out.ctypes.data, out.nbytes
+        else:
+            mv = memoryview(out)
+            cap = mv.nbytes
+            ptr = C.addressof((C.c_char * max(cap, 1)).from_buffer(out)) if cap else None
+        _check(lib().sme_index_copy_records(self._h, part, ptr, cap, C.byref(n)))
+        return n.value
 
     def csr(self):
         """(offsets[V+1], docno[P], tf[P], true_df[V]) in reduce-output order (tf desc, docno asc)."""
@@ -306,18 +348,23 @@ class Index:
                                       ids.ctypes.data_as(C.POINTER(C.c_int32))))
         return ids[:len(bs)]
 
-    def query_topk(self, term_ids, q_offsets, k=10):
-        """Batched rank(): returns (docno[nq,k], score[nq,k]); docno -1 pads."""
+    def query_topk(self, term_ids, q_offsets, k=10, with_tie=False):
+        """Batched rank(): returns (docno[nq,k], score[nq,k]); docno -1 pads.
+        with_tie: also the uint32 tie word of every result (sme_query_topk_tie),
+        the key doc-shard merges need under SME_TIE_REFERENCE."""
         term_ids = np.ascontiguousarray(term_ids, dtype=np.int32)
         q_offsets = np.ascontiguousarray(q_offsets, dtype=np.int64)
         nq = len(q_offsets) - 1
         dn = np.zeros((max(nq, 1), k), dtype=np.int32)
         sc = np.zeros((max(nq, 1), k), dtype=np.float64)
-        _check(lib().sme_query_topk(self._h, term_ids.ctypes.data_as(C.POINTER(C.c_int32)),
-                                    q_offsets.ctypes.data_as(C.POINTER(C.c_int64)), nq, k,
-                                    dn.ctypes.data_as(C.POINTER(C.c_int32)),
-                                    sc.ctypes.data_as(C.POINTER(C.c_double))))
-        return dn[:nq], sc[:nq]
+        args = [self._h, term_ids.ctypes.data_as(C.POINTER(C.c_int32)), q_offsets.ctypes.data_as(C.POINTER(C.c_int64)),
+                nq, k, dn.ctypes.data_as(C.POINTER(C.c_int32)), sc.ctypes.data_as(C.POINTER(C.c_double))]
+        if not with_tie:
+            _check(lib().sme_query_topk(*args))
+            return dn[:nq], sc[:nq]
+        tie = np.zeros((max(nq, 1), k), dtype=np.uint32)
+        _check(lib().sme_query_topk_tie(*args, tie.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return dn[:nq], sc[:nq], tie[:nq]
 
     def prepare_queries(self, stream=None):
         """Build the query-side heavy rows now (else the first query batch does);
@@ -330,9 +377,15 @@ class Index:
         """TF-IDF weights with all-reduced N (and df) of a doc-sharded index."""
         _check(lib().sme_index_reweight(self._h, n_global, C.c_void_p(d_df_global or 0), C.c_void_p(stream or 0)))
 
-    def query_topk_device(self, d_terms, d_qoff, nq, k, d_out_docno, d_out_score, stream=None):
-        _check(lib().sme_query_topk_device(self._h, C.c_void_p(d_terms), C.c_void_p(d_qoff), nq, k,
-                                           C.c_void_p(d_out_docno), C.c_void_p(d_out_score), C.c_void_p(stream or 0)))
+    def query_topk_device(self, d_terms, d_qoff, nq, k, d_out_docno, d_out_score, stream=None, d_out_tie=None):
+        if d_out_tie is None:
+            _check(lib().sme_query_topk_device(self._h, C.c_void_p(d_terms), C.c_void_p(d_qoff), nq, k,
+                                               C.c_void_p(d_out_docno), C.c_void_p(d_out_score),
+                                               C.c_void_p(stream or 0)))
+        else:
+            _check(lib().sme_query_topk_device_tie(self._h, C.c_void_p(d_terms), C.c_void_p(d_qoff), nq, k,
+                                                   C.c_void_p(d_out_docno), C.c_void_p(d_out_score),
+                                                   C.c_void_p(d_out_tie), C.c_void_p(stream or 0)))
 
 
 class DeviceCorpus:

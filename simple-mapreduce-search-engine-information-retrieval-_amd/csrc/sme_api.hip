@@ -8,6 +8,7 @@
 #include <vector>
 
 #include <algorithm>
+#include <thread>
 
 #include "sme_internal.hpp"
 
@@ -127,6 +128,66 @@ void ensure_host_terms(sme_index *ix) {
   }
   ix->h_terms_ready = true;
 }
+
+// Device -> host copy of n bytes at d into dst.  Pinned dst (hipHostMalloc /
+// hipHostRegister memory): one DMA.  Pageable dst: 64 MiB chunks DMA'd into
+// the context's two pinned staging buffers while the host copies the previous
+// chunk out of the other buffer, spread over up to 8 threads (one host thread
+// moves ~10 GB/s; PCIe Gen5 x16 ~50 GB/s).  A plain pageable hipMemcpy of the
+// c2 record stream ran at ~2 GB/s.
+void copy_d2h(sme_ctx *cx, void *dst, const void *d, size_t n, hipStream_t st) {
+  if (!n) return;
+  hipPointerAttribute_t at{};
+  bool pinned = false;
+  if (hipPointerGetAttributes(&at, dst) == hipSuccess)
+    pinned = at.type == hipMemoryTypeHost;
+  else
+    (void)hipGetLastError();  // pageable memory: not an error for the caller
+  if (pinned) {
+    SME_HIP(hipMemcpyAsync(dst, d, n, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    return;
+  }
+  constexpr size_t kStage = size_t(64) << 20;
+  if (!cx->h_stage[0]) {
+    for (auto &b : cx->h_stage) SME_HIP(hipHostMalloc(&b, kStage, hipHostMallocDefault));
+    cx->h_stage_cap = kStage;
+  }
+  hipEvent_t ev[2];
+  for (auto &e : ev) SME_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  const size_t nch = (n + kStage - 1) / kStage;
+  auto issue = [&](size_t c) {
+    const size_t o = c * kStage, len = std::min(kStage, n - o);
+    SME_HIP(hipMemcpyAsync(cx->h_stage[c & 1], (const uint8_t *)d + o, len, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipEventRecord(ev[c & 1], st));
+  };
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned nth = std::min(8u, hw);
+  try {
+    issue(0);
+    for (size_t c = 0; c < nch; c++) {
+      SME_HIP(hipEventSynchronize(ev[c & 1]));
+      if (c + 1 < nch) issue(c + 1);  // the other buffer's chunk was copied out last iteration
+      const size_t o = c * kStage, len = std::min(kStage, n - o);
+      const uint8_t *src = (const uint8_t *)cx->h_stage[c & 1];
+      uint8_t *out = (uint8_t *)dst + o;
+      const unsigned t = len >= (size_t(8) << 20) ? nth : 1u;
+      const size_t per = (len + t - 1) / t;
+      std::vector<std::thread> th;
+      for (unsigned i = 1; i < t; i++) {
+        const size_t lo = std::min(len, i * per), hi = std::min(len, lo + per);
+        if (hi > lo) th.emplace_back([=] { memcpy(out + lo, src + lo, hi - lo); });
+      }
+      memcpy(out, src, std::min(len, per));
+      for (auto &x : th) x.join();
+    }
+  } catch (...) {
+    (void)hipStreamSynchronize(st);
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    throw;
+  }
+  for (auto &e : ev) (void)hipEventDestroy(e);
+}
 }  // namespace
 
 extern "C" {
@@ -141,7 +202,8 @@ int sme_create(const sme_config *cfg, sme_ctx **out) {
     if (cfg->num_partitions < 1) throw sme::Error(SME_EINVAL, "num_partitions must be >= 1");
     if (cfg->idf_mode != SME_IDF_REFERENCE && cfg->idf_mode != SME_IDF_TRUE_DF)
       throw sme::Error(SME_EINVAL, "bad idf_mode");
-    if (cfg->tiebreak != SME_TIE_DOCNO) throw sme::Error(SME_EINVAL, "bad tiebreak");
+    if (cfg->tiebreak != SME_TIE_DOCNO && cfg->tiebreak != SME_TIE_REFERENCE)
+      throw sme::Error(SME_EINVAL, "bad tiebreak");
     int ndev = 0;
     SME_HIP(hipGetDeviceCount(&ndev));
     if (cfg->device < 0 || cfg->device >= ndev) throw sme::Error(SME_EINVAL, "bad device ordinal");
@@ -197,6 +259,8 @@ static void ctx_release(sme_ctx *cx) {
   (void)hipSetDevice(cx->device);
   (void)hipDeviceSynchronize();
   if (cx->own_stream) (void)hipStreamDestroy(cx->own_stream);
+  for (auto &b : cx->h_stage)
+    if (b) (void)hipHostFree(b);
   delete cx;
 }
 
@@ -340,8 +404,9 @@ int sme_build_index(sme_ctx *cx, const uint8_t *corpus, size_t nbytes, sme_index
     if (!cx || !out || (!corpus && nbytes)) throw sme::Error(SME_EINVAL, "null argument");
     set_device(cx);
     hipStream_t st = cx->own_stream;
-    sme::DevBuf buf;
-    uint8_t *d = buf.as<uint8_t>(nbytes + 16);
+    // the corpus's device copy is kept in the context (no hipMalloc per build);
+    // a pinned host corpus is copied at DMA rate
+    uint8_t *d = cx->h_corpus_dev.as<uint8_t>(nbytes + 16);
     if (nbytes) SME_HIP(hipMemcpyAsync(d, corpus, nbytes, hipMemcpyHostToDevice, st));
     sme_index *ix = sme::build_index(cx, d, nbytes, st);
     SME_HIP(hipStreamSynchronize(st));
@@ -375,16 +440,40 @@ int sme_index_partition_records(sme_index *ix, int part, const uint8_t **buf, si
     set_device(ix->ctx);
     hipStream_t st = ix->ctx->own_stream;
     sme::serialize_index(ix, st);
+    const int64_t a = ix->part_start[part], b = ix->part_start[part + 1];
     if (!ix->h_parts_ready[part]) {
-      const int64_t a = ix->part_start[part], b = ix->part_start[part + 1];
-      ix->h_parts[part].resize((size_t)(b - a));
-      if (b > a)
-        SME_HIP(hipMemcpy(ix->h_parts[part].data(), (const uint8_t *)ix->d_ser.p + a, (size_t)(b - a),
-                          hipMemcpyDeviceToHost));
+      // default-initialised (not zero-filled) host storage, filled straight from HBM
+      ix->h_parts[part].reset(new uint8_t[(size_t)(b - a) + 1]);
+      copy_d2h(ix->ctx, ix->h_parts[part].get(), (const uint8_t *)ix->d_ser.p + a, (size_t)(b - a), st);
       ix->h_parts_ready[part] = 1;
     }
-    *buf = ix->h_parts[part].data();
-    *n = ix->h_parts[part].size();
+    *buf = ix->h_parts[part].get();
+    *n = (size_t)(b - a);
+  });
+}
+
+int sme_index_serialize(sme_index *ix, uint64_t *part_offsets, float *device_ms) {
+  return guard([&] {
+    if (!ix) throw sme::Error(SME_EINVAL, "null index");
+    set_device(ix->ctx);
+    sme::serialize_index(ix, ix->ctx->own_stream);
+    if (part_offsets)
+      for (int p = 0; p <= ix->R; p++) part_offsets[p] = (uint64_t)ix->part_start[p];
+    if (device_ms) *device_ms = ix->ser_ms;
+  });
+}
+
+int sme_index_copy_records(sme_index *ix, int part, void *dst, size_t cap, size_t *n) {
+  return guard([&] {
+    if (!ix || !n || (!dst && cap)) throw sme::Error(SME_EINVAL, "null argument");
+    if (part < -1 || part >= ix->R) throw sme::Error(SME_EINVAL, "partition out of range");
+    set_device(ix->ctx);
+    hipStream_t st = ix->ctx->own_stream;
+    sme::serialize_index(ix, st);
+    const int64_t a = part < 0 ? 0 : ix->part_start[part], b = part < 0 ? ix->part_start[ix->R] : ix->part_start[part + 1];
+    if ((size_t)(b - a) > cap) throw sme::Error(SME_EINVAL, "destination smaller than the records");
+    copy_d2h(ix->ctx, dst, (const uint8_t *)ix->d_ser.p + a, (size_t)(b - a), st);
+    *n = (size_t)(b - a);
   });
 }
 
@@ -484,12 +573,24 @@ int sme_query_topk_device(sme_index *ix, const int32_t *d_term_ids, const int64_
     if (!ix || (nq > 0 && (!d_term_ids || !d_q_offsets || !d_out_docno || !d_out_score)))
       throw sme::Error(SME_EINVAL, "null argument");
     set_device(ix->ctx);
-    sme::query_topk(ix, d_term_ids, d_q_offsets, nq, k, d_out_docno, d_out_score, stream_of(ix->ctx, stream));
+    sme::query_topk(ix, d_term_ids, d_q_offsets, nq, k, d_out_docno, d_out_score, nullptr,
+                    stream_of(ix->ctx, stream));
   });
 }
 
-int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq, int k,
-                   int32_t *out_docno, double *out_score) {
+int sme_query_topk_device_tie(sme_index *ix, const int32_t *d_term_ids, const int64_t *d_q_offsets, int nq, int k,
+                              int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie, void *stream) {
+  return guard([&] {
+    if (!ix || (nq > 0 && (!d_term_ids || !d_q_offsets || !d_out_docno || !d_out_score || !d_out_tie)))
+      throw sme::Error(SME_EINVAL, "null argument");
+    set_device(ix->ctx);
+    sme::query_topk(ix, d_term_ids, d_q_offsets, nq, k, d_out_docno, d_out_score, d_out_tie,
+                    stream_of(ix->ctx, stream));
+  });
+}
+
+static int query_topk_host(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq, int k,
+                           int32_t *out_docno, double *out_score, uint32_t *out_tie) {
   return guard([&] {
     if (!ix || (nq > 0 && (!term_ids || !q_offsets || !out_docno || !out_score)))
       throw sme::Error(SME_EINVAL, "null argument");
@@ -502,18 +603,32 @@ int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offs
     for (int64_t i = 0; i < nt; i++)
       if (term_ids[i] < -1 || term_ids[i] >= ix->V)
         throw sme::Error(SME_EINVAL, "term id " + std::to_string(term_ids[i]) + " outside [-1, V)");
-    sme::DevBuf a, b, c, d;
+    sme::DevBuf a, b, c, d, e;
     int32_t *dt = a.as<int32_t>(nt + 1);
     int64_t *dq = b.as<int64_t>(nq + 1);
     int32_t *dd = c.as<int32_t>((size_t)nq * k);
     double *ds = d.as<double>((size_t)nq * k);
+    uint32_t *dtie = out_tie ? e.as<uint32_t>((size_t)nq * k) : nullptr;
     if (nt) SME_HIP(hipMemcpyAsync(dt, term_ids, nt * sizeof(int32_t), hipMemcpyHostToDevice, st));
     SME_HIP(hipMemcpyAsync(dq, q_offsets, (nq + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    sme::query_topk(ix, dt, dq, nq, k, dd, ds, st);
+    sme::query_topk(ix, dt, dq, nq, k, dd, ds, dtie, st);
     SME_HIP(hipMemcpyAsync(out_docno, dd, (size_t)nq * k * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     SME_HIP(hipMemcpyAsync(out_score, ds, (size_t)nq * k * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (out_tie)
+      SME_HIP(hipMemcpyAsync(out_tie, dtie, (size_t)nq * k * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
   });
+}
+
+int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq, int k,
+                   int32_t *out_docno, double *out_score) {
+  return query_topk_host(ix, term_ids, q_offsets, nq, k, out_docno, out_score, nullptr);
+}
+
+int sme_query_topk_tie(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq, int k,
+                       int32_t *out_docno, double *out_score, uint32_t *out_tie) {
+  if (nq > 0 && !out_tie) return fail(SME_EINVAL, "null argument");
+  return query_topk_host(ix, term_ids, q_offsets, nq, k, out_docno, out_score, out_tie);
 }
 
 int sme_index_term_fingerprints(sme_index *ix, uint64_t *d_out, void *stream) {

@@ -284,7 +284,8 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   auto tmp = [&](size_t b) { return cx->cub_tmp.get(b); };
   size_t tbb = 0;
   ix->part_start.assign((size_t)R + 1, 0);
-  ix->h_parts.assign((size_t)R, {});
+  ix->h_parts.clear();
+  ix->h_parts.resize((size_t)R);
   ix->h_parts_ready.assign((size_t)R, 0);
   ix->ser_ready = true;
   if (V == 0) {

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -40,6 +41,13 @@ struct sme_ctx {
   int64_t opt_agg_two_pass = 0;   // "agg_two_pass": 1 = count + emit aggregation passes
   int64_t opt_tok_grid = 4096;    // "tok_grid": tokenizer workgroups (>= 1)
   int64_t opt_raw_load_pct = 40;  // "raw_load_pct": raw-vocabulary table load of the next build (10..90)
+  // pinned host staging of device -> host record copies into pageable caller
+  // memory (sme_index_copy_records): two buffers, DMA into one while the host
+  // copies out of the other
+  void *h_stage[2] = {nullptr, nullptr};
+  size_t h_stage_cap = 0;
+  // device copy of a host corpus (sme_build_index), kept across builds
+  sme::DevBuf h_corpus_dev;
   // indexes borrow the context (its pool, workspace, stream): sme_destroy defers
   // the delete until the last index is freed, whatever order a host frees them in
   int live_indexes = 0;
@@ -75,7 +83,9 @@ struct sme_index {
   sme::DevBuf d_ser;
   std::vector<int64_t> part_start;  // R+1
   bool ser_ready = false;
-  std::vector<std::vector<uint8_t>> h_parts;
+  float ser_ms = 0.0f;  // device time of the k_ser_* pass (serialize_index)
+  // host copies of the partitions (sme_index_partition_records), not zero-filled
+  std::vector<std::unique_ptr<uint8_t[]>> h_parts;
   std::vector<char> h_parts_ready;
   // host copies (lazily)
   std::vector<int64_t> h_off;
@@ -159,7 +169,7 @@ void serialize_index(sme_index *ix, hipStream_t st);
 void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t st);
 void prepare_queries(sme_index *ix, hipStream_t st);
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k,
-                int32_t *d_out_docno, double *d_out_score, hipStream_t st);
+                int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie, hipStream_t st);
 void tokenize_string(sme_ctx *cx, const uint8_t *h_utf8, size_t n, std::vector<std::vector<uint16_t>> &out,
                      hipStream_t st);
 void term_fingerprints(sme_index *ix, uint64_t *d_out, hipStream_t st);

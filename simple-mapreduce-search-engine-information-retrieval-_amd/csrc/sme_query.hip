@@ -35,14 +35,30 @@ constexpr int kQPer = 4;  // postings per lane per step
 constexpr int kMaxQTerms = 128;
 constexpr int kLutLds = 256;  // 1 + ln(tf) for tf < 256 from LDS, the rare rest from HBM
 
-__device__ __forceinline__ bool better(double as, int32_t ad, double bs, int32_t bd) {
-  return as > bs || (as == bs && ad < bd);
+// Result order: score desc, then a 64-bit key asc.  key = tie << 32 | (docno
+// with its sign bit flipped, so docnos compare as signed ints); tie = 0 for the
+// north-star order (docno asc) and ref_tie() for the reference's (SME_TIE_REFERENCE):
+// rank() appends candidates to `scores` in first-encounter order -- query token
+// order, each term's postings in reduce order (tf desc, docno asc) -- and
+// Collections.sort is stable and only ever asks compareTo <= 0 / > 0, i.e.
+// b.score <= a.score / b.score > a.score, so equal scores keep that order
+// (IntDocVectorsForwardIndex.java:195-215,363-365; tools/t5_divergence.py).
+__device__ __forceinline__ bool better(double as, uint64_t ak, double bs, uint64_t bk) {
+  return as > bs || (as == bs && ak < bk);
 }
+__device__ __forceinline__ uint64_t doc_key(uint32_t tie, int32_t d) {
+  return ((uint64_t)tie << 32) | ((uint32_t)d ^ 0x80000000u);
+}
+__device__ __forceinline__ int32_t key_doc(uint64_t k) { return (int32_t)((uint32_t)k ^ 0x80000000u); }
+// first-encounter rank of a document first met at query token j with tf f
+// (tf < 2^24: the host checks max_tf in this mode)
+__device__ __forceinline__ uint32_t ref_tie(int j, int f) { return ((uint32_t)j << 24) | (0xFFFFFFu - (uint32_t)f); }
+constexpr uint64_t kNoKey = ~0ull;
 
 // insert (s, d) into the descending register list ts/td (fully unrolled: no
 // dynamic register indexing)
 template <int K>
-__device__ __forceinline__ void topk_insert(double (&ts)[K], int32_t (&td)[K], double s, int32_t d) {
+__device__ __forceinline__ void topk_insert(double (&ts)[K], uint64_t (&td)[K], double s, uint64_t d) {
   if (!better(s, d, ts[K - 1], td[K - 1])) return;
   bool done = false;
 #pragma unroll
@@ -74,16 +90,18 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int l) {
 // merge the per-lane lists: k rounds of block arg-max over list heads; thread 0
 // writes query q's k results (docno -1 / score 0 padding)
 template <int KMAX>
-__device__ __forceinline__ void emit_topk(double (&ts)[KMAX], int32_t (&td)[KMAX], int k, int q, int32_t *out_d,
-                                          double *out_s, double *red_s, int32_t *red_d, int32_t *red_t) {
+__device__ __forceinline__ void emit_topk(double (&ts)[KMAX], uint64_t (&td)[KMAX], int k, int q, int32_t *out_d,
+                                          double *out_s, uint32_t *out_t, double *red_s, uint64_t *red_d,
+                                          int32_t *red_t) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   for (int r = 0; r < k; r++) {
     double bs = ts[0];
-    int32_t bd = td[0];
+    uint64_t bd = td[0];
     int32_t bt = tid;
     for (int o = 32; o > 0; o >>= 1) {
       double os = __shfl_xor(bs, o, 64);
-      int32_t od = __shfl_xor(bd, o, 64), ot = __shfl_xor(bt, o, 64);
+      uint64_t od = __shfl_xor(bd, o, 64);
+      int32_t ot = __shfl_xor(bt, o, 64);
       if (better(os, od, bs, bd)) {
         bs = os;
         bd = od;
@@ -112,12 +130,13 @@ __device__ __forceinline__ void emit_topk(double (&ts)[KMAX], int32_t (&td)[KMAX
         td[j] = td[j + 1];
       }
       ts[KMAX - 1] = -INFINITY;
-      td[KMAX - 1] = 0x7FFFFFFF;
+      td[KMAX - 1] = kNoKey;
     }
     if (tid == 0) {
       const bool valid = bs != -INFINITY;
-      out_d[(int64_t)q * k + r] = valid ? bd : -1;
+      out_d[(int64_t)q * k + r] = valid ? key_doc(bd) : -1;
       out_s[(int64_t)q * k + r] = valid ? bs : 0.0;
+      if (out_t) out_t[(int64_t)q * k + r] = valid ? (uint32_t)(bd >> 32) : 0xFFFFFFFFu;
     }
     __syncthreads();
   }
@@ -128,15 +147,18 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
                                                 const int32_t *__restrict__ tf, const double *__restrict__ lut,
                                                 int max_tf, const double *__restrict__ idf, int64_t V,
                                                 const int32_t *__restrict__ terms, const int64_t *__restrict__ qoff,
-                                                int nq, int k, int32_t *out_d, double *out_s, int *err) {
+                                                int nq, int k, int32_t *out_d, double *out_s, uint32_t *out_t,
+                                                int reftie, int *err) {
   __shared__ double acc[kTile];
+  __shared__ uint32_t first[kTile];  // SME_TIE_REFERENCE: ref_tie of the document's first token
   __shared__ double s_lut[kLutLds];
   __shared__ int64_t cur[kMaxQTerms], endp[kMaxQTerms];
   __shared__ double tidf[kMaxQTerms];
   __shared__ int32_t s_next;
   __shared__ unsigned long long s_stop;
   __shared__ double red_s[kQNT / 64];
-  __shared__ int32_t red_d[kQNT / 64], red_t[kQNT / 64];
+  __shared__ uint64_t red_d[kQNT / 64];
+  __shared__ int32_t red_t[kQNT / 64];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   for (int j = tid; j < kTile; j += kQNT) acc[j] = -1.0;  // untouched (weights are >= 0)
   for (int j = tid; j < kLutLds; j += kQNT) s_lut[j] = j <= max_tf ? lut[j] : 0.0;
@@ -159,11 +181,11 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
       if (b < e) atomicMin(&s_next, docno[b]);
     }
     double ts[KMAX];
-    int32_t td[KMAX];
+    uint64_t td[KMAX];
 #pragma unroll
     for (int j = 0; j < KMAX; j++) {
       ts[j] = -INFINITY;
-      td[j] = 0x7FFFFFFF;
+      td[j] = kNoKey;
     }
     __syncthreads();
     while (s_next != 0x7FFFFFFF) {  // uniform: read after a barrier
@@ -205,6 +227,7 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
             const double w = __dmul_rn(l, w_idf);
             const double v = acc[d];
             acc[d] = v < 0.0 ? w : __dadd_rn(v, w);
+            if (reftie && v < 0.0) first[d] = ref_tie(i, fv[u]);  // terms run in token order
           }
           if (stop) break;
           p += (int64_t)kQPer * kQNT;
@@ -231,11 +254,11 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
         const double sc = acc[j];
         if (sc < 0.0) continue;
         acc[j] = -1.0;
-        topk_insert<KMAX>(ts, td, sc, lo + j);
+        topk_insert<KMAX>(ts, td, sc, doc_key(reftie ? first[j] : 0u, lo + j));
       }
       __syncthreads();
     }
-    emit_topk<KMAX>(ts, td, k, q, out_d, out_s, red_s, red_d, red_t);
+    emit_topk<KMAX>(ts, td, k, q, out_d, out_s, out_t, red_s, red_d, red_t);
   }
 }
 
@@ -529,14 +552,14 @@ __global__ void k_query_keys(const int32_t *terms, const int64_t *qoff, int nq, 
 // Bitonic sort of n (power of two) entries of one wave's LDS buffer, best
 // first (score desc, docno asc).  The workgroup is one wave, so the barriers
 // only order the LDS traffic.
-__device__ __forceinline__ void wave_sort(double *s, int32_t *d, int n) {
+__device__ __forceinline__ void wave_sort(double *s, uint64_t *d, int n) {
   const int lane = threadIdx.x;
   for (int size = 2; size <= n; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int i = lane; i < (n >> 1); i += 64) {
         const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1)), hi = lo + stride;
         const double as = s[lo], bs = s[hi];
-        const int32_t ad = d[lo], bd = d[hi];
+        const uint64_t ad = d[lo], bd = d[hi];
         const bool sw = (lo & size) == 0 ? better(bs, bd, as, ad) : better(as, ad, bs, bd);
         if (sw) {
           s[lo] = bs;
@@ -569,8 +592,10 @@ struct QBmArgs {
   const int64_t *qoff;
   const int32_t *qorder;
   int nq, k, nseed;
+  int reftie;             // SME_TIE_REFERENCE order (ref_tie keys)
   int32_t *out_d;
   double *out_s;
+  uint32_t *out_t;        // optional: tie word of every result (multi-shard merges)
   const unsigned long long *wmax_bits;
   unsigned long long *stats;  // SME_EXPERIMENTS builds only (else nullptr)
 };
@@ -581,7 +606,7 @@ __global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
   __shared__ uint32_t lacc[kQT];             // sparse terms' impact sums of the tile's documents
   __shared__ uint8_t trow[kSRows * kQT];     // tf bytes of the tile for the first kSRows sparse terms
   __shared__ double bs[C];
-  __shared__ int32_t bd[C];
+  __shared__ uint64_t bd[C];  // doc_key of every buffered candidate
   __shared__ uint32_t s_big;  // sparse slots whose term has a tf > 255 in the tile
   const int lane = threadIdx.x;
   const double wmax = __longlong_as_double((long long)*a.wmax_bits);
@@ -638,7 +663,7 @@ __global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
     int cnt = 0;  // buffer fill (wave-uniform)
     bool th_ok = false;
     double th_s = 0.0;
-    int32_t th_d = 0;
+    uint64_t th_d = 0;
     uint32_t gate = 1;  // touched documents only until k of them are held
     uint32_t st_tiles = 0, st_blocks = 0, st_cand = 0, st_comp = 0;
     // sort the buffer, keep the best k, raise th and the gate
@@ -648,7 +673,7 @@ __global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
       while (n2 < cnt) n2 <<= 1;
       for (int i = cnt + lane; i < n2; i += 64) {
         bs[i] = -INFINITY;
-        bd[i] = 0x7FFFFFFF;
+        bd[i] = kNoKey;
       }
       __syncthreads();
       wave_sort(bs, bd, n2);
@@ -801,13 +826,14 @@ __global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
         const bool have = cm != 0;
         if (__ballot(have) == 0) break;  // wave-uniform
         double S = 0.0;
-        int32_t d = 0x7FFFFFFF;
+        uint64_t key = kNoKey;
         bool keep = false;
         if (have) {
           const int b = (int)__builtin_ctz(cm);
           cm &= cm - 1;
           const int r = kQBlk * lane + b;
-          d = (int32_t)(dbase + r);
+          const int32_t d = (int32_t)(dbase + r);
+          uint32_t tie = 0xFFFFFFFFu;  // first contributing token (reference order)
           // exact score: query-token order, fp64, as rank() accumulates it
           for (uint64_t m = amask; m; m &= m - 1) {
             const int j = (int)__builtin_ctzll(m);
@@ -831,15 +857,19 @@ __global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
                 if (lo < e && a.docno[lo] == d) f = a.tf[lo];
               }
             }
-            if (f != 0) S = __dadd_rn(S, __dmul_rn(a.lut[f], rld(midf, j)));
+            if (f != 0) {
+              S = __dadd_rn(S, __dmul_rn(a.lut[f], rld(midf, j)));
+              if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f);
+            }
           }
-          keep = !th_ok || better(S, d, th_s, th_d);
+          key = doc_key(a.reftie ? tie : 0u, d);
+          keep = !th_ok || better(S, key, th_s, th_d);
         }
         const uint64_t km = (uint64_t)__ballot(keep);
         if (keep) {
           const int p = cnt + (int)lane_prefix(km);
           bs[p] = S;
-          bd[p] = d;
+          bd[p] = key;
         }
         cnt += __popcll(km);
         if (cnt > C - 64) compact();
@@ -902,8 +932,9 @@ __global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
       }
     }
     for (int r = lane; r < a.k; r += 64) {
-      a.out_d[(int64_t)q * a.k + r] = r < cnt ? bd[r] : -1;
+      a.out_d[(int64_t)q * a.k + r] = r < cnt ? key_doc(bd[r]) : -1;
       a.out_s[(int64_t)q * a.k + r] = r < cnt ? bs[r] : 0.0;
+      if (a.out_t) a.out_t[(int64_t)q * a.k + r] = r < cnt ? (uint32_t)(bd[r] >> 32) : 0xFFFFFFFFu;
     }
     __syncthreads();
   }
@@ -981,11 +1012,14 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
 }
 
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k, int32_t *d_out_docno,
-                double *d_out_score, hipStream_t st) {
+                double *d_out_score, uint32_t *d_out_tie, hipStream_t st) {
   if (k < 1) throw Error(SME_EINVAL, "k must be >= 1");
   if (k > 448) throw Error(SME_ELIMIT, "top-k with k > 448");
   if (nq <= 0) return;
   sme_ctx *cx = ix->ctx;
+  const int reftie = cx->cfg.tiebreak == SME_TIE_REFERENCE ? 1 : 0;
+  if (reftie && ix->max_tf > 0xFFFFFF)
+    throw Error(SME_ELIMIT, "reference tie order with a term frequency >= 2^24");
   auto &W = cx->ws;
   int *err = W[63].as<int>(4);
   unsigned long long *wmax = reinterpret_cast<unsigned long long *>(err + 2);
@@ -1111,8 +1145,10 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     qa.nq = nq;
     qa.k = k;
     qa.nseed = (int)std::max<int64_t>(0, std::min<int64_t>(cx->opt_seed_tiles, kMaxSeed));
+    qa.reftie = reftie;
     qa.out_d = d_out_docno;
     qa.out_s = d_out_score;
+    qa.out_t = d_out_tie;
     qa.wmax_bits = (const unsigned long long *)wmax;
     qa.stats = qstats;
     const unsigned wgrid = (unsigned)std::min<int64_t>(8 * (((int64_t)nq + 7) / 8), 1 << 30);
@@ -1125,11 +1161,11 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   } else if (k <= 16) {
     const unsigned grid = (unsigned)std::min(nq, 1 << 20);
     hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
-                       d_qoff, nq, k, d_out_docno, d_out_score, err);
+                       d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
   } else {
     const unsigned grid = (unsigned)std::min(nq, 1 << 20);
     hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
-                       d_qoff, nq, k, d_out_docno, d_out_score, err);
+                       d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
   }
   SME_CHECK_LAUNCH();
   SME_HIP(hipEventRecord(e1, st));

@@ -170,6 +170,11 @@ void serialize_index(sme_index *ix, hipStream_t st) {
   uint32_t *part2 = W[51].as<uint32_t>(V + 1), *idx2 = W[52].as<uint32_t>(V + 1);
   int64_t *grp_bytes = W[53].as<int64_t>(V + 1), *scan = W[54].as<int64_t>(V + 1);
   unsigned long long *psum = W[55].as<unsigned long long>(R + 1);
+  // device time of the pass (sizes + partition sort + writes; the host reads the
+  // partition sizes in between, so the two legs are timed separately)
+  hipEvent_t ev[4];
+  for (auto &e : ev) SME_HIP(hipEventCreate(&e));
+  SME_HIP(hipEventRecord(ev[0], st));
   SME_HIP(hipMemsetAsync(psum, 0, (R + 1) * sizeof(unsigned long long), st));
   const int G = (int)std::min<int64_t>(std::max<int64_t>((V + 255) / 256, 1), 8192);
   if (V > 0)
@@ -177,6 +182,7 @@ void serialize_index(sme_index *ix, hipStream_t st) {
                        (const uint16_t *)ix->d_term_chars.p, gram, ix->K, (const int64_t *)ix->d_off.p, V, R, rec_bytes,
                        part, idx, psum);
   SME_CHECK_LAUNCH();
+  SME_HIP(hipEventRecord(ev[1], st));
   std::vector<unsigned long long> hps(R + 1);
   SME_HIP(hipMemcpyAsync(hps.data(), psum, (R + 1) * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   SME_HIP(hipStreamSynchronize(st));
@@ -188,6 +194,7 @@ void serialize_index(sme_index *ix, hipStream_t st) {
   }
   const int64_t total = ix->part_start[R];
   uint8_t *out = ix->d_ser.as<uint8_t>(total + 16);
+  SME_HIP(hipEventRecord(ev[2], st));
   if (V > 0) {
     int bits = 1;
     while ((1 << bits) < R) bits++;
@@ -211,9 +218,16 @@ void serialize_index(sme_index *ix, hipStream_t st) {
                        (const int32_t *)ix->d_rec_docno.p, N, out + ix->part_start[part_sp]);
     SME_CHECK_LAUNCH();
   }
+  SME_HIP(hipEventRecord(ev[3], st));
   SME_HIP(hipStreamSynchronize(st));
+  float m0 = 0, m1 = 0;
+  SME_HIP(hipEventElapsedTime(&m0, ev[0], ev[1]));
+  SME_HIP(hipEventElapsedTime(&m1, ev[2], ev[3]));
+  for (auto &e : ev) (void)hipEventDestroy(e);
+  ix->ser_ms = m0 + m1;
   ix->ser_ready = true;
-  ix->h_parts.assign(R, {});
+  ix->h_parts.clear();
+  ix->h_parts.resize((size_t)R);
   ix->h_parts_ready.assign(R, 0);
 }
 

@@ -164,3 +164,65 @@ extern "C" int sme_synth_corpus(int device, const uint8_t *vocab, const int64_t 
 extern "C" void sme_synth_free(void *d) {
   if (d) (void)hipFree(d);
 }
+
+// ---- calibration: achievable HBM bandwidth on this device -------------------
+// A streaming copy (16-byte nontemporal loads and stores, grid-stride, 8 x 256
+// workgroups per CU), the measured ceiling beside the 8 TB/s spec that bench.py
+// reports its roofline fractions against.
+namespace sme {
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_hbm_copy(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst, int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; u++) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+}  // namespace sme
+
+/* HBM copy calibration (bench.py): copies `bytes` (rounded down to 16) between
+ * two device buffers `reps` times after one warm-up; *gbps = 2 x bytes / mean
+ * kernel time (read + write). */
+extern "C" int sme_hbm_copy_bench(int device, size_t bytes, int reps, double *gbps) {
+  try {
+    if (!gbps || reps < 1 || bytes < 16) return SME_EINVAL;
+    SME_HIP(hipSetDevice(device));
+    const int64_t n16 = (int64_t)(bytes / 16);
+    void *a = nullptr, *b = nullptr;
+    SME_HIP(hipMalloc(&a, n16 * 16));
+    SME_HIP(hipMalloc(&b, n16 * 16));
+    hipStream_t st;
+    SME_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    SME_HIP(hipMemsetAsync(a, 1, n16 * 16, st));
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    const dim3 grid((unsigned)(8 * cus));
+    hipEvent_t e0, e1;
+    SME_HIP(hipEventCreate(&e0));
+    SME_HIP(hipEventCreate(&e1));
+    hipLaunchKernelGGL(sme::k_hbm_copy, grid, dim3(256), 0, st, (const sme::u32x4 *)a, (sme::u32x4 *)b, n16);
+    SME_HIP(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; r++)
+      hipLaunchKernelGGL(sme::k_hbm_copy, grid, dim3(256), 0, st, (const sme::u32x4 *)(r & 1 ? b : a),
+                         (sme::u32x4 *)(r & 1 ? a : b), n16);
+    SME_HIP(hipGetLastError());
+    SME_HIP(hipEventRecord(e1, st));
+    SME_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    SME_HIP(hipEventElapsedTime(&ms, e0, e1));
+    *gbps = 2.0 * (double)(n16 * 16) * reps / (ms * 1e-3) / 1e9;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipStreamDestroy(st);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    return SME_OK;
+  } catch (const sme::Error &e) {
+    return e.code;
+  }
+}

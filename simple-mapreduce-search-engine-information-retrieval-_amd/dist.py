@@ -209,24 +209,36 @@ def owner_bounds(nq, world):
     return [nq * r // world for r in range(world + 1)]
 
 
-def _merge_rows(s, d, k):
-    """rows of candidate (score, docno) lists -> the best k per row, (score desc,
-    docno asc); docno -1 pads."""
+def _merge_rows(s, d, k, t=None):
+    """rows of candidate (score, docno[, tie]) lists -> the best k per row, (score
+    desc, tie asc, docno asc); docno -1 pads.  The tie word (sme_query_topk_tie)
+    is 0 under SME_TIE_DOCNO and the first-encounter rank under SME_TIE_REFERENCE,
+    a property of the document and the query alone, so shards merge into the
+    single index's order."""
     d = d.to(torch.int64)
-    valid = d >= 0
+    # docno -1 is padding; other negative docnos are real results (docids missing
+    # from the mapping: binarySearch's -(insertion point) - 1 <= -2, T14)
+    valid = d != -1
     s = torch.where(valid, s, torch.full_like(s, -float("inf")))
-    d = torch.where(valid, d, torch.full_like(d, 1 << 40))
-    # stable sort by docno, then stable sort by -score
-    i1 = torch.argsort(d, dim=1, stable=True)
-    s1, d1 = torch.gather(s, 1, i1), torch.gather(d, 1, i1)
+    # one int64 key: tie (32 bits) above the docno (+2^31, 32 bits); pads last
+    key = d + (1 << 31)
+    if t is not None:
+        key = key + (t.to(torch.int64) & 0xFFFFFFFF) * (1 << 32)
+    key = torch.where(valid, key, torch.full_like(key, (1 << 63) - 1))
+    # stable sort by key, then stable sort by -score
+    i1 = torch.argsort(key, dim=1, stable=True)
+    s1, k1 = torch.gather(s, 1, i1), torch.gather(key, 1, i1)
     i2 = torch.argsort(-s1, dim=1, stable=True)[:, :k]
-    out_d, out_s = torch.gather(d1, 1, i2), torch.gather(s1, 1, i2)
-    pad = out_d >= (1 << 40)
+    out_k, out_s = torch.gather(k1, 1, i2), torch.gather(s1, 1, i2)
+    pad = out_k == (1 << 63) - 1
+    out_d = (out_k & 0xFFFFFFFF) - (1 << 31)
+    out_t = (out_k >> 32) & 0xFFFFFFFF
     return (torch.where(pad, torch.full_like(out_d, -1), out_d).to(torch.int32),
-            torch.where(pad, torch.zeros_like(out_s), out_s))
+            torch.where(pad, torch.zeros_like(out_s), out_s),
+            torch.where(pad, torch.full_like(out_t, 0xFFFFFFFF), out_t))
 
 
-def merge_topk_owner(docno, score, k, group=None):
+def merge_topk_owner(docno, score, k, group=None, tie=None):
     """Query-owner merge: docno int32 [Q, k] (-1 pads), score float64
     [Q, k] of this shard -> (q0, q1, docno [q1-q0, k], score [q1-q0, k]), the global
     top-k of the queries this rank owns.  One all_to_all moves every shard's lists
@@ -243,16 +255,21 @@ def merge_topk_owner(docno, score, k, group=None):
     dist.all_to_all_single(rd, docno.contiguous().reshape(-1), [my * k] * world, ins, group=group)
     s = rs.reshape(world, my, k).permute(1, 0, 2).reshape(my, world * k)
     d = rd.reshape(world, my, k).permute(1, 0, 2).reshape(my, world * k)
-    md, ms = _merge_rows(s, d, k)
+    t = None
+    if tie is not None:  # uint32 words travel as int64 (collectives have no uint32)
+        rt = torch.empty(world * my * k, dtype=torch.int64, device=docno.device)
+        dist.all_to_all_single(rt, tie.to(torch.int64).contiguous().reshape(-1), [my * k] * world, ins, group=group)
+        t = rt.reshape(world, my, k).permute(1, 0, 2).reshape(my, world * k)
+    md, ms, _ = _merge_rows(s, d, k, t)
     return b[r], b[r + 1], md, ms
 
 
-def merge_topk(docno, score, k, group=None):
+def merge_topk(docno, score, k, group=None, tie=None):
     """Global (docno, score) [Q, k] on every rank: the query-owner merge, then an
     all_gather of the merged slices (Q x k x 12 B, not W x Q x k)."""
     world = dist.get_world_size(group)
     nq = docno.shape[0]
-    q0, q1, md, ms = merge_topk_owner(docno, score, k, group)
+    q0, q1, md, ms = merge_topk_owner(docno, score, k, group, tie)
     b = owner_bounds(nq, world)
     m = max(b[i + 1] - b[i] for i in range(world))
     pd = torch.full((m, k), -1, dtype=md.dtype, device=md.device)

@@ -1,7 +1,8 @@
 """One rank of the world-2 libsme shard test (tests/test_dist_gpu.py): a fresh
 process that touches the GPU only after it starts.  Builds its shard with libsme,
 all-reduces N and df (gloo) into sme_index_reweight, scores its shard, merges the
-per-shard top-k lists and checks them against the single-index oracle.
+per-shard top-k lists and checks them against the single-index oracle, in both
+tie orders (north star; the reference's Collections.sort order via tie words).
 usage: dist_gpu_worker.py RANK WORLD PORT IDF_MODE OUT_DIR"""
 import importlib
 import os
@@ -31,36 +32,42 @@ def main():
         n = 700
         corpus = synth.gen_corpus(n, V=900, seed=31, len_lo=10, len_hi=80)
         mapping = synth.mapping_bytes(n)
-        ctx = sme.Context(1, 1, idf_mode)
-        cuts = D.split_points(corpus, world, ctx)
-        ctx.load_docno_mapping(mapping)
-        ix = ctx.build(corpus[cuts[rank]:cuts[rank + 1]])
-        N = D.global_count(ix.N)
-        assert N == n
-        gdf = D.global_df_index(ix)
-        ix.reweight(N, gdf.data_ptr())
         full = O.OracleIndex(corpus, mapping, 1, 1)
         fterms = sorted({t[0][0] for t in full.terms() if t[0] != (" ",)})
         fdf = {t[0][0]: len(t[3]) for t in full.terms() if t[0] != (" ",)}
-        names = [ix.term(t) for t in range(ix.V)]
-        g = gdf.cpu().numpy()
-        assert all(int(g[t]) == fdf[names[t]] for t in range(ix.V))  # df all-reduce through fingerprints
         rng = np.random.default_rng(11)
         queries = [[fterms[i] for i in rng.integers(0, len(fterms), rng.integers(1, 7))] for _ in range(60)]
         flat = [t for q in queries for t in q]
-        ids = ix.lookup(flat).astype(np.int32)  # -1: not in this shard, skipped like an unknown term
         qoff = np.zeros(len(queries) + 1, np.int64)
         qoff[1:] = np.cumsum([len(q) for q in queries])
-        for k in (10, 100):
-            dn, sc = ix.query_topk(ids, qoff, k)
-            md, ms = D.merge_topk(torch.from_numpy(dn), torch.from_numpy(sc), k)
-            q0, q1, od, osc = D.merge_topk_owner(torch.from_numpy(dn), torch.from_numpy(sc), k)
-            assert torch.equal(od, md[q0:q1]) and torch.equal(osc, ms[q0:q1])
-            for q, tl in enumerate(queries):
-                rd, rs = full.query(tl, k, idf_mode, 0)
-                assert md[q, :len(rd)].tolist() == rd, (k, q, tl)
-                assert ms[q, :len(rs)].numpy().tolist() == rs, (k, q)  # fp64 bit-exact
-                assert (md[q, len(rd):] == -1).all()
+        # tiebreak 0: north-star order; 1: the reference's printed order (oracle
+        # order 1 = Java 6 Collections.sort), merged through the tie words
+        for tiebreak in (0, 1):
+            ctx = sme.Context(1, 1, idf_mode, tiebreak=tiebreak)
+            cuts = D.split_points(corpus, world, ctx)
+            ctx.load_docno_mapping(mapping)
+            ix = ctx.build(corpus[cuts[rank]:cuts[rank + 1]])
+            N = D.global_count(ix.N)
+            assert N == n
+            gdf = D.global_df_index(ix)
+            ix.reweight(N, gdf.data_ptr())
+            names = [ix.term(t) for t in range(ix.V)]
+            g = gdf.cpu().numpy()
+            assert all(int(g[t]) == fdf[names[t]] for t in range(ix.V))  # df all-reduce through fingerprints
+            ids = ix.lookup(flat).astype(np.int32)  # -1: not in this shard, skipped like an unknown term
+            for k in (10, 100):
+                dn, sc, tie = ix.query_topk(ids, qoff, k, with_tie=True)
+                tt = torch.from_numpy(tie.astype(np.int64))
+                md, ms = D.merge_topk(torch.from_numpy(dn), torch.from_numpy(sc), k, tie=tt)
+                q0, q1, od, osc = D.merge_topk_owner(torch.from_numpy(dn), torch.from_numpy(sc), k, tie=tt)
+                assert torch.equal(od, md[q0:q1]) and torch.equal(osc, ms[q0:q1])
+                for q, tl in enumerate(queries):
+                    rd, rs = full.query(tl, k, idf_mode, 1 if tiebreak else 0)
+                    assert md[q, :len(rd)].tolist() == rd, (tiebreak, k, q, tl)
+                    assert ms[q, :len(rs)].numpy().tolist() == rs, (tiebreak, k, q)  # fp64 bit-exact
+                    assert (md[q, len(rd):] == -1).all()
+            ix.close()
+            ctx.close()
         open(os.path.join(out_dir, "ok%d" % rank), "w").write("ok")
     finally:
         dist.destroy_process_group()

@@ -245,6 +245,21 @@ class CpuOptIndex:
         self.N, self.V, self.P, self.build_s = n.value, v.value, p.value, s.value
         self.threads = threads
 
+    @classmethod
+    def from_csr(cls, N, off, docno, tf):
+        """Wrap CSR arrays (reduce order) of an index built elsewhere; no term strings."""
+        import numpy as np
+        L = lib()
+        L.or_cpuopt_from_csr.restype = C.c_void_p
+        L.or_cpuopt_from_csr.argtypes = [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+        self = cls.__new__(cls)
+        off = np.ascontiguousarray(off, np.int64)
+        docno = np.ascontiguousarray(docno, np.int32)
+        tf = np.ascontiguousarray(tf, np.int32)
+        self._h = L.or_cpuopt_from_csr(N, len(off) - 1, off.ctypes.data, docno.ctypes.data, tf.ctypes.data)
+        self.N, self.V, self.P, self.build_s, self.threads = N, len(off) - 1, int(off[-1]), 0.0, 0
+        return self
+
     def csr(self):
         """(offsets, docno, tf) in reduce order and the term strings (TermDF order)."""
         import numpy as np

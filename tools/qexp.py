@@ -1,0 +1,93 @@
+"""Query-path experiments on the GPU (timing only; parity is the tests' job).
+
+Builds the c2 index once on the device, draws the c3 batch, then runs the batch
+under several sme_set_option settings and prints per setting the scoring kernel
+ms, per-batch prep ms and QPS, checking every setting's results against the
+first one's (docnos + score bits).  With an experiment build
+(SME_LIB_PATH=.../libsme_exp.so, compiled with -DSME_EXPERIMENTS) SME_QSTATS=1
+makes the kernel print its visit counters.
+    python tools/qexp.py [--docs N] [--queries Q] [--k K] [--config c2|c5] \
+        [--opts "heavy_div=32,seed_tiles=4;heavy_div=0"]
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "simple-mapreduce-search-engine-information-retrieval-_amd"
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--docs", type=int, default=1_000_000)
+    p.add_argument("--queries", type=int, default=100_000)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--config", default="c2")
+    p.add_argument("--opts", default="")
+    p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--tiebreak", type=int, default=0)
+    a = p.parse_args()
+    import torch
+    sme = importlib.import_module(PKG)
+    synth = importlib.import_module(PKG + ".synth")
+    cfg = dict(c2=dict(V=1 << 20, seed=42, lo=400, hi=600, qseed=7),
+               c5=dict(V=30000, seed=9, lo=40, hi=72, qseed=9))[a.config]
+    dc = sme.DeviceCorpus(a.docs, V=cfg["V"], seed=cfg["seed"], len_lo=cfg["lo"], len_hi=cfg["hi"])
+    ctx = sme.Context(k=1, num_partitions=1, device=0, tiebreak=a.tiebreak)
+    ctx.load_docno_mapping(synth.mapping_bytes(a.docs))
+    st = torch.cuda.current_stream().cuda_stream
+    ix = ctx.build_device(dc.ptr, dc.nbytes, st)
+    torch.cuda.synchronize()
+    print("index N=%d V=%d P=%d" % (ix.N, ix.V, ix.P), flush=True)
+    _, _, _, df = ix.csr()
+    terms, qoff = synth.queries_by_df(df, a.queries, seed=cfg["qseed"])
+    d_terms = torch.from_numpy(terms).cuda()
+    d_qoff = torch.from_numpy(qoff).cuda()
+    k = a.k
+    base = None
+    settings = [""] + [s for s in a.opts.split(";") if s.strip()]
+    for s in settings:
+        opts = dict(kv.split("=") for kv in s.split(",") if kv.strip())
+        for n, v in opts.items():
+            ctx.set_option(n.strip(), int(v))
+        out_d = torch.empty((a.queries, k), dtype=torch.int32, device="cuda")
+        out_s = torch.empty((a.queries, k), dtype=torch.float64, device="cuda")
+        t_idx = ix.prepare_queries(st)
+        kms, pms, walls = [], [], []
+        for r in range(a.reps + 1):
+            t0 = time.perf_counter()
+            ix.query_topk_device(d_terms.data_ptr(), d_qoff.data_ptr(), a.queries, k, out_d.data_ptr(),
+                                 out_s.data_ptr(), st)
+            torch.cuda.synchronize()
+            walls.append((time.perf_counter() - t0) * 1e3)
+            prof = ctx.last_build_profile()
+            kms.append(prof.get("query_kernel"))
+            pms.append(prof.get("query_prep"))
+        res = (out_d.cpu().numpy(), out_s.cpu().numpy())
+        same = None
+        if base is None:
+            base = res
+        else:
+            same = bool(np.array_equal(base[0], res[0]) and np.array_equal(base[1].view(np.int64),
+                                                                            res[1].view(np.int64)))
+        print(json.dumps({"opts": s or "default", "kernel_ms": round(float(np.median(kms[1:])), 3),
+                          "prep_ms": round(float(np.median(pms[1:])), 3),
+                          "wall_ms": round(float(np.median(walls[1:])), 3),
+                          "qps": round(a.queries / (np.median(walls[1:]) / 1e3), 1),
+                          "index_prep_ms": round(t_idx, 3), "same_as_default": same,
+                          "name": prof.get("query_kernel_name")}), flush=True)
+        for n in opts:  # restore defaults
+            ctx.set_option(n.strip(), {"heavy_div": 32, "seed_tiles": 4, "query_order": 1,
+                                       "query_kernel": 0}.get(n.strip(), 0))
+    ix.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
