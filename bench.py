@@ -324,6 +324,7 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     kms.append(qp.get("query_kernel"))
     pms.append(qp.get("query_prep"))
     kname = qp.get("query_kernel_name", kname)
+    qextra = {key: qp[key] for key in ("query_seed", "query_final", "query_total", "query_overflow") if key in qp}
     kms = [x for x in kms if x is not None]
     qk_ms = sum(kms) / len(kms) if kms else None
     pms = [x for x in pms if x is not None]
@@ -356,6 +357,9 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
                          "traffic_fetch_raw": qtr[1], "traffic_write": qtr[2],
                          "what": "A_q = 8*sum(df of distinct batch terms) + 4*sum|q| + 12*k*Q per launch / "
                                  "mean launch time (HIP events)"},
+            "kernel_split_ms": qextra,
+            "kernel_split_what": "k_query_win path: seed (k_query_seed), final selection + overflow re-runs "
+                                 "(k_query_final, k_query_bm), their total; query_overflow = queries re-run",
             "postings_touched_GBps": round(touched / t_k / 1e9, 2),
             "postings_touched_what": "8 B x postings of every query term (re-reads across queries included)"}
 
@@ -394,7 +398,7 @@ def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank):
         base = (out_d[:nq].cpu().numpy(), out_s[:nq].cpu().numpy()) if hasattr(out_d, "cpu") else None
         d1, s1 = ix.query_topk(t_s, q_s, k)
         ok = base is None or (np.array_equal(base[0], d1) and np.array_equal(base[1], s1))
-        for opts in ({"heavy_div": 0}, {"query_kernel": 1}):
+        for opts in ({"heavy_div": 0}, {"query_kernel": 2}, {"query_kernel": 1}):
             if "query_kernel" in opts and k > 32:
                 continue
             try:
@@ -479,10 +483,7 @@ def end_to_end_stage(sme, ctx, d_corpus, nbytes, torch, reps=2):
 
 
 def _hip_copy(dst, src, n, kind):
-    h = C.CDLL("libamdhip64.so")
-    h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    rc = h.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), n, kind)
-    assert rc == 0, rc
+    importlib.import_module(PKG).memcpy(dst, src, n)
 
 
 def pmc_traffic(kernel, a, detail=False):

@@ -72,6 +72,15 @@ typedef struct {
 const char *sme_last_error(void);
 const char *sme_version(void);
 
+/* Device-memory plumbing for hosts without a HIP binding of their own (a JNI /
+ * ctypes host passing d_df_global to sme_index_reweight, or reading a device
+ * corpus back): allocation on `device`, and a copy in any direction
+ * (hipMemcpyDefault; stream NULL = synchronous).  They run on the library's own
+ * HIP runtime, so pointers from it and to it always agree. */
+int sme_device_alloc(int device, size_t n, void **d);
+void sme_device_free(void *d);
+int sme_memcpy(void *dst, const void *src, size_t n, void *stream);
+
 int sme_create(const sme_config *cfg, sme_ctx **out);
 void sme_destroy(sme_ctx *ctx);
 

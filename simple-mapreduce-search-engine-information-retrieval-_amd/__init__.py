@@ -41,7 +41,7 @@ class _Config(C.Structure):
 _lib = None
 
 EXPORTS = [
-    "sme_last_error", "sme_version", "sme_create", "sme_destroy", "sme_load_docno_mapping", "sme_build_index",
+    "sme_last_error", "sme_version", "sme_device_alloc", "sme_device_free", "sme_memcpy", "sme_create", "sme_destroy", "sme_load_docno_mapping", "sme_build_index",
     "sme_build_index_device", "sme_index_free", "sme_index_stats", "sme_index_partition_records", "sme_index_serialize",
     "sme_index_copy_records", "sme_index_csr",
     "sme_index_device_arrays", "sme_index_term", "sme_tokenize", "sme_lookup_terms", "sme_query_topk",
@@ -62,6 +62,10 @@ def lib():
     L = C.CDLL(LIB_PATH)
     vp, sz, i64p, i32p = C.c_void_p, C.c_size_t, C.POINTER(C.c_int64), C.POINTER(C.c_int32)
     L.sme_last_error.restype = C.c_char_p
+    L.sme_device_alloc.argtypes = [C.c_int, sz, C.POINTER(vp)]
+    L.sme_device_free.argtypes = [vp]
+    L.sme_device_free.restype = None
+    L.sme_memcpy.argtypes = [vp, vp, sz, vp]
     L.sme_version.restype = C.c_char_p
     L.sme_create.argtypes = [C.POINTER(_Config), C.POINTER(vp)]
     L.sme_destroy.argtypes = [vp]
@@ -111,17 +115,16 @@ def _check(rc):
         raise SmeError(rc, lib().sme_last_error().decode("utf-8", "replace"))
 
 
-def _hip():
-    h = C.CDLL("libamdhip64.so")
-    h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    return h
+def memcpy(dst, src, nbytes, stream=None):
+    """Copy between host and device memory through libsme's HIP runtime
+    (sme_memcpy; stream None = synchronous).  Python never loads a HIP runtime
+    of its own: torch's bundled one and the library's could disagree."""
+    _check(lib().sme_memcpy(C.c_void_p(dst), C.c_void_p(src), nbytes, C.c_void_p(stream or 0)))
 
 
 def _d2h(arr, dptr, nbytes):
-    """hipMemcpy device -> host into a numpy array."""
-    rc = _hip().hipMemcpy(arr.ctypes.data, C.c_void_p(dptr), nbytes, 2)
-    if rc != 0:
-        raise SmeError(-2, "hipMemcpy failed: %d" % rc)
+    """device -> host into a numpy array."""
+    memcpy(arr.ctypes.data, dptr, nbytes)
 
 
 def _host_bytes(p, n):

@@ -193,6 +193,30 @@ void copy_d2h(sme_ctx *cx, void *dst, const void *d, size_t n, hipStream_t st) {
 extern "C" {
 
 const char *sme_last_error(void) { return g_err.c_str(); }
+
+int sme_device_alloc(int device, size_t n, void **d) {
+  return guard([&] {
+    if (!d) throw sme::Error(SME_EINVAL, "null argument");
+    SME_HIP(hipSetDevice(device));
+    *d = nullptr;
+    SME_HIP(hipMalloc(d, n ? n : 16));
+  });
+}
+
+void sme_device_free(void *d) {
+  if (d) (void)hipFree(d);
+}
+
+int sme_memcpy(void *dst, const void *src, size_t n, void *stream) {
+  return guard([&] {
+    if (n == 0) return;
+    if (!dst || !src) throw sme::Error(SME_EINVAL, "null argument");
+    if (stream)
+      SME_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDefault, (hipStream_t)stream));
+    else
+      SME_HIP(hipMemcpy(dst, src, n, hipMemcpyDefault));
+  });
+}
 const char *sme_version(void) { return "sme 0.1 (gfx950)"; }
 
 int sme_create(const sme_config *cfg, sme_ctx **out) {
@@ -229,7 +253,7 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
       if (v < lo || v > hi) throw sme::Error(SME_EINVAL, "option " + n + " out of range");
     };
     if (n == "query_kernel") {
-      range(0, 1);
+      range(0, 2);
       cx->opt_query_kernel = v;
     } else if (n == "heavy_div") {
       range(0, int64_t(1) << 40);
@@ -246,6 +270,12 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
     } else if (n == "tok_grid") {
       range(1, int64_t(1) << 30);
       cx->opt_tok_grid = v;
+    } else if (n == "cand_cap") {
+      range(1, 2048);
+      cx->opt_cand_cap = v;
+    } else if (n == "seed_m") {
+      range(0, 4096);
+      cx->opt_seed_m = v;
     } else if (n == "raw_load_pct") {
       range(10, 90);
       cx->opt_raw_load_pct = v;
@@ -660,7 +690,10 @@ int sme_last_build_profile(const sme_ctx *cx, const char **json) {
     if (cx->last_query_ms >= 0) os << (cx->last_profile.empty() ? "" : ",") << "\"query_kernel\":" << cx->last_query_ms;
     if (cx->last_query_ms >= 0) os << ",\"query_prep\":" << cx->last_query_prep_ms;
     if (cx->last_query_ms >= 0) os << ",\"query_index\":" << cx->last_query_index_ms;
-    if (cx->last_query_ms >= 0) os << ",\"query_kernel_name\":\"" << (cx->last_query_tiled ? "k_query_bm" : "k_query") << "\"";
+    if (cx->last_query_ms >= 0) os << ",\"query_kernel_name\":\"" << cx->last_query_name << "\"";
+    if (cx->last_query_ms >= 0 && cx->last_query_name == std::string("k_query_win"))
+      os << ",\"query_seed\":" << cx->last_query_seed_ms << ",\"query_final\":" << cx->last_query_final_ms
+         << ",\"query_overflow\":" << cx->last_query_overflow << ",\"query_total\":" << cx->last_query_total_ms;
     os << "}";
     const_cast<sme_ctx *>(cx)->profile_json = os.str();
     *json = cx->profile_json.c_str();

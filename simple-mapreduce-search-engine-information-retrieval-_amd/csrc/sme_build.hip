@@ -3532,6 +3532,7 @@ void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t 
                        idf_ref, d_gdf, Nn, d_tab, sdf, d_tab + by_df.size(), ix->idf_mode, (double *)ix->d_w.p);
   SME_CHECK_LAUNCH();
   SME_HIP(hipStreamSynchronize(st));
+  ix->q_ready = false;  // impact rows and alpha depend on idf (prepare_queries rebuilds them)
 }
 
 }  // namespace sme

@@ -940,8 +940,463 @@ __global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
   }
 }
 
-// Index-resident heavy rows (see k_query_bm): built once per index and heavy
-// threshold; tf-based, so TF-IDF reweighting keeps them.
+__device__ __forceinline__ uint32_t qhash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ void qwave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ---------------------------------------------------------------------------
+// Window-major scoring (default path): k_query_seed -> k_query_win -> k_query_final.
+//
+// 1. Seed (one wave per query): a lower bound th0 of the query's k-th best
+//    score.  Every term's first M postings in REDUCE order (its highest tf, the
+//    documents most likely to rank) are scored over a SUBSET of the query's
+//    terms -- the heavy terms (tf from the index-resident tf rows) and the term
+//    itself -- in query-token order.  fp64 addition is monotone and every weight
+//    is >= 0, so this partial sum S'(d) <= S(d) bit for bit, and the k-th best
+//    S' over distinct documents is <= the k-th best S.  Fewer than k distinct
+//    seeds (every term's df < k): th0 = -1, every touched document qualifies.
+// 2. Windows (one wave per (query, 4096-document window)): workgroup b takes
+//    window x and a slice of the query batch, with the 8 XCDs on 8 different
+//    windows and every slice of a window on one XCD, so each window's heavy
+//    rows are fetched into that XCD's L2 once and read there by every query of
+//    the batch.  A(d) = sum of the term impacts q_j(tf) (index-resident impact
+//    rows for heavy terms: four bytes per dword split into packed u16 pairs by
+//    two v_perm; sparse terms' postings of the window added into LDS) is > alpha
+//    * R(d), so S(d) >= th0 implies A(d) >= gate(th0) (the gate of k_query_bm).
+//    Documents over the gate are scored exactly (left-to-right fp64 sum in
+//    token order, as rank() accumulates) and those with S >= th0 appended to the
+//    query's candidate list.  The threshold is static, so windows and queries
+//    are independent: no cross-window state, no rising-gate sweep.
+// 3. Final (one wave per query): sort the candidates (score desc, key asc), emit
+//    the best k.  A query with more candidates than the list holds (deep exact
+//    ties at th0) goes to k_query_bm, which sweeps it with a rising gate.
+// ---------------------------------------------------------------------------
+constexpr int kWinB = 12;
+constexpr int kWin = 1 << kWinB;     // documents per window (4 tiles of 1024)
+constexpr int kWDL = kWin / 64;      // documents per lane (64)
+constexpr int kWNT = 256;            // 4 waves per workgroup, each on its own query
+constexpr int kSList = 256;          // a window's sparse postings kept in LDS for exact tf lookups
+constexpr int kSeedSlots = 1024;     // seed documents per query (LDS hash)
+constexpr int kCandMax = 2048;       // largest candidate list per query (final kernel LDS)
+static_assert(kWDL == 64, "one lane owns 64 documents: four uint4 impact loads per heavy term");
+
+__device__ __forceinline__ uint32_t gate_of(double th0, double alpha) {
+  if (!(th0 > 0.0)) return 1u;
+  const double g = floor(__dmul_rn(__dmul_rn(th0, alpha), 1.0 - 0x1p-40));
+  return g >= 0.0 ? (uint32_t)g + 1u : 1u;
+}
+
+struct QSeedArgs {
+  const int64_t *off;
+  const int32_t *docno_o, *tf_o;  // reduce order: tf desc, docno asc
+  const double *lut, *idf;
+  int64_t V;
+  const int32_t *hrow_of;         // term -> heavy row or -1 (nullptr: none)
+  const uint8_t *tfrow;           // [H][hstride] tf bytes at docno - dmin
+  int64_t hstride, dmin;
+  const int32_t *terms;
+  const int64_t *qoff;
+  int nq, k, M;
+  double *th0;
+};
+
+__global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
+  __shared__ int32_t hk[kSeedSlots];                // docno (INT32_MIN empty: never a docno)
+  __shared__ unsigned long long hs[kSeedSlots];     // best S' bits (non-negative doubles order as u64)
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < a.nq; q += gridDim.x) {
+    const int64_t q0 = a.qoff[q];
+    const int nt = (int)(a.qoff[q + 1] - q0);
+    int64_t mb = 0;
+    int32_t mdf = 0, hr = -1;
+    double midf = 0.0;
+    if (lane < nt) {
+      const int32_t t = a.terms[q0 + lane];
+      if (t >= 0 && t < a.V) {
+        mb = a.off[t];
+        mdf = (int32_t)(a.off[t + 1] - mb);
+        midf = a.idf[t];
+        if (a.hrow_of && mdf > 0) hr = a.hrow_of[t];
+      }
+    }
+    const uint64_t am = (uint64_t)__ballot(lane < nt && mdf > 0);
+    const uint64_t hm = (uint64_t)__ballot(hr >= 0 && mdf > 0);
+    for (int i = lane; i < kSeedSlots; i += 64) {
+      hk[i] = INT32_MIN;
+      hs[i] = 0ull;
+    }
+    __syncthreads();
+    // seeds per term: M, so that every term's seeds fit the table at load <= 1/2
+    const int na = __popcll(am);
+    const int M = na > 0 ? min(a.M, (kSeedSlots / 2) / na) : 0;
+    for (uint64_t mj = am; mj; mj &= mj - 1) {
+      const int j = (int)__builtin_ctzll(mj);
+      const int64_t b = rl64(mb, j);
+      const int32_t n = min(M, __builtin_amdgcn_readlane(mdf, j));
+      for (int32_t i0 = 0; i0 < n; i0 += 64) {
+        const int32_t i = i0 + lane;
+        if (i >= n) continue;
+        const int32_t d = a.docno_o[b + i], fj = a.tf_o[b + i];
+        double S = 0.0;
+        for (uint64_t m = am; m; m &= m - 1) {
+          const int x = (int)__builtin_ctzll(m);
+          int f = 0;
+          if (x == j) f = fj;
+          else if ((hm >> x) & 1)
+            f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(hr, x) * a.hstride + ((int64_t)d - a.dmin)];
+          if (f != 0) S = __dadd_rn(S, __dmul_rn(a.lut[f], rld(midf, x)));
+        }
+        uint32_t h = qhash32((uint32_t)d) & (kSeedSlots - 1);
+        for (;;) {
+          const int32_t old = atomicCAS(&hk[h], INT32_MIN, d);
+          if (old == INT32_MIN || old == d) break;
+          h = (h + 1) & (kSeedSlots - 1);
+        }
+        atomicMax(&hs[h], (unsigned long long)__double_as_longlong(S));
+      }
+    }
+    __syncthreads();
+    // k-th largest S' over the distinct seeds: compact, then a bitonic sort
+    __shared__ double ss[kSeedSlots];
+    __shared__ uint64_t sk_[kSeedSlots];
+    __shared__ int s_n;
+    if (lane == 0) s_n = 0;
+    __syncthreads();
+    for (int i = lane; i < kSeedSlots; i += 64)
+      if (hk[i] != INT32_MIN) {
+        const int p = atomicAdd(&s_n, 1);
+        ss[p] = __longlong_as_double((long long)hs[i]);
+        sk_[p] = (uint64_t)(uint32_t)hk[i];
+      }
+    __syncthreads();
+    const int n = s_n;
+    double th = -1.0;
+    if (n >= a.k) {
+      int n2 = 2;
+      while (n2 < n) n2 <<= 1;
+      for (int i = n + lane; i < n2; i += 64) {
+        ss[i] = -INFINITY;
+        sk_[i] = kNoKey;
+      }
+      __syncthreads();
+      wave_sort(ss, sk_, n2);
+      th = ss[a.k - 1];
+    }
+    if (lane == 0) a.th0[q] = th;
+    __syncthreads();
+  }
+}
+
+struct QWinArgs {
+  const int64_t *off;
+  const int32_t *docno, *tf;   // docno-order CSR
+  const double *lut, *idf;
+  int64_t V;
+  const int32_t *row_of, *sk;  // batch rows, skip table [rows][T + 1]
+  const uint8_t *qlut;         // impact tables [rows][256]
+  const int32_t *hrow_of;      // nullptr: no heavy rows
+  const uint8_t *imp, *tfrow;  // [H][hstride] impact / tf bytes
+  int64_t hstride, dmin, T, nwin;
+  const int32_t *terms;
+  const int64_t *qoff;
+  const int32_t *qorder;
+  int nq, nslices, reftie, cap;
+  double alpha;
+  const double *th0;
+  unsigned int *ccnt;          // candidates per query
+  double *cs;                  // [nq][cap] scores
+  uint64_t *ck;                // [nq][cap] doc keys
+};
+
+__global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
+  __shared__ uint32_t lacc_all[kWNT / 64][kWin / 2];  // sparse impact sums, u16 pairs (see below)
+  __shared__ uint32_t slist_all[kWNT / 64][kSList];   // the window's sparse postings: r | tf << 12
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t *lacc = lacc_all[wv], *slist = slist_all[wv];
+  // workgroup -> (window, query slice): the 8 XCDs (b % 8) on 8 windows, every
+  // slice of one window on one XCD
+  const int64_t G = 8 * (int64_t)a.nslices;
+  const int64_t b = blockIdx.x, w = b % G;
+  const int64_t x = (b / G) * 8 + (w & 7);
+  if (x >= a.nwin) return;
+  const int s = (int)(w >> 3);
+  const int p_lo = (int)((int64_t)a.nq * s / a.nslices), p_hi = (int)((int64_t)a.nq * (s + 1) / a.nslices);
+  const int64_t wbase = a.dmin + (x << kWinB);    // first docno of the window
+  const int64_t hoff = (x << kWinB) + (int64_t)kWDL * lane;  // this lane's bytes in a heavy row
+  for (int pos = p_lo + wv; pos < p_hi; pos += kWNT / 64) {
+    const int q = a.qorder ? a.qorder[pos] : pos;
+    const int64_t q0 = a.qoff[q];
+    const int nt = (int)(a.qoff[q + 1] - q0);  // <= 64 (host checked)
+    int64_t mb = 0;
+    int32_t mdf = 0, brow = 0, hr = -1;
+    double midf = 0.0;
+    if (lane < nt) {
+      const int32_t t = a.terms[q0 + lane];
+      if (t >= 0 && t < a.V) {
+        mb = a.off[t];
+        mdf = (int32_t)(a.off[t + 1] - mb);
+        midf = a.idf[t];
+        brow = a.row_of[t];
+        if (a.hrow_of && mdf > 0) hr = a.hrow_of[t];
+      }
+    }
+    const uint64_t hm = (uint64_t)__ballot(hr >= 0);
+    const uint64_t sm = (uint64_t)__ballot(lane < nt && mdf > 0 && hr < 0);
+    if ((hm | sm) == 0) continue;
+    const double th0 = a.th0[q];
+    const uint32_t gate = gate_of(th0, a.alpha);
+    // sparse terms: postings of the window (skip table at 1024-doc tiles)
+    int32_t mc = 0, me = 0;
+    if ((sm >> lane) & 1) {
+      const int32_t *row = a.sk + (int64_t)brow * (a.T + 1);
+      mc = row[x << 2];
+      me = row[(x << 2) + 4];
+    }
+    // heavy terms: impact bytes of this lane's 64 documents, four terms' loads in flight
+    uint32_t acc[kWDL / 2];  // acc[m]: documents 2m (low u16), 2m + 1 (high) of the lane
+#pragma unroll
+    for (int m = 0; m < kWDL / 2; m++) acc[m] = 0;
+    for (uint64_t mh = hm; mh;) {
+      uint4 v[4][4];
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        if (mh) {
+          const int j = (int)__builtin_ctzll(mh);
+          mh &= mh - 1;
+          const uint4 *p = reinterpret_cast<const uint4 *>(
+              a.imp + (int64_t)__builtin_amdgcn_readlane(hr, j) * a.hstride + hoff);
+#pragma unroll
+          for (int c = 0; c < 4; c++) v[g][c] = p[c];
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; c++) v[g][c] = make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 4; g++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const uint32_t w4[4] = {v[g][c].x, v[g][c].y, v[g][c].z, v[g][c].w};
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            acc[8 * c + 2 * u] += __builtin_amdgcn_perm(0u, w4[u], 0x0C010C00u);
+            acc[8 * c + 2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
+          }
+        }
+    }
+    const int32_t cj = ((sm >> lane) & 1) ? me - mc : 0;
+    const int32_t incl = wave_incl_sum(cj), prej = incl - cj;
+    const int32_t total = __shfl(incl, 63, 64);
+    const bool listed = total <= kSList;  // else exact tf lookups search the global postings
+    if (total > 0) {
+      // lacc[m * 64 + l] holds documents 64 l + 2m (low), + 1 (high): lane l's
+      // 32 words are a conflict-free column
+#pragma unroll
+      for (int m = 0; m < kWDL / 2; m++) lacc[m * 64 + lane] = 0;
+      qwave_sync();
+      const int64_t plo = mb + mc;
+      for (int32_t e0 = 0; e0 < total; e0 += 64) {
+        const int32_t e = e0 + lane;
+        int64_t pb = 0;
+        double wj = 0.0;
+        int rj = 0;
+        for (uint64_t m = sm; m; m &= m - 1) {
+          const int j = (int)__builtin_ctzll(m);
+          const int32_t pj = __builtin_amdgcn_readlane(prej, j);
+          if (e >= pj) {
+            pb = rl64(plo, j) - pj;
+            wj = rld(midf, j);
+            rj = __builtin_amdgcn_readlane(brow, j);
+          }
+        }
+        if (e < total) {
+          const int32_t d = a.docno[pb + e], f = a.tf[pb + e];
+          const int r = (int)((int64_t)d - wbase);
+          const uint32_t qv = f <= 255 ? (uint32_t)a.qlut[(int64_t)rj * 256 + f] : impact(a.lut[f], wj, a.alpha);
+          atomicAdd(&lacc[((r & 63) >> 1) * 64 + (r >> 6)], qv << ((r & 1) << 4));
+          if (listed) slist[e] = (uint32_t)r | ((uint32_t)min(f, 0xFFFFF) << 12);
+        }
+      }
+      qwave_sync();
+#pragma unroll
+      for (int m = 0; m < kWDL / 2; m++) acc[m] += lacc[m * 64 + lane];
+    }
+    // documents over the gate
+    uint64_t cm = 0;
+#pragma unroll
+    for (int m = 0; m < kWDL / 2; m++) {
+      if ((acc[m] & 0xFFFFu) >= gate) cm |= 1ull << (2 * m);
+      if ((acc[m] >> 16) >= gate) cm |= 1ull << (2 * m + 1);
+    }
+    const uint64_t amask = hm | sm;
+    for (;;) {
+      const bool have = cm != 0;
+      if (__ballot(have) == 0) break;  // wave-uniform
+      double S = 0.0;
+      uint64_t key = kNoKey;
+      bool keep = false;
+      if (have) {
+        const int bb = (int)__builtin_ctzll(cm);
+        cm &= cm - 1;
+        const int r = kWDL * lane + bb;
+        const int32_t d = (int32_t)(wbase + r);
+        uint32_t tie = 0xFFFFFFFFu;
+        for (uint64_t m = amask; m; m &= m - 1) {
+          const int j = (int)__builtin_ctzll(m);
+          int f = 0;
+          if ((hm >> j) & 1) {
+            f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(hr, j) * a.hstride + (x << kWinB) + r];
+          } else if (listed) {
+            int lo = __builtin_amdgcn_readlane(prej, j), hi = lo + __builtin_amdgcn_readlane(cj, j);
+            while (lo < hi) {  // the term's entries are docno-ascending
+              const int mid = (lo + hi) >> 1;
+              if ((int)(slist[mid] & 0xFFFu) < r) lo = mid + 1;
+              else hi = mid;
+            }
+            if (lo < __builtin_amdgcn_readlane(prej, j) + __builtin_amdgcn_readlane(cj, j) &&
+                (int)(slist[lo] & 0xFFFu) == r) {
+              f = (int)(slist[lo] >> 12);
+              if (f == 0xFFFFF) f = -1;  // tf >= 2^20: read it from the postings
+            }
+          } else {
+            f = -1;
+          }
+          if (f < 0) {  // global binary search over the term's postings in the window
+            const int64_t base = rl64(mb, j);
+            int64_t lo = base + __builtin_amdgcn_readlane(mc, j);
+            const int64_t e = base + __builtin_amdgcn_readlane(me, j);
+            int64_t hi = e;
+            while (lo < hi) {
+              const int64_t mid = (lo + hi) >> 1;
+              if (a.docno[mid] < d) lo = mid + 1;
+              else hi = mid;
+            }
+            f = (lo < e && a.docno[lo] == d) ? a.tf[lo] : 0;
+          }
+          if (f != 0) {
+            S = __dadd_rn(S, __dmul_rn(a.lut[f], rld(midf, j)));
+            if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f);
+          }
+        }
+        key = doc_key(a.reftie ? tie : 0u, d);
+        keep = S >= th0;  // th0 < 0 (no seed): every touched document
+      }
+      const uint64_t km = (uint64_t)__ballot(keep);
+      if (km) {
+        unsigned int base = 0;
+        if (lane == 0) base = atomicAdd(&a.ccnt[q], (unsigned int)__popcll(km));
+        base = (unsigned int)__shfl((int)base, 0, 64);
+        if (keep) {
+          const unsigned int idx = base + lane_prefix(km);
+          if (idx < (unsigned int)a.cap) {
+            a.cs[(int64_t)q * a.cap + idx] = S;
+            a.ck[(int64_t)q * a.cap + idx] = key;
+          }
+        }
+      }
+    }
+    qwave_sync();  // this wave's LDS is rewritten by its next query
+  }
+}
+
+struct QFinalArgs {
+  int nq, k, cap;
+  const unsigned int *ccnt;
+  const double *cs;
+  const uint64_t *ck;
+  int32_t *out_d;
+  double *out_s;
+  uint32_t *out_t;
+  int32_t *ovf;               // queries whose list overflowed
+  unsigned int *novf;
+};
+
+__global__ __launch_bounds__(64) void k_query_final(QFinalArgs a) {
+  __shared__ double bs[kCandMax];
+  __shared__ uint64_t bk[kCandMax];
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < a.nq; q += gridDim.x) {
+    const unsigned int c = a.ccnt[q];
+    if (c > (unsigned int)a.cap) {
+      if (lane == 0) a.ovf[atomicAdd(a.novf, 1u)] = q;
+      continue;
+    }
+    const int n = (int)c;
+    int n2 = 2;
+    while (n2 < n) n2 <<= 1;
+    for (int i = lane; i < n2; i += 64) {
+      bs[i] = i < n ? a.cs[(int64_t)q * a.cap + i] : -INFINITY;
+      bk[i] = i < n ? a.ck[(int64_t)q * a.cap + i] : kNoKey;
+    }
+    __syncthreads();
+    wave_sort(bs, bk, n2);
+    for (int r = lane; r < a.k; r += 64) {
+      a.out_d[(int64_t)q * a.k + r] = r < n ? key_doc(bk[r]) : -1;
+      a.out_s[(int64_t)q * a.k + r] = r < n ? bs[r] : 0.0;
+      if (a.out_t) a.out_t[(int64_t)q * a.k + r] = r < n ? (uint32_t)(bk[r] >> 32) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+  }
+}
+
+// impact rows from tf rows: q(tf) = floor(lut[tf] * idf * alpha) + 1 (0 for tf = 0)
+__global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const int32_t *hterm, int64_t H,
+                                                   int64_t stride, const double *lut, int max_tf, const double *idf,
+                                                   double alpha, uint8_t *imp) {
+  __shared__ uint8_t ql[256];
+  const int64_t chunks = stride >> 12;  // 4096-byte chunks per row
+  for (int64_t c = blockIdx.x; c < H * chunks; c += gridDim.x) {
+    const int64_t row = c / chunks;
+    const double wi = idf[hterm[row]];
+    __syncthreads();
+    const int f = threadIdx.x;
+    ql[f] = (uint8_t)(f == 0 ? 0u : f <= max_tf ? impact(lut[f], wi, alpha) : 255u);
+    __syncthreads();
+    const uint4 *src = reinterpret_cast<const uint4 *>(tfrow + c * 4096);
+    uint4 *dst = reinterpret_cast<uint4 *>(imp + c * 4096);
+    const uint4 v = src[threadIdx.x];
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      o[u] = (uint32_t)ql[w4[u] & 0xFF] | ((uint32_t)ql[(w4[u] >> 8) & 0xFF] << 8) |
+             ((uint32_t)ql[(w4[u] >> 16) & 0xFF] << 16) | ((uint32_t)ql[w4[u] >> 24] << 24);
+    dst[threadIdx.x] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+// largest weight of any term (its max tf is the first posting of the
+// reduce-order CSR): the index's impact scale alpha = 253.5 / wmax
+__global__ void k_index_wmax(const int64_t *off, int64_t V, const int32_t *tf_o, const double *lut,
+                             const double *idf, unsigned long long *wmax_bits) {
+  unsigned long long wm = 0;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
+    if (off[t + 1] > off[t]) {
+      const unsigned long long wb =
+          (unsigned long long)__double_as_longlong(__dmul_rn(lut[tf_o[off[t]]], idf[t]));
+      wm = wb > wm ? wb : wm;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long u = __shfl_xor(wm, o, 64);
+    wm = u > wm ? u : wm;
+  }
+  if ((threadIdx.x & 63) == 0 && wm) atomicMax(wmax_bits, wm);
+}
+
+// Index-resident query structures, built once per index and heavy threshold:
+// the heavy terms' tf rows with their 16 / 1024-document maxima (k_query_bm),
+// the index's impact scale alpha = 253.5 / (largest weight of any term) and the
+// heavy terms' impact rows q(tf) at that scale (k_query_win).  The impact rows
+// and alpha depend on idf: sme_index_reweight drops them (q_ready).
 void prepare_queries(sme_index *ix, hipStream_t st) {
   sme_ctx *cx = ix->ctx;
   const int64_t div = cx->opt_heavy_div;
@@ -951,8 +1406,25 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
   SME_HIP(hipEventCreate(&e1));
   SME_HIP(hipEventRecord(e0, st));
   ix->q_H = 0;
-  ix->q_T = (ix->V > 0 && ix->P > 0 && ix->dmax >= ix->dmin) ? ((ix->dmax - ix->dmin) >> kQB) + 1 : 0;
+  // tiles of 1024 documents, a multiple of 4 (k_query_win's 4096-document windows)
+  ix->q_T = (ix->V > 0 && ix->P > 0 && ix->dmax >= ix->dmin) ? ((((ix->dmax - ix->dmin) >> kQB) + 1 + 3) & ~int64_t(3))
+                                                             : 0;
   const int64_t V = ix->V, T = ix->q_T;
+  ix->q_alpha = 1.0;
+  if (V > 0 && ix->P > 0) {
+    unsigned long long *wb = reinterpret_cast<unsigned long long *>(cx->ws[35].as<uint64_t>(1));
+    SME_HIP(hipMemsetAsync(wb, 0, sizeof(uint64_t), st));
+    hipLaunchKernelGGL(k_index_wmax, dim3((unsigned)std::min<int64_t>((V + 255) / 256, 4096)), dim3(256), 0, st,
+                       (const int64_t *)ix->d_off.p, V, (const int32_t *)ix->d_tf_o.p, (const double *)ix->d_lut.p,
+                       (const double *)ix->d_idf.p, wb);
+    SME_CHECK_LAUNCH();
+    unsigned long long h = 0;
+    SME_HIP(hipMemcpyAsync(&h, wb, sizeof h, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    ix->q_wmax_bits = h;
+    const double wmax = __builtin_bit_cast(double, h);
+    ix->q_alpha = wmax > 0.0 ? 253.5 / wmax : 1.0;
+  }
   if (T > 0 && div > 0) {
     auto &W = cx->ws;
     const int64_t *off = (const int64_t *)ix->d_off.p;
@@ -971,7 +1443,7 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     // memory budget for the rows: 1/8 of the device's free memory, at most 16 GB
     size_t fr = 0, tot = 0;
     SME_HIP(hipMemGetInfo(&fr, &tot));
-    const double per_row = (double)stride + (double)(T << 6) + (double)T;
+    const double per_row = 2.0 * (double)stride + (double)(T << 6) + (double)T;
     const int64_t cap = (int64_t)(std::min<double>((double)fr / 8.0, 16e9) / per_row);
     const int64_t H = std::min<int64_t>(nh, cap);
     int32_t *hrow_of = ix->d_hrow_of.as<int32_t>(V);
@@ -984,7 +1456,7 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, hdf, hpre, (int)H + 1, st));
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, hdf, hpre, (int)H + 1, st));
       uint8_t *buf = ix->d_heavy.as<uint8_t>((size_t)H * (size_t)per_row + 64);
-      uint8_t *tfrow = buf, *bm16 = buf + H * stride, *bm1k = bm16 + H * (T << 6);
+      uint8_t *tfrow = buf, *imp = buf + H * stride, *bm16 = imp + H * stride, *bm1k = bm16 + H * (T << 6);
       SME_HIP(hipMemsetAsync(tfrow, 0, (size_t)(H * stride), st));
       hipLaunchKernelGGL(k_heavy_fill, dim3(16384), dim3(256), 0, st, hpre, H, hterm, off,
                          (const int32_t *)ix->d_docno_d.p, (const int32_t *)ix->d_tf_d.p, ix->dmin, stride, tfrow);
@@ -993,7 +1465,11 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
                          st, (const uint4 *)tfrow, n16, bm16);
       hipLaunchKernelGGL(k_heavy_bm1k, dim3((unsigned)std::min<int64_t>((n1k + 255) / 256, 1 << 16)), dim3(256), 0,
                          st, (const uint4 *)bm16, n1k, bm1k);
+      hipLaunchKernelGGL(k_heavy_imp, dim3((unsigned)std::min<int64_t>(H * (stride >> 12), 1 << 16)), dim3(256), 0, st,
+                         tfrow, hterm, H, stride, (const double *)ix->d_lut.p, ix->max_tf,
+                         (const double *)ix->d_idf.p, ix->q_alpha, imp);
       SME_CHECK_LAUNCH();
+      ix->q_imp = imp;
       ix->q_tfrow = tfrow;
       ix->q_bm16 = bm16;
       ix->q_bm1k = bm1k;
@@ -1085,9 +1561,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           hipLaunchKernelGGL(k_skip_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T, skw);
           hipLaunchKernelGGL(k_skip_suffix, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 16384)), dim3(256), 0,
                              st, nrows, T, skw);
-          const unsigned gR = (unsigned)std::min<int64_t>((nrows + 255) / 256, 8192);
-          hipLaunchKernelGGL(k_row_wmax, dim3(gR), dim3(256), 0, st, tor, rdf, nrows, off,
-                             (const int32_t *)ix->d_tf_o.p, lut, idf, wmax);
+          // impact scale: the index's (prepare_queries), shared by every batch
+          SME_HIP(hipMemcpyAsync(wmax, &ix->q_wmax_bits, sizeof(uint64_t), hipMemcpyHostToDevice, st));
           hipLaunchKernelGGL(k_row_qlut, dim3((unsigned)std::min<int64_t>(nrows, 16384)), dim3(256), 0, st, tor, nrows,
                              lut, ix->max_tf, idf, (const unsigned long long *)wmax, ql);
           SME_CHECK_LAUNCH();
@@ -1109,9 +1584,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     qord = qi + nq;
   }
   // events on the launch stream bracket the scoring kernel (bench.py roofline)
-  hipEvent_t e0, e1;
-  SME_HIP(hipEventCreate(&e0));
-  SME_HIP(hipEventCreate(&e1));
+  hipEvent_t e0, e1, e2, e3;
+  for (hipEvent_t *e : {&e0, &e1, &e2, &e3}) SME_HIP(hipEventCreate(e));
   SME_HIP(hipEventRecord(e0, st));
   unsigned long long *qstats = nullptr;
 #ifdef SME_EXPERIMENTS
@@ -1121,8 +1595,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     SME_HIP(hipMemsetAsync(qstats, 0, 8 * sizeof(uint64_t), st));
   }
 #endif
+  QBmArgs qa{};
   if (tiled) {
-    QBmArgs qa;
     qa.off = off;
     qa.docno = dn;
     qa.tf = tf;
@@ -1151,37 +1625,137 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     qa.out_t = d_out_tie;
     qa.wmax_bits = (const unsigned long long *)wmax;
     qa.stats = qstats;
-    const unsigned wgrid = (unsigned)std::min<int64_t>(8 * (((int64_t)nq + 7) / 8), 1 << 30);
-    if (k <= 64)
-      hipLaunchKernelGGL(k_query_bm<128>, dim3(wgrid), dim3(64), 0, st, qa);
-    else if (k <= 192)
-      hipLaunchKernelGGL(k_query_bm<256>, dim3(wgrid), dim3(64), 0, st, qa);
-    else
-      hipLaunchKernelGGL(k_query_bm<512>, dim3(wgrid), dim3(64), 0, st, qa);
-  } else if (k <= 16) {
-    const unsigned grid = (unsigned)std::min(nq, 1 << 20);
-    hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
-                       d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
-  } else {
-    const unsigned grid = (unsigned)std::min(nq, 1 << 20);
-    hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
-                       d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
   }
-  SME_CHECK_LAUNCH();
-  SME_HIP(hipEventRecord(e1, st));
+  auto launch_bm = [&](const QBmArgs &x) {
+    const unsigned wgrid = (unsigned)std::min<int64_t>(8 * (((int64_t)x.nq + 7) / 8), 1 << 30);
+    if (k <= 64)
+      hipLaunchKernelGGL(k_query_bm<128>, dim3(wgrid), dim3(64), 0, st, x);
+    else if (k <= 192)
+      hipLaunchKernelGGL(k_query_bm<256>, dim3(wgrid), dim3(64), 0, st, x);
+    else
+      hipLaunchKernelGGL(k_query_bm<512>, dim3(wgrid), dim3(64), 0, st, x);
+  };
+  const bool win = tiled && cx->opt_query_kernel == 0;
+  int64_t n_ovf = 0;
+  if (win) {
+    // 1. seed thresholds
+    double *th0 = W[41].as<double>(nq);
+    QSeedArgs sa;
+    sa.off = off;
+    sa.docno_o = (const int32_t *)ix->d_docno_o.p;
+    sa.tf_o = (const int32_t *)ix->d_tf_o.p;
+    sa.lut = lut;
+    sa.idf = idf;
+    sa.V = V;
+    sa.hrow_of = qa.hrow_of;
+    sa.tfrow = ix->q_tfrow;
+    sa.hstride = T << kQB;
+    sa.dmin = ix->dmin;
+    sa.terms = d_terms;
+    sa.qoff = d_qoff;
+    sa.nq = nq;
+    sa.k = k;
+    sa.M = (int)std::min<int64_t>(std::max<int64_t>(cx->opt_seed_m, cx->opt_seed_m > 0 ? 2 * (int64_t)k : 0),
+                                  kSeedSlots / 2);
+    sa.th0 = th0;
+    hipLaunchKernelGGL(k_query_seed, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, sa);
+    SME_CHECK_LAUNCH();
+    SME_HIP(hipEventRecord(e1, st));
+    // 2. windows x query slices
+    const int cap = (int)std::min<int64_t>(cx->opt_cand_cap, kCandMax);
+    unsigned int *ccnt = W[42].as<unsigned int>(nq + 1);
+    double *cs = W[43].as<double>((size_t)nq * cap);
+    uint64_t *ckk = W[61].as<uint64_t>((size_t)nq * cap);
+    int32_t *ovf = W[62].as<int32_t>(nq + 2);
+    unsigned int *novf = ccnt + nq;
+    SME_HIP(hipMemsetAsync(ccnt, 0, (nq + 1) * sizeof(unsigned int), st));
+    QWinArgs wa;
+    wa.off = off;
+    wa.docno = dn;
+    wa.tf = tf;
+    wa.lut = lut;
+    wa.idf = idf;
+    wa.V = V;
+    wa.row_of = row_of;
+    wa.sk = sk;
+    wa.qlut = qlut;
+    wa.hrow_of = qa.hrow_of;
+    wa.imp = ix->q_imp;
+    wa.tfrow = ix->q_tfrow;
+    wa.hstride = T << kQB;
+    wa.dmin = ix->dmin;
+    wa.T = T;
+    wa.nwin = T >> 2;
+    wa.terms = d_terms;
+    wa.qoff = d_qoff;
+    wa.qorder = qord;
+    wa.nq = nq;
+    wa.nslices = (int)std::max<int64_t>(1, std::min<int64_t>(nq / 512, 4096));
+    wa.reftie = reftie;
+    wa.cap = cap;
+    wa.alpha = ix->q_alpha;
+    wa.th0 = th0;
+    wa.ccnt = ccnt;
+    wa.cs = cs;
+    wa.ck = ckk;
+    const int64_t G = 8 * (int64_t)wa.nslices;
+    const int64_t wg = ((wa.nwin + 7) / 8) * G;
+    if (wg >= (int64_t(1) << 31)) throw Error(SME_ELIMIT, "query batch x windows too large for one launch");
+    hipLaunchKernelGGL(k_query_win, dim3((unsigned)wg), dim3(kWNT), 0, st, wa);
+    SME_CHECK_LAUNCH();
+    SME_HIP(hipEventRecord(e2, st));
+    // 3. per-query selection; overflowed lists -> k_query_bm
+    QFinalArgs fa{nq, k, cap, ccnt, cs, ckk, d_out_docno, d_out_score, d_out_tie, ovf, novf};
+    hipLaunchKernelGGL(k_query_final, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, fa);
+    SME_CHECK_LAUNCH();
+    unsigned int h_novf = 0;
+    SME_HIP(hipMemcpyAsync(&h_novf, novf, sizeof h_novf, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    n_ovf = h_novf;
+    if (n_ovf > 0) {
+      QBmArgs ob = qa;
+      ob.qorder = ovf;
+      ob.nq = (int)n_ovf;
+      launch_bm(ob);
+      SME_CHECK_LAUNCH();
+    }
+  } else if (tiled) {
+    SME_HIP(hipEventRecord(e1, st));
+    launch_bm(qa);
+    SME_CHECK_LAUNCH();
+    SME_HIP(hipEventRecord(e2, st));
+  } else {
+    SME_HIP(hipEventRecord(e1, st));
+    const unsigned grid = (unsigned)std::min(nq, 1 << 20);
+    if (k <= 16)
+      hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
+                         d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
+    else
+      hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
+                         d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
+    SME_CHECK_LAUNCH();
+    SME_HIP(hipEventRecord(e2, st));
+  }
+  SME_HIP(hipEventRecord(e3, st));
   int h_err = 0;
   SME_HIP(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, st));
   SME_HIP(hipStreamSynchronize(st));
-  float ms = 0, pms = 0;
-  SME_HIP(hipEventElapsedTime(&ms, e0, e1));
+  float ms = 0, pms = 0, sms = 0, fms = 0;
+  SME_HIP(hipEventElapsedTime(&ms, e1, e2));
   SME_HIP(hipEventElapsedTime(&pms, ep, e0));
+  SME_HIP(hipEventElapsedTime(&sms, e0, e1));
+  SME_HIP(hipEventElapsedTime(&fms, e2, e3));
   cx->last_query_ms = ms;
   cx->last_query_prep_ms = pms;
+  cx->last_query_seed_ms = sms;
+  cx->last_query_final_ms = fms;
+  cx->last_query_total_ms = sms + ms + fms;
+  cx->last_query_overflow = n_ovf;
   cx->last_query_index_ms = tiled ? ix->q_prep_ms : 0.0f;
-  (void)hipEventDestroy(ep);
   cx->last_query_tiled = tiled;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  cx->last_query_name = win ? "k_query_win" : tiled ? "k_query_bm" : "k_query";
+  (void)hipEventDestroy(ep);
+  for (hipEvent_t e : {e0, e1, e2, e3}) (void)hipEventDestroy(e);
   if (qstats) {
     uint64_t h[8];
     SME_HIP(hipMemcpy(h, qstats, sizeof h, hipMemcpyDeviceToHost));

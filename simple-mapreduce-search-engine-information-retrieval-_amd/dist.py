@@ -25,6 +25,8 @@ result equals the single-index result bit for bit: a document's score only uses 
 own postings, and N / df are the global ones.  A docid duplicated ACROSS shards would
 be merged by the reference's single reducer but stays two postings here.
 """
+import importlib
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -134,12 +136,8 @@ def global_df(local_df, l2g, n_global_terms, group=None):
 
 
 def _hip_d2d(dst, src, nbytes, stream):
-    import ctypes as C
-    h = C.CDLL("libamdhip64.so")
-    h.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
-    rc = h.hipMemcpyAsync(C.c_void_p(dst), C.c_void_p(src), nbytes, 3, C.c_void_p(stream))
-    if rc != 0:
-        raise RuntimeError("hipMemcpyAsync failed: %d" % rc)
+    """device -> device copy on `stream` through libsme's HIP runtime."""
+    importlib.import_module(__package__).memcpy(dst, src, nbytes, stream)
 
 
 def global_df_index(ix, group=None, timings=None):

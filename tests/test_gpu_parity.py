@@ -180,7 +180,8 @@ def test_queries_vs_oracle(sme, synth, idf_mode):
 
 def _query_opts(ix, terms, qoff, k, **opts):
     """Query with context path options set (sme_set_option), then restore the defaults."""
-    defaults = {"query_kernel": 0, "heavy_div": 32, "seed_tiles": 4, "query_order": 1}
+    defaults = {"query_kernel": 0, "heavy_div": 32, "seed_tiles": 4, "query_order": 1, "cand_cap": 1024,
+                "seed_m": 64}
     try:
         for n, v in opts.items():
             ix.ctx.set_option(n, v)
@@ -191,13 +192,17 @@ def _query_opts(ix, terms, qoff, k, **opts):
 
 
 def _query_both_kernels(ix, terms, qoff, k):
-    """Default block-max scoring (heavy rows for terms covering >= 1/32 of the
-    docno span, 4 seed tiles), the same on postings only, every term heavy, only
-    full-span terms heavy, no seed tiles, batch query order, and the streaming
-    kernel (k <= 32): all identical bits."""
+    """Default window-major scoring (seeded threshold, heavy impact rows for terms
+    covering >= 1/32 of the docno span), the same on postings only, every term
+    heavy, only full-span terms heavy, without seeds, with candidate lists so
+    short that most queries overflow to the block-max sweep, the block-max sweep
+    itself (4 / 0 / 8 seed tiles, batch order), and the streaming kernel
+    (k <= 32): all identical bits."""
     dn, sc = ix.query_topk(terms, qoff, k)
-    variants = [{"heavy_div": 0}, {"heavy_div": 1 << 30}, {"heavy_div": 1}, {"seed_tiles": 0},
-                {"seed_tiles": 8, "query_order": 0}]
+    assert ix.ctx.last_build_profile()["query_kernel_name"] in ("k_query_win", "k_query")
+    variants = [{"heavy_div": 0}, {"heavy_div": 1 << 30}, {"heavy_div": 1}, {"seed_m": 0}, {"cand_cap": 4},
+                {"cand_cap": 1, "heavy_div": 1}, {"query_kernel": 2}, {"query_kernel": 2, "seed_tiles": 0},
+                {"query_kernel": 2, "seed_tiles": 8, "query_order": 0}, {"query_kernel": 2, "heavy_div": 0}]
     if k <= 32:
         variants.append({"query_kernel": 1})
     for v in variants:
@@ -237,7 +242,7 @@ def test_queries_multi_tile(sme, synth):
         long_terms = np.concatenate([tu[:ou[3]], q64])
         long_off = np.concatenate([ou[:4], [ou[3] + nlong]]).astype(np.int64)
         dn, sc = ix.query_topk(long_terms, long_off, 10)
-        assert ix.ctx.last_build_profile()["query_kernel_name"] == ("k_query_bm" if nlong == 64 else "k_query")
+        assert ix.ctx.last_build_profile()["query_kernel_name"] == ("k_query_win" if nlong == 64 else "k_query")
         for q in range(4):
             tl = [names[t] for t in long_terms[long_off[q]:long_off[q + 1]] if t >= 0]
             rd, rs = ref.query(tl, 10, 0, 0)
@@ -488,19 +493,16 @@ def test_weight_pass_and_reweight(sme, synth, idf_mode):
     assert np.array_equal(w, _expected_weights(ix, idf_mode))
     # reweight with a larger global N and per-term df + 3 (as after a df all-reduce)
     df = ix.csr()[3].astype(np.int64) + 3
-    hip = C.CDLL("libamdhip64.so")
-    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
-    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    hip.hipFree.argtypes = [C.c_void_p]
+    L = sme.lib()
     d_df = C.c_void_p()
-    assert hip.hipMalloc(C.byref(d_df), df.nbytes) == 0
+    assert L.sme_device_alloc(0, df.nbytes, C.byref(d_df)) == 0
     try:
-        assert hip.hipMemcpy(d_df, df.ctypes.data, df.nbytes, 1) == 0
+        sme.memcpy(d_df.value, df.ctypes.data, df.nbytes)
         ix.reweight(7 * n, d_df.value)
         _, _, w2 = ix.weights()
         assert np.array_equal(w2, _expected_weights(ix, idf_mode, N=7 * n, df_override=df))
     finally:
-        hip.hipFree(d_df)
+        L.sme_device_free(d_df)
 
 
 def test_query_term_id_bounds(sme, synth):

@@ -81,10 +81,12 @@ def main():
                           "wall_ms": round(float(np.median(walls[1:])), 3),
                           "qps": round(a.queries / (np.median(walls[1:]) / 1e3), 1),
                           "index_prep_ms": round(t_idx, 3), "same_as_default": same,
-                          "name": prof.get("query_kernel_name")}), flush=True)
+                          "name": prof.get("query_kernel_name"),
+                          "split": {x: prof.get(x) for x in ("query_seed", "query_final", "query_overflow",
+                                                             "query_total") if x in prof}}), flush=True)
         for n in opts:  # restore defaults
-            ctx.set_option(n.strip(), {"heavy_div": 32, "seed_tiles": 4, "query_order": 1,
-                                       "query_kernel": 0}.get(n.strip(), 0))
+            ctx.set_option(n.strip(), {"heavy_div": 32, "seed_tiles": 4, "query_order": 1, "query_kernel": 0,
+                                       "cand_cap": 1024, "seed_m": 64}[n.strip()])
     ix.close()
     ctx.close()
 
