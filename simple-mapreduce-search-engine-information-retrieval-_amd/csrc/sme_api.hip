@@ -271,8 +271,14 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
       range(1, int64_t(1) << 30);
       cx->opt_tok_grid = v;
     } else if (n == "cand_cap") {
-      range(1, 2048);
+      range(1, 1024);
       cx->opt_cand_cap = v;
+    } else if (n == "win_sample") {
+      range(0, 1);
+      cx->opt_win_sample = v;
+    } else if (n == "win_slice") {
+      range(1, int64_t(1) << 30);
+      cx->opt_win_slice = v;
     } else if (n == "seed_m") {
       range(0, 4096);
       cx->opt_seed_m = v;
@@ -693,7 +699,7 @@ int sme_last_build_profile(const sme_ctx *cx, const char **json) {
     if (cx->last_query_ms >= 0) os << ",\"query_kernel_name\":\"" << cx->last_query_name << "\"";
     if (cx->last_query_ms >= 0 && cx->last_query_name == std::string("k_query_win"))
       os << ",\"query_seed\":" << cx->last_query_seed_ms << ",\"query_final\":" << cx->last_query_final_ms
-         << ",\"query_overflow\":" << cx->last_query_overflow << ",\"query_total\":" << cx->last_query_total_ms;
+         << ",\"query_overflow\":" << cx->last_query_overflow << ",\"query_fallback\":" << cx->last_query_fallback << ",\"query_total\":" << cx->last_query_total_ms;
     os << "}";
     const_cast<sme_ctx *>(cx)->profile_json = os.str();
     *json = cx->profile_json.c_str();

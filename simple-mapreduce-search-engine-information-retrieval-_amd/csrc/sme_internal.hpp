@@ -34,7 +34,8 @@ struct sme_ctx {
   bool last_query_tiled = false;  // tiled path (k_query_win / k_query_bm) or the streaming k_query
   const char *last_query_name = "k_query";  // the scoring kernel that ran
   float last_query_seed_ms = 0.0f, last_query_final_ms = 0.0f, last_query_total_ms = 0.0f;
-  int64_t last_query_overflow = 0;  // k_query_win queries re-run by k_query_bm (candidate list overflow)
+  int64_t last_query_overflow = 0;  // k_query_win queries whose first candidate list overflowed
+  int64_t last_query_fallback = 0;  // of those, queries finally scored by k_query_bm
   // Path options (sme_set_option).  Every setting gives identical results; they
   // exist so tests can hold each path to the others and benches can sweep them.
   int64_t opt_query_kernel = 0;   // "query_kernel": 0 window-major (auto), 1 streaming k_query, 2 block-max sweep
@@ -44,8 +45,10 @@ struct sme_ctx {
   int64_t opt_agg_two_pass = 0;   // "agg_two_pass": 1 = count + emit aggregation passes
   int64_t opt_tok_grid = 4096;    // "tok_grid": tokenizer workgroups (>= 1)
   int64_t opt_raw_load_pct = 40;  // "raw_load_pct": raw-vocabulary table load of the next build (10..90)
-  int64_t opt_cand_cap = 1024;    // "cand_cap": candidate list per query of k_query_win (1..2048)
+  int64_t opt_cand_cap = 1024;    // "cand_cap": candidate list per query of k_query_win (1..1024)
   int64_t opt_seed_m = 64;        // "seed_m": seed postings per term (k_query_seed; 0 = no seed)
+  int64_t opt_win_slice = 512;    // "win_slice": queries per k_query_win workgroup slice (>= 1)
+  int64_t opt_win_sample = 1;     // "win_sample": 1 = every 8th window first, thresholds raised, then the rest
   // pinned host staging of device -> host record copies into pageable caller
   // memory (sme_index_copy_records): two buffers, DMA into one while the host
   // copies out of the other
@@ -105,7 +108,7 @@ struct sme_index {
   // and 1024-doc block maxima of the terms covering >= 1/div of the docno span
   sme::DevBuf d_hrow_of;  // int32 [V] heavy row or -1
   sme::DevBuf d_heavy;    // u8 [H][T * 1024] tf | [H][T * 64] bm16 | [H][T] bm1k
-  const uint8_t *q_tfrow = nullptr, *q_bm16 = nullptr, *q_bm1k = nullptr, *q_imp = nullptr;
+  const uint8_t *q_tfrow = nullptr, *q_bm16 = nullptr, *q_bm1k = nullptr, *q_imp = nullptr, *q_bmq = nullptr;
   double q_alpha = 1.0;                 // impact scale 253.5 / (largest weight of any term)
   unsigned long long q_wmax_bits = 0;   // that weight's bits
   int64_t q_T = 0, q_H = 0, q_div = -1;

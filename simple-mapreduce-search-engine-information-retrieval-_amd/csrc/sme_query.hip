@@ -483,6 +483,16 @@ __global__ __launch_bounds__(256) void k_skip_suffix(int64_t nrows, int64_t T, i
     }
   }
 }
+// window-granular skip table, transposed: skt[w * nrows + row] = first posting of
+// the row's term in window w (4 tiles) or later.  Every query of a k_query_win
+// workgroup reads window x's entries, so they sit together (L2-resident).
+__global__ void k_skip_win(const int32_t *sk, int64_t nrows, int64_t T, int64_t nwin, int32_t *skt) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nrows * (nwin + 1);
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w = i / nrows, row = i - w * nrows;
+    skt[i] = sk[row * (T + 1) + (w << 2)];
+  }
+}
 // rows with df = 0 (possible only for empty terms) never get a posting: all zeros
 __global__ void k_skip_zero_rows(const int64_t *rdf, int64_t nrows, int64_t T, int32_t *sk) {
   for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x)
@@ -986,7 +996,9 @@ constexpr int kWDL = kWin / 64;      // documents per lane (64)
 constexpr int kWNT = 256;            // 4 waves per workgroup, each on its own query
 constexpr int kSList = 256;          // a window's sparse postings kept in LDS for exact tf lookups
 constexpr int kSeedSlots = 1024;     // seed documents per query (LDS hash)
-constexpr int kCandMax = 2048;       // largest candidate list per query (final kernel LDS)
+constexpr int kCandMax = 1024;       // largest candidate list per query (final kernel LDS)
+constexpr int kWinRounds = 3;        // window passes before an overflowing query goes to k_query_bm
+constexpr int kCList = 512;          // documents over the gate listed per round of exact scoring
 static_assert(kWDL == 64, "one lane owns 64 documents: four uint4 impact loads per heavy term");
 
 __device__ __forceinline__ uint32_t gate_of(double th0, double alpha) {
@@ -995,53 +1007,99 @@ __device__ __forceinline__ uint32_t gate_of(double th0, double alpha) {
   return g >= 0.0 ? (uint32_t)g + 1u : 1u;
 }
 
+// Per-batch query tables for the window path: one 32-byte record per query
+// term (postings base, df, batch row, heavy row, idf) and one per position of
+// the query order (query, first term, term count), so a wave reaches a query's
+// terms in two independent loads instead of four dependent ones.
+struct QDesc {
+  int64_t mb;
+  int32_t mdf, brow, hr, pad;
+  double idf;
+};
+struct QPos {
+  int64_t q0;
+  int32_t q, nt;
+};
+static_assert(sizeof(QDesc) == 32 && sizeof(QPos) == 16, "record sizes");
+__global__ void k_query_desc(const int32_t *terms, int64_t n, int64_t V, const int64_t *off, const double *idf,
+                             const int32_t *row_of, const int32_t *hrow_of, QDesc *out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t t = terms[i];
+    QDesc d{0, 0, 0, -1, 0, 0.0};
+    if (t >= 0 && t < V) {
+      d.mb = off[t];
+      d.mdf = (int32_t)(off[t + 1] - d.mb);
+      d.brow = row_of[t];
+      d.hr = (hrow_of && d.mdf > 0) ? hrow_of[t] : -1;
+      d.idf = idf[t];
+    }
+    out[i] = d;
+  }
+}
+__global__ void k_query_pos(const int32_t *qorder, const int64_t *qoff, int nq, QPos *out) {
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < nq; p += gridDim.x * blockDim.x) {
+    const int q = qorder ? qorder[p] : p;
+    out[p] = QPos{qoff[q], q, (int32_t)(qoff[q + 1] - qoff[q])};
+  }
+}
+__device__ __forceinline__ QDesc ld_desc(const QDesc *d, int64_t q0, int nt, int lane) {
+  if (lane < nt) return d[q0 + lane];
+  return QDesc{0, 0, 0, -1, 0, 0.0};
+}
+
+// Bitonic sort of n (power of two) doubles of one wave's LDS array, descending.
+__device__ __forceinline__ void wave_sort_desc(double *s, int n) {
+  const int lane = threadIdx.x & 63;
+  for (int size = 2; size <= n; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < (n >> 1); i += 64) {
+        const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1)), hi = lo + stride;
+        const double a = s[lo], b = s[hi];
+        if ((lo & size) == 0 ? b > a : a > b) {
+          s[lo] = b;
+          s[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+}
+
 struct QSeedArgs {
-  const int64_t *off;
+  const QDesc *desc;
+  const int64_t *qoff;
   const int32_t *docno_o, *tf_o;  // reduce order: tf desc, docno asc
-  const double *lut, *idf;
-  int64_t V;
-  const int32_t *hrow_of;         // term -> heavy row or -1 (nullptr: none)
+  const double *lut;
   const uint8_t *tfrow;           // [H][hstride] tf bytes at docno - dmin
   int64_t hstride, dmin;
-  const int32_t *terms;
-  const int64_t *qoff;
   int nq, k, M;
   double *th0;
+  uint64_t *thk;  // key part of the threshold: kNoKey (every key passes at th0)
 };
 
 __global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
-  __shared__ int32_t hk[kSeedSlots];                // docno (INT32_MIN empty: never a docno)
-  __shared__ unsigned long long hs[kSeedSlots];     // best S' bits (non-negative doubles order as u64)
+  __shared__ int32_t hk[kSeedSlots];             // docno (INT32_MIN empty: never a docno)
+  __shared__ unsigned long long hs[kSeedSlots];  // best S' bits (non-negative doubles order as u64)
+  __shared__ int s_n;
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < a.nq; q += gridDim.x) {
     const int64_t q0 = a.qoff[q];
     const int nt = (int)(a.qoff[q + 1] - q0);
-    int64_t mb = 0;
-    int32_t mdf = 0, hr = -1;
-    double midf = 0.0;
-    if (lane < nt) {
-      const int32_t t = a.terms[q0 + lane];
-      if (t >= 0 && t < a.V) {
-        mb = a.off[t];
-        mdf = (int32_t)(a.off[t + 1] - mb);
-        midf = a.idf[t];
-        if (a.hrow_of && mdf > 0) hr = a.hrow_of[t];
-      }
-    }
-    const uint64_t am = (uint64_t)__ballot(lane < nt && mdf > 0);
-    const uint64_t hm = (uint64_t)__ballot(hr >= 0 && mdf > 0);
+    const QDesc D = ld_desc(a.desc, q0, nt, lane);
+    const uint64_t am = (uint64_t)__ballot(D.mdf > 0);
+    const uint64_t hm = (uint64_t)__ballot(D.hr >= 0);
     for (int i = lane; i < kSeedSlots; i += 64) {
       hk[i] = INT32_MIN;
       hs[i] = 0ull;
     }
+    if (lane == 0) s_n = 0;
     __syncthreads();
     // seeds per term: M, so that every term's seeds fit the table at load <= 1/2
     const int na = __popcll(am);
     const int M = na > 0 ? min(a.M, (kSeedSlots / 2) / na) : 0;
     for (uint64_t mj = am; mj; mj &= mj - 1) {
       const int j = (int)__builtin_ctzll(mj);
-      const int64_t b = rl64(mb, j);
-      const int32_t n = min(M, __builtin_amdgcn_readlane(mdf, j));
+      const int64_t b = rl64(D.mb, j);
+      const int32_t n = min(M, __builtin_amdgcn_readlane(D.mdf, j));
       for (int32_t i0 = 0; i0 < n; i0 += 64) {
         const int32_t i = i0 + lane;
         if (i >= n) continue;
@@ -1052,8 +1110,8 @@ __global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
           int f = 0;
           if (x == j) f = fj;
           else if ((hm >> x) & 1)
-            f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(hr, x) * a.hstride + ((int64_t)d - a.dmin)];
-          if (f != 0) S = __dadd_rn(S, __dmul_rn(a.lut[f], rld(midf, x)));
+            f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, x) * a.hstride + ((int64_t)d - a.dmin)];
+          if (f != 0) S = __dadd_rn(S, __dmul_rn(a.lut[f], rld(D.idf, x)));
         }
         uint32_t h = qhash32((uint32_t)d) & (kSeedSlots - 1);
         for (;;) {
@@ -1065,134 +1123,132 @@ __global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
       }
     }
     __syncthreads();
-    // k-th largest S' over the distinct seeds: compact, then a bitonic sort
-    __shared__ double ss[kSeedSlots];
-    __shared__ uint64_t sk_[kSeedSlots];
-    __shared__ int s_n;
-    if (lane == 0) s_n = 0;
+    // k-th largest S' over the distinct seeds: compact the used slots' scores
+    // (read into registers first, then written over the table), sort, pick
+    double v[kSeedSlots / 64];
+#pragma unroll
+    for (int u = 0; u < kSeedSlots / 64; u++) {
+      const int i = u * 64 + lane;
+      v[u] = hk[i] != INT32_MIN ? __longlong_as_double((long long)hs[i]) : -1.0;
+    }
     __syncthreads();
-    for (int i = lane; i < kSeedSlots; i += 64)
-      if (hk[i] != INT32_MIN) {
-        const int p = atomicAdd(&s_n, 1);
-        ss[p] = __longlong_as_double((long long)hs[i]);
-        sk_[p] = (uint64_t)(uint32_t)hk[i];
-      }
+    double *ss = reinterpret_cast<double *>(hs);
+#pragma unroll
+    for (int u = 0; u < kSeedSlots / 64; u++)
+      if (v[u] >= 0.0) ss[atomicAdd(&s_n, 1)] = v[u];
     __syncthreads();
     const int n = s_n;
     double th = -1.0;
     if (n >= a.k) {
       int n2 = 2;
       while (n2 < n) n2 <<= 1;
-      for (int i = n + lane; i < n2; i += 64) {
-        ss[i] = -INFINITY;
-        sk_[i] = kNoKey;
-      }
+      for (int i = n + lane; i < n2; i += 64) ss[i] = -INFINITY;
       __syncthreads();
-      wave_sort(ss, sk_, n2);
+      wave_sort_desc(ss, n2);
       th = ss[a.k - 1];
     }
-    if (lane == 0) a.th0[q] = th;
+    if (lane == 0) {
+      a.th0[q] = th;
+      a.thk[q] = kNoKey;
+    }
     __syncthreads();
   }
 }
 
 struct QWinArgs {
-  const int64_t *off;
+  const QDesc *desc;
+  const QPos *qpos;
   const int32_t *docno, *tf;   // docno-order CSR
-  const double *lut, *idf;
-  int64_t V;
-  const int32_t *row_of, *sk;  // batch rows, skip table [rows][T + 1]
+  const double *lut;
+  int max_tf;
+  const int32_t *skt;          // window skip table, transposed [nwin + 1][nrows]
+  int64_t nrows;
   const uint8_t *qlut;         // impact tables [rows][256]
-  const int32_t *hrow_of;      // nullptr: no heavy rows
   const uint8_t *imp, *tfrow;  // [H][hstride] impact / tf bytes
+  const uint8_t *bmq;          // [H][hstride / 16] impact bound of every 16-document block
   int64_t hstride, dmin, T, nwin;
-  const int32_t *terms;
-  const int64_t *qoff;
-  const int32_t *qorder;
+  const int32_t *wlist;        // windows of this launch (nullptr: 0 .. nwin - 1), nw of them
+  int64_t nw;
   int nq, nslices, reftie, cap;
   double alpha;
-  const double *th0;
+  const double *th0;           // per query threshold: keep (S, key) not worse than (th0, thk)
+  const uint64_t *thk;
   unsigned int *ccnt;          // candidates per query
   double *cs;                  // [nq][cap] scores
   uint64_t *ck;                // [nq][cap] doc keys
+  unsigned long long *stats;   // SME_EXPERIMENTS builds only (else nullptr)
+  int exper;                   // SME_EXPERIMENTS timing switches (0 in the product)
 };
 
 __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
   __shared__ uint32_t lacc_all[kWNT / 64][kWin / 2];  // sparse impact sums, u16 pairs (see below)
   __shared__ uint32_t slist_all[kWNT / 64][kSList];   // the window's sparse postings: r | tf << 12
+  __shared__ uint32_t lblk_all[kWNT / 64][kWin / 16];  // sparse impact sums per 16-document block
+  __shared__ uint16_t blist_all[kWNT / 64][kWin / 16];  // blocks over the gate
+  __shared__ uint16_t clist_all[kWNT / 64][kCList];     // documents over the gate
+  __shared__ double s_lut[kLutLds];                    // 1 + ln(tf) for tf < 256
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t *lacc = lacc_all[wv], *slist = slist_all[wv];
+  uint32_t *lacc = lacc_all[wv], *slist = slist_all[wv], *lblk = lblk_all[wv];
+  uint16_t *blist = blist_all[wv], *clist = clist_all[wv];
+  for (int i = threadIdx.x; i < kLutLds; i += kWNT) s_lut[i] = i <= a.max_tf ? a.lut[i] : 0.0;
+  __syncthreads();
   // workgroup -> (window, query slice): the 8 XCDs (b % 8) on 8 windows, every
   // slice of one window on one XCD
   const int64_t G = 8 * (int64_t)a.nslices;
   const int64_t b = blockIdx.x, w = b % G;
-  const int64_t x = (b / G) * 8 + (w & 7);
-  if (x >= a.nwin) return;
+  const int64_t xi = (b / G) * 8 + (w & 7);
+  if (xi >= a.nw) return;
+  const int64_t x = a.wlist ? a.wlist[xi] : xi;
   const int s = (int)(w >> 3);
   const int p_lo = (int)((int64_t)a.nq * s / a.nslices), p_hi = (int)((int64_t)a.nq * (s + 1) / a.nslices);
-  const int64_t wbase = a.dmin + (x << kWinB);    // first docno of the window
-  const int64_t hoff = (x << kWinB) + (int64_t)kWDL * lane;  // this lane's bytes in a heavy row
-  for (int pos = p_lo + wv; pos < p_hi; pos += kWNT / 64) {
-    const int q = a.qorder ? a.qorder[pos] : pos;
-    const int64_t q0 = a.qoff[q];
-    const int nt = (int)(a.qoff[q + 1] - q0);  // <= 64 (host checked)
-    int64_t mb = 0;
-    int32_t mdf = 0, brow = 0, hr = -1;
-    double midf = 0.0;
-    if (lane < nt) {
-      const int32_t t = a.terms[q0 + lane];
-      if (t >= 0 && t < a.V) {
-        mb = a.off[t];
-        mdf = (int32_t)(a.off[t + 1] - mb);
-        midf = a.idf[t];
-        brow = a.row_of[t];
-        if (a.hrow_of && mdf > 0) hr = a.hrow_of[t];
-      }
-    }
-    const uint64_t hm = (uint64_t)__ballot(hr >= 0);
-    const uint64_t sm = (uint64_t)__ballot(lane < nt && mdf > 0 && hr < 0);
-    if ((hm | sm) == 0) continue;
-    const double th0 = a.th0[q];
+  const int64_t wbase = a.dmin + (x << kWinB);  // first docno of the window
+  int pos = p_lo + wv;
+  if (pos >= p_hi) return;
+  // software pipeline over this wave's queries: the next query's position
+  // record, term records, threshold and skip entries load while this one runs
+  QPos P = a.qpos[pos];
+  QDesc D = ld_desc(a.desc, P.q0, P.nt, lane);
+  double th0 = a.th0[P.q];
+  uint64_t thk = a.thk[P.q];
+  int32_t mc = 0, me = 0;
+  if (D.mdf > 0 && D.hr < 0) {
+    mc = a.skt[x * a.nrows + D.brow];
+    me = a.skt[(x + 1) * a.nrows + D.brow];
+  }
+  for (;;) {
+    const int npos = pos + kWNT / 64;
+    const bool hasn = npos < p_hi;
+    QPos NP{0, 0, 0};
+    if (hasn) NP = a.qpos[npos];
+    const uint64_t hm = (uint64_t)__ballot(D.hr >= 0);
+    const uint64_t sm = (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
     const uint32_t gate = gate_of(th0, a.alpha);
-    // sparse terms: postings of the window (skip table at 1024-doc tiles)
-    int32_t mc = 0, me = 0;
-    if ((sm >> lane) & 1) {
-      const int32_t *row = a.sk + (int64_t)brow * (a.T + 1);
-      mc = row[x << 2];
-      me = row[(x << 2) + 4];
-    }
-    // heavy terms: impact bytes of this lane's 64 documents, four terms' loads in flight
-    uint32_t acc[kWDL / 2];  // acc[m]: documents 2m (low u16), 2m + 1 (high) of the lane
+    // heavy terms' block maxima: one dword per term = the impact bound of this
+    // lane's four 16-document blocks (index-resident bmq rows), all loads in flight
+    uint32_t ub0 = 0, ub1 = 0;  // blocks 4 lane + {0, 1} | {2, 3} as u16 pairs
+    {
+      const int64_t boff = (x << (kWinB - 4)) + 4 * lane;
+      for (uint64_t mh = hm; mh;) {
+        uint32_t wq[4];
 #pragma unroll
-    for (int m = 0; m < kWDL / 2; m++) acc[m] = 0;
-    for (uint64_t mh = hm; mh;) {
-      uint4 v[4][4];
-#pragma unroll
-      for (int g = 0; g < 4; g++) {
-        if (mh) {
-          const int j = (int)__builtin_ctzll(mh);
-          mh &= mh - 1;
-          const uint4 *p = reinterpret_cast<const uint4 *>(
-              a.imp + (int64_t)__builtin_amdgcn_readlane(hr, j) * a.hstride + hoff);
-#pragma unroll
-          for (int c = 0; c < 4; c++) v[g][c] = p[c];
-        } else {
-#pragma unroll
-          for (int c = 0; c < 4; c++) v[g][c] = make_uint4(0, 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < 4; g++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          const uint32_t w4[4] = {v[g][c].x, v[g][c].y, v[g][c].z, v[g][c].w};
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            acc[8 * c + 2 * u] += __builtin_amdgcn_perm(0u, w4[u], 0x0C010C00u);
-            acc[8 * c + 2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
+        for (int g = 0; g < 4; g++) {
+          wq[g] = 0;
+          if (mh) {
+            const int j = (int)__builtin_ctzll(mh);
+            mh &= mh - 1;
+            wq[g] = *reinterpret_cast<const uint32_t *>(
+                a.bmq + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * (a.hstride >> 4) + boff);
           }
         }
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          ub0 += __builtin_amdgcn_perm(0u, wq[g], 0x0C010C00u);
+          ub1 += __builtin_amdgcn_perm(0u, wq[g], 0x0C030C02u);
+        }
+      }
     }
+    // sparse terms: the window's postings into LDS -- impact sums per document
+    // and per block, and the (document, tf) list for exact lookups
     const int32_t cj = ((sm >> lane) & 1) ? me - mc : 0;
     const int32_t incl = wave_incl_sum(cj), prej = incl - cj;
     const int32_t total = __shfl(incl, 63, 64);
@@ -1202,8 +1258,10 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
       // 32 words are a conflict-free column
 #pragma unroll
       for (int m = 0; m < kWDL / 2; m++) lacc[m * 64 + lane] = 0;
+#pragma unroll
+      for (int m = 0; m < 4; m++) lblk[m * 64 + lane] = 0;
       qwave_sync();
-      const int64_t plo = mb + mc;
+      const int64_t plo = D.mb + mc;
       for (int32_t e0 = 0; e0 < total; e0 += 64) {
         const int32_t e = e0 + lane;
         int64_t pb = 0;
@@ -1214,8 +1272,8 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
           const int32_t pj = __builtin_amdgcn_readlane(prej, j);
           if (e >= pj) {
             pb = rl64(plo, j) - pj;
-            wj = rld(midf, j);
-            rj = __builtin_amdgcn_readlane(brow, j);
+            wj = rld(D.idf, j);
+            rj = __builtin_amdgcn_readlane(D.brow, j);
           }
         }
         if (e < total) {
@@ -1223,129 +1281,278 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
           const int r = (int)((int64_t)d - wbase);
           const uint32_t qv = f <= 255 ? (uint32_t)a.qlut[(int64_t)rj * 256 + f] : impact(a.lut[f], wj, a.alpha);
           atomicAdd(&lacc[((r & 63) >> 1) * 64 + (r >> 6)], qv << ((r & 1) << 4));
+          // block b = r >> 4 of lane b >> 2: lblk[(b & 3) * 64 + (b >> 2)]
+          atomicAdd(&lblk[((r >> 4) & 3) * 64 + (r >> 6)], qv);
           if (listed) slist[e] = (uint32_t)r | ((uint32_t)min(f, 0xFFFFF) << 12);
         }
       }
       qwave_sync();
-#pragma unroll
-      for (int m = 0; m < kWDL / 2; m++) acc[m] += lacc[m * 64 + lane];
     }
-    // documents over the gate
-    uint64_t cm = 0;
-#pragma unroll
-    for (int m = 0; m < kWDL / 2; m++) {
-      if ((acc[m] & 0xFFFFu) >= gate) cm |= 1ull << (2 * m);
-      if ((acc[m] >> 16) >= gate) cm |= 1ull << (2 * m + 1);
+    // next query's term records and threshold (in flight during the block phase)
+    QDesc ND{0, 0, 0, -1, 0, 0.0};
+    double nth0 = 0.0;
+    uint64_t nthk = kNoKey;
+    if (hasn) {
+      ND = ld_desc(a.desc, NP.q0, NP.nt, lane);
+      nth0 = a.th0[NP.q];
+      nthk = a.thk[NP.q];
     }
-    const uint64_t amask = hm | sm;
-    for (;;) {
-      const bool have = cm != 0;
-      if (__ballot(have) == 0) break;  // wave-uniform
-      double S = 0.0;
-      uint64_t key = kNoKey;
-      bool keep = false;
-      if (have) {
-        const int bb = (int)__builtin_ctzll(cm);
-        cm &= cm - 1;
-        const int r = kWDL * lane + bb;
-        const int32_t d = (int32_t)(wbase + r);
-        uint32_t tie = 0xFFFFFFFFu;
-        for (uint64_t m = amask; m; m &= m - 1) {
-          const int j = (int)__builtin_ctzll(m);
-          int f = 0;
-          if ((hm >> j) & 1) {
-            f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(hr, j) * a.hstride + (x << kWinB) + r];
-          } else if (listed) {
-            int lo = __builtin_amdgcn_readlane(prej, j), hi = lo + __builtin_amdgcn_readlane(cj, j);
-            while (lo < hi) {  // the term's entries are docno-ascending
-              const int mid = (lo + hi) >> 1;
-              if ((int)(slist[mid] & 0xFFFu) < r) lo = mid + 1;
-              else hi = mid;
+    // blocks over the gate: heavy maxima + the block's sparse impact sum
+    uint32_t ub[4] = {ub0 & 0xFFFFu, ub0 >> 16, ub1 & 0xFFFFu, ub1 >> 16};
+    if (total > 0) {
+#pragma unroll
+      for (int m = 0; m < 4; m++) ub[m] += lblk[m * 64 + lane];
+    }
+    uint32_t bm = 0;
+#pragma unroll
+    for (int m = 0; m < 4; m++) bm |= (ub[m] >= gate ? 1u : 0u) << m;
+    const int32_t bl = __popc(bm);
+    const int32_t bincl = wave_incl_sum(bl);
+    const int32_t nblk = __shfl(bincl, 63, 64);
+    if (a.stats && lane == 0) {
+      atomicAdd(a.stats + 0, 1ull);
+      atomicAdd(a.stats + 1, (unsigned long long)total);
+      atomicAdd(a.stats + 2, (unsigned long long)nblk);
+      atomicAdd(a.stats + 3, (unsigned long long)__popcll(hm));
+    }
+    if (nblk > 0 && !(a.exper & 1)) {
+      qwave_sync();
+      {
+        int32_t o = bincl - bl;
+        for (uint32_t m = bm; m; m &= m - 1) blist[o++] = (uint16_t)(4 * lane + __builtin_ctz(m));
+      }
+      qwave_sync();
+      const uint64_t amask = hm | sm;
+      // one passing block per lane: exact A(d) of its 16 documents
+      for (int32_t b0 = 0; b0 < nblk; b0 += 64) {
+        const bool hb = b0 + lane < nblk;
+        const int blk = hb ? (int)blist[b0 + lane] : 0;
+        const int r0 = blk << 4;  // first document of the block in the window
+        uint32_t acc[8];          // documents r0 + 2m (low u16), + 1 (high)
+        if (total > 0) {
+          // documents r0 .. r0 + 15 = lane blk >> 2, words m = 8 (blk & 3) + i
+#pragma unroll
+          for (int i = 0; i < 8; i++) acc[i] = hb ? lacc[(8 * (blk & 3) + i) * 64 + (blk >> 2)] : 0u;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; i++) acc[i] = 0;
+        }
+        for (uint64_t mh = hm; mh;) {
+          uint4 v[4];
+#pragma unroll
+          for (int g = 0; g < 4; g++) {
+            v[g] = make_uint4(0, 0, 0, 0);
+            if (mh) {
+              const int j = (int)__builtin_ctzll(mh);
+              mh &= mh - 1;
+              if (hb)
+                v[g] = *reinterpret_cast<const uint4 *>(a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride +
+                                                       (x << kWinB) + r0);
             }
-            if (lo < __builtin_amdgcn_readlane(prej, j) + __builtin_amdgcn_readlane(cj, j) &&
-                (int)(slist[lo] & 0xFFFu) == r) {
-              f = (int)(slist[lo] >> 12);
-              if (f == 0xFFFFF) f = -1;  // tf >= 2^20: read it from the postings
-            }
-          } else {
-            f = -1;
           }
-          if (f < 0) {  // global binary search over the term's postings in the window
-            const int64_t base = rl64(mb, j);
-            int64_t lo = base + __builtin_amdgcn_readlane(mc, j);
-            const int64_t e = base + __builtin_amdgcn_readlane(me, j);
-            int64_t hi = e;
-            while (lo < hi) {
-              const int64_t mid = (lo + hi) >> 1;
-              if (a.docno[mid] < d) lo = mid + 1;
-              else hi = mid;
+#pragma unroll
+          for (int g = 0; g < 4; g++) {
+            const uint32_t w4[4] = {v[g].x, v[g].y, v[g].z, v[g].w};
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+              acc[2 * u] += __builtin_amdgcn_perm(0u, w4[u], 0x0C010C00u);
+              acc[2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
             }
-            f = (lo < e && a.docno[lo] == d) ? a.tf[lo] : 0;
-          }
-          if (f != 0) {
-            S = __dadd_rn(S, __dmul_rn(a.lut[f], rld(midf, j)));
-            if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f);
           }
         }
-        key = doc_key(a.reftie ? tie : 0u, d);
-        keep = S >= th0;  // th0 < 0 (no seed): every touched document
-      }
-      const uint64_t km = (uint64_t)__ballot(keep);
-      if (km) {
-        unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(&a.ccnt[q], (unsigned int)__popcll(km));
-        base = (unsigned int)__shfl((int)base, 0, 64);
-        if (keep) {
-          const unsigned int idx = base + lane_prefix(km);
-          if (idx < (unsigned int)a.cap) {
-            a.cs[(int64_t)q * a.cap + idx] = S;
-            a.ck[(int64_t)q * a.cap + idx] = key;
+        uint32_t cm = 0;  // documents of the block over the gate
+        if (hb) {
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            if ((acc[i] & 0xFFFFu) >= gate) cm |= 1u << (2 * i);
+            if ((acc[i] >> 16) >= gate) cm |= 1u << (2 * i + 1);
+          }
+        }
+        // candidates listed in LDS, scored one per lane
+        const int32_t cl = __popc(cm);
+        const int32_t cincl = wave_incl_sum(cl);
+        const int32_t ncand = (a.exper & 2) ? 0 : __shfl(cincl, 63, 64);
+        if (a.stats && lane == 0) atomicAdd(a.stats + 4, (unsigned long long)ncand);
+        for (int32_t k0 = 0; k0 < ncand; k0 += kCList) {
+          const int32_t kn = min(ncand - k0, kCList);
+          qwave_sync();
+          {
+            int32_t o = cincl - cl - k0;
+            for (uint32_t m = cm; m; m &= m - 1, o++)
+              if (o >= 0 && o < kn) clist[o] = (uint16_t)(r0 + __builtin_ctz(m));
+          }
+          qwave_sync();
+          for (int32_t c0 = 0; c0 < kn; c0 += 64) {
+            double S = 0.0;
+            uint64_t key = kNoKey;
+            bool keep = false;
+            if (c0 + lane < kn) {
+              const int r = (int)clist[c0 + lane];
+              const int32_t d = (int32_t)(wbase + r);
+              uint32_t tie = 0xFFFFFFFFu;
+              for (uint64_t m = amask; m; m &= m - 1) {
+                const int j = (int)__builtin_ctzll(m);
+                int f = 0;
+                if ((hm >> j) & 1) {
+                  f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
+                } else if (listed) {
+                  const int lo0 = __builtin_amdgcn_readlane(prej, j), hi0 = lo0 + __builtin_amdgcn_readlane(cj, j);
+                  int lo = lo0, hi = hi0;
+                  while (lo < hi) {  // the term's entries are docno-ascending
+                    const int mid = (lo + hi) >> 1;
+                    if ((int)(slist[mid] & 0xFFFu) < r) lo = mid + 1;
+                    else hi = mid;
+                  }
+                  if (lo < hi0 && (int)(slist[lo] & 0xFFFu) == r) {
+                    f = (int)(slist[lo] >> 12);
+                    if (f == 0xFFFFF) f = -1;  // tf >= 2^20: read it from the postings
+                  }
+                } else {
+                  f = -1;
+                }
+                if (f < 0) {  // global binary search over the term's postings in the window
+                  const int64_t base = rl64(D.mb, j);
+                  int64_t lo = base + __builtin_amdgcn_readlane(mc, j);
+                  const int64_t e = base + __builtin_amdgcn_readlane(me, j);
+                  int64_t hi = e;
+                  while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (a.docno[mid] < d) lo = mid + 1;
+                    else hi = mid;
+                  }
+                  f = (lo < e && a.docno[lo] == d) ? a.tf[lo] : 0;
+                }
+                if (f != 0) {
+                  S = __dadd_rn(S, __dmul_rn(f < kLutLds ? s_lut[f] : a.lut[f], rld(D.idf, j)));
+                  if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f);
+                }
+              }
+              key = doc_key(a.reftie ? tie : 0u, d);
+              keep = S > th0 || (S == th0 && key <= thk);  // th0 < 0 (no seed): every touched document
+            }
+            const uint64_t km = (uint64_t)__ballot(keep);
+            if (a.stats && lane == 0) atomicAdd(a.stats + 5, (unsigned long long)__popcll(km));
+            if (km) {
+              unsigned int base = 0;
+              if (lane == 0) base = atomicAdd(&a.ccnt[P.q], (unsigned int)__popcll(km));
+              base = (unsigned int)__shfl((int)base, 0, 64);
+              if (keep) {
+                const unsigned int idx = base + lane_prefix(km);
+                if (idx < (unsigned int)a.cap) {
+                  a.cs[(int64_t)P.q * a.cap + idx] = S;
+                  a.ck[(int64_t)P.q * a.cap + idx] = key;
+                }
+              }
+            }
           }
         }
       }
     }
-    qwave_sync();  // this wave's LDS is rewritten by its next query
+    if (!hasn) break;
+    // next query's skip entries, then rotate the pipeline
+    int32_t nmc = 0, nme = 0;
+    if (ND.mdf > 0 && ND.hr < 0) {
+      nmc = a.skt[x * a.nrows + ND.brow];
+      nme = a.skt[(x + 1) * a.nrows + ND.brow];
+    }
+    qwave_sync();  // this wave's LDS is rewritten for the next query
+    pos = npos;
+    P = NP;
+    D = ND;
+    th0 = nth0;
+    thk = nthk;
+    mc = nmc;
+    me = nme;
   }
 }
 
 struct QFinalArgs {
-  int nq, k, cap;
+  const int32_t *qlist;       // queries of this round (nullptr: 0 .. n-1)
+  int n, k, cap;
   const unsigned int *ccnt;
   const double *cs;
   const uint64_t *ck;
   int32_t *out_d;
   double *out_s;
   uint32_t *out_t;
+  double *th_s;               // overflowed queries: raised threshold for the next round
+  uint64_t *th_k;
   int32_t *ovf;               // queries whose list overflowed
   unsigned int *novf;
 };
 
+// Per query: sort the candidates (score desc, key asc) and emit the best k.  A
+// list that overflowed holds `cap` arbitrary candidates -- real documents with
+// exact scores -- so the k-th best of them, B, is a valid bound: every document
+// of the true top k is at least as good as B.  It becomes the query's threshold
+// (score and key) for the next round, which keeps only documents not worse
+// than B (deep exact ties at the score are cut by key).
 __global__ __launch_bounds__(64) void k_query_final(QFinalArgs a) {
   __shared__ double bs[kCandMax];
   __shared__ uint64_t bk[kCandMax];
   const int lane = threadIdx.x;
-  for (int q = blockIdx.x; q < a.nq; q += gridDim.x) {
+  for (int i = blockIdx.x; i < a.n; i += gridDim.x) {
+    const int q = a.qlist ? a.qlist[i] : i;
     const unsigned int c = a.ccnt[q];
-    if (c > (unsigned int)a.cap) {
+    const bool over = c > (unsigned int)a.cap;
+    if (over && a.cap < a.k) {  // too few to bound anything: straight to the fallback
       if (lane == 0) a.ovf[atomicAdd(a.novf, 1u)] = q;
       continue;
     }
-    const int n = (int)c;
+    const int n = over ? a.cap : (int)c;
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
-    for (int i = lane; i < n2; i += 64) {
-      bs[i] = i < n ? a.cs[(int64_t)q * a.cap + i] : -INFINITY;
-      bk[i] = i < n ? a.ck[(int64_t)q * a.cap + i] : kNoKey;
+    for (int j = lane; j < n2; j += 64) {
+      bs[j] = j < n ? a.cs[(int64_t)q * a.cap + j] : -INFINITY;
+      bk[j] = j < n ? a.ck[(int64_t)q * a.cap + j] : kNoKey;
     }
     __syncthreads();
     wave_sort(bs, bk, n2);
-    for (int r = lane; r < a.k; r += 64) {
-      a.out_d[(int64_t)q * a.k + r] = r < n ? key_doc(bk[r]) : -1;
-      a.out_s[(int64_t)q * a.k + r] = r < n ? bs[r] : 0.0;
-      if (a.out_t) a.out_t[(int64_t)q * a.k + r] = r < n ? (uint32_t)(bk[r] >> 32) : 0xFFFFFFFFu;
+    if (over) {
+      if (lane == 0) {
+        a.th_s[q] = bs[a.k - 1];
+        a.th_k[q] = bk[a.k - 1];
+        a.ovf[atomicAdd(a.novf, 1u)] = q;
+      }
+    } else {
+      for (int r = lane; r < a.k; r += 64) {
+        a.out_d[(int64_t)q * a.k + r] = r < n ? key_doc(bk[r]) : -1;
+        a.out_s[(int64_t)q * a.k + r] = r < n ? bs[r] : 0.0;
+        if (a.out_t) a.out_t[(int64_t)q * a.k + r] = r < n ? (uint32_t)(bk[r] >> 32) : 0xFFFFFFFFu;
+      }
     }
     __syncthreads();
   }
+}
+// After the sample windows: every query's k-th best candidate so far (stored
+// entries, all real documents with exact scores) bounds its k-th best score
+// from below; if it beats the seed threshold it replaces it, so the remaining
+// windows keep far fewer documents.
+__global__ __launch_bounds__(64) void k_query_raise(int nq, int k, int cap, const unsigned int *ccnt, const double *cs,
+                                                    const uint64_t *ck, double *th_s, uint64_t *th_k) {
+  __shared__ double bs[kCandMax];
+  __shared__ uint64_t bk[kCandMax];
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+    const int n = (int)min(ccnt[q], (unsigned int)cap);
+    if (n < k) continue;
+    int n2 = 2;
+    while (n2 < n) n2 <<= 1;
+    for (int j = lane; j < n2; j += 64) {
+      bs[j] = j < n ? cs[(int64_t)q * cap + j] : -INFINITY;
+      bk[j] = j < n ? ck[(int64_t)q * cap + j] : kNoKey;
+    }
+    __syncthreads();
+    wave_sort(bs, bk, n2);
+    if (lane == 0 && better(bs[k - 1], bk[k - 1], th_s[q], th_k[q])) {
+      th_s[q] = bs[k - 1];
+      th_k[q] = bk[k - 1];
+    }
+    __syncthreads();
+  }
+}
+__global__ void k_reset_cnt(const int32_t *qlist, int n, unsigned int *ccnt) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) ccnt[qlist[i]] = 0;
 }
 
 // impact rows from tf rows: q(tf) = floor(lut[tf] * idf * alpha) + 1 (0 for tf = 0)
@@ -1371,6 +1578,32 @@ __global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const i
       o[u] = (uint32_t)ql[w4[u] & 0xFF] | ((uint32_t)ql[(w4[u] >> 8) & 0xFF] << 8) |
              ((uint32_t)ql[(w4[u] >> 16) & 0xFF] << 16) | ((uint32_t)ql[w4[u] >> 24] << 24);
     dst[threadIdx.x] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+// impact bound rows of the 16-document blocks: q(block's largest tf) (q is
+// monotone in tf, so this is the largest impact in the block); one workgroup per row
+__global__ __launch_bounds__(256) void k_heavy_bmq(const uint8_t *bm16, const int32_t *hterm, int64_t H, int64_t stride,
+                                                   const double *lut, int max_tf, const double *idf, double alpha,
+                                                   uint8_t *bmq) {
+  __shared__ uint8_t ql[256];
+  for (int64_t row = blockIdx.x; row < H; row += gridDim.x) {
+    const double wi = idf[hterm[row]];
+    __syncthreads();
+    const int f = threadIdx.x;
+    ql[f] = (uint8_t)(f == 0 ? 0u : f <= max_tf ? impact(lut[f], wi, alpha) : 255u);
+    __syncthreads();
+    const uint4 *src = reinterpret_cast<const uint4 *>(bm16 + row * stride);
+    uint4 *dst = reinterpret_cast<uint4 *>(bmq + row * stride);
+    for (int64_t i = threadIdx.x; i < (stride >> 4); i += blockDim.x) {
+      const uint4 v = src[i];
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        o[u] = (uint32_t)ql[w4[u] & 0xFF] | ((uint32_t)ql[(w4[u] >> 8) & 0xFF] << 8) |
+               ((uint32_t)ql[(w4[u] >> 16) & 0xFF] << 16) | ((uint32_t)ql[w4[u] >> 24] << 24);
+      dst[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
   }
 }
 // largest weight of any term (its max tf is the first posting of the
@@ -1443,7 +1676,7 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     // memory budget for the rows: 1/8 of the device's free memory, at most 16 GB
     size_t fr = 0, tot = 0;
     SME_HIP(hipMemGetInfo(&fr, &tot));
-    const double per_row = 2.0 * (double)stride + (double)(T << 6) + (double)T;
+    const double per_row = 2.0 * (double)stride + 2.0 * (double)(T << 6) + (double)T;
     const int64_t cap = (int64_t)(std::min<double>((double)fr / 8.0, 16e9) / per_row);
     const int64_t H = std::min<int64_t>(nh, cap);
     int32_t *hrow_of = ix->d_hrow_of.as<int32_t>(V);
@@ -1455,8 +1688,9 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
       SME_HIP(hipMemsetAsync(hdf + H, 0, sizeof(int64_t), st));
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, hdf, hpre, (int)H + 1, st));
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, hdf, hpre, (int)H + 1, st));
-      uint8_t *buf = ix->d_heavy.as<uint8_t>((size_t)H * (size_t)per_row + 64);
+      uint8_t *buf = ix->d_heavy.as<uint8_t>((size_t)H * (size_t)per_row + 128);
       uint8_t *tfrow = buf, *imp = buf + H * stride, *bm16 = imp + H * stride, *bm1k = bm16 + H * (T << 6);
+      uint8_t *bmq = bm1k + H * T + 64 - ((H * T) & 15);  // 16-byte aligned
       SME_HIP(hipMemsetAsync(tfrow, 0, (size_t)(H * stride), st));
       hipLaunchKernelGGL(k_heavy_fill, dim3(16384), dim3(256), 0, st, hpre, H, hterm, off,
                          (const int32_t *)ix->d_docno_d.p, (const int32_t *)ix->d_tf_d.p, ix->dmin, stride, tfrow);
@@ -1468,8 +1702,11 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
       hipLaunchKernelGGL(k_heavy_imp, dim3((unsigned)std::min<int64_t>(H * (stride >> 12), 1 << 16)), dim3(256), 0, st,
                          tfrow, hterm, H, stride, (const double *)ix->d_lut.p, ix->max_tf,
                          (const double *)ix->d_idf.p, ix->q_alpha, imp);
+      hipLaunchKernelGGL(k_heavy_bmq, dim3((unsigned)std::min<int64_t>(H, 1 << 16)), dim3(256), 0, st, bm16, hterm, H,
+                         T << 6, (const double *)ix->d_lut.p, ix->max_tf, (const double *)ix->d_idf.p, ix->q_alpha, bmq);
       SME_CHECK_LAUNCH();
       ix->q_imp = imp;
+      ix->q_bmq = bmq;
       ix->q_tfrow = tfrow;
       ix->q_bm16 = bm16;
       ix->q_bm1k = bm1k;
@@ -1517,6 +1754,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   const int64_t T = tiled ? ix->q_T : 0;
   const int32_t *row_of = nullptr, *sk = nullptr;
   const uint8_t *qlut = nullptr;
+  int64_t nrows_b = 0;      // distinct batch terms (rows of the skip / impact tables)
+  int32_t *skt = nullptr;   // k_query_win: window skip table, transposed
   int h_mx = 0;
   if (tiled) {
     hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
@@ -1539,6 +1778,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       SME_HIP(hipMemcpyAsync(&nrows32, rowo + V, sizeof(int32_t), hipMemcpyDeviceToHost, st));
       SME_HIP(hipStreamSynchronize(st));
       const int64_t nrows = nrows32;
+      nrows_b = nrows;
       if ((double)nrows * (double)(T + 1) * 4.0 > 8.0e9) {
         tiled = false;
       } else {
@@ -1561,6 +1801,12 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           hipLaunchKernelGGL(k_skip_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T, skw);
           hipLaunchKernelGGL(k_skip_suffix, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 16384)), dim3(256), 0,
                              st, nrows, T, skw);
+          if (cx->opt_query_kernel == 0) {
+            const int64_t nwin = T >> 2, ne = nrows * (nwin + 1);
+            skt = W[31].as<int32_t>(ne);
+            hipLaunchKernelGGL(k_skip_win, dim3((unsigned)std::min<int64_t>((ne + 255) / 256, 65536)), dim3(256), 0,
+                               st, skw, nrows, T, nwin, skt);
+          }
           // impact scale: the index's (prepare_queries), shared by every batch
           SME_HIP(hipMemcpyAsync(wmax, &ix->q_wmax_bits, sizeof(uint64_t), hipMemcpyHostToDevice, st));
           hipLaunchKernelGGL(k_row_qlut, dim3((unsigned)std::min<int64_t>(nrows, 16384)), dim3(256), 0, st, tor, nrows,
@@ -1638,87 +1884,148 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   const bool win = tiled && cx->opt_query_kernel == 0;
   int64_t n_ovf = 0;
   if (win) {
+    // per-batch records: term descriptors (batch term order), position records (query order)
+    int64_t nterm = 0;
+    SME_HIP(hipMemcpyAsync(&nterm, d_qoff + nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    QDesc *qdesc = reinterpret_cast<QDesc *>(W[34].as<uint4>(2 * (size_t)std::max<int64_t>(nterm, 1)));
+    QPos *qpos = reinterpret_cast<QPos *>(W[33].as<uint4>((size_t)nq));
+    if (nterm > 0)
+      hipLaunchKernelGGL(k_query_desc, dim3((unsigned)std::min<int64_t>((nterm + 255) / 256, 8192)), dim3(256), 0, st,
+                         d_terms, nterm, V, off, idf, row_of, qa.hrow_of, qdesc);
+    hipLaunchKernelGGL(k_query_pos, dim3((unsigned)std::min((nq + 255) / 256, 8192)), dim3(256), 0, st, qord, d_qoff,
+                       nq, qpos);
+    SME_CHECK_LAUNCH();
+    SME_HIP(hipEventRecord(e0, st));
     // 1. seed thresholds
     double *th0 = W[41].as<double>(nq);
+    uint64_t *thk = W[32].as<uint64_t>(nq);
     QSeedArgs sa;
-    sa.off = off;
+    sa.desc = qdesc;
+    sa.qoff = d_qoff;
     sa.docno_o = (const int32_t *)ix->d_docno_o.p;
     sa.tf_o = (const int32_t *)ix->d_tf_o.p;
     sa.lut = lut;
-    sa.idf = idf;
-    sa.V = V;
-    sa.hrow_of = qa.hrow_of;
     sa.tfrow = ix->q_tfrow;
     sa.hstride = T << kQB;
     sa.dmin = ix->dmin;
-    sa.terms = d_terms;
-    sa.qoff = d_qoff;
     sa.nq = nq;
     sa.k = k;
     sa.M = (int)std::min<int64_t>(std::max<int64_t>(cx->opt_seed_m, cx->opt_seed_m > 0 ? 2 * (int64_t)k : 0),
                                   kSeedSlots / 2);
     sa.th0 = th0;
+    sa.thk = thk;
     hipLaunchKernelGGL(k_query_seed, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, sa);
     SME_CHECK_LAUNCH();
     SME_HIP(hipEventRecord(e1, st));
-    // 2. windows x query slices
+    // 2. windows x query slices; 3. per-query selection.  Overflowed lists run
+    // again with the raised threshold (at most kWinRounds rounds), the rest -> k_query_bm
     const int cap = (int)std::min<int64_t>(cx->opt_cand_cap, kCandMax);
     unsigned int *ccnt = W[42].as<unsigned int>(nq + 1);
     double *cs = W[43].as<double>((size_t)nq * cap);
     uint64_t *ckk = W[61].as<uint64_t>((size_t)nq * cap);
-    int32_t *ovf = W[62].as<int32_t>(nq + 2);
+    int32_t *ovf = W[62].as<int32_t>(2 * (size_t)nq + 2);
     unsigned int *novf = ccnt + nq;
     SME_HIP(hipMemsetAsync(ccnt, 0, (nq + 1) * sizeof(unsigned int), st));
     QWinArgs wa;
-    wa.off = off;
+    wa.desc = qdesc;
+    wa.qpos = qpos;
     wa.docno = dn;
     wa.tf = tf;
     wa.lut = lut;
-    wa.idf = idf;
-    wa.V = V;
-    wa.row_of = row_of;
-    wa.sk = sk;
+    wa.max_tf = ix->max_tf;
+    wa.skt = skt;
+    wa.nrows = nrows_b;
     wa.qlut = qlut;
-    wa.hrow_of = qa.hrow_of;
     wa.imp = ix->q_imp;
+    wa.bmq = ix->q_bmq;
     wa.tfrow = ix->q_tfrow;
     wa.hstride = T << kQB;
     wa.dmin = ix->dmin;
     wa.T = T;
     wa.nwin = T >> 2;
-    wa.terms = d_terms;
-    wa.qoff = d_qoff;
-    wa.qorder = qord;
-    wa.nq = nq;
-    wa.nslices = (int)std::max<int64_t>(1, std::min<int64_t>(nq / 512, 4096));
     wa.reftie = reftie;
     wa.cap = cap;
     wa.alpha = ix->q_alpha;
     wa.th0 = th0;
+    wa.thk = thk;
     wa.ccnt = ccnt;
     wa.cs = cs;
     wa.ck = ckk;
-    const int64_t G = 8 * (int64_t)wa.nslices;
-    const int64_t wg = ((wa.nwin + 7) / 8) * G;
-    if (wg >= (int64_t(1) << 31)) throw Error(SME_ELIMIT, "query batch x windows too large for one launch");
-    hipLaunchKernelGGL(k_query_win, dim3((unsigned)wg), dim3(kWNT), 0, st, wa);
-    SME_CHECK_LAUNCH();
-    SME_HIP(hipEventRecord(e2, st));
-    // 3. per-query selection; overflowed lists -> k_query_bm
-    QFinalArgs fa{nq, k, cap, ccnt, cs, ckk, d_out_docno, d_out_score, d_out_tie, ovf, novf};
-    hipLaunchKernelGGL(k_query_final, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, fa);
-    SME_CHECK_LAUNCH();
-    unsigned int h_novf = 0;
-    SME_HIP(hipMemcpyAsync(&h_novf, novf, sizeof h_novf, hipMemcpyDeviceToHost, st));
-    SME_HIP(hipStreamSynchronize(st));
-    n_ovf = h_novf;
-    if (n_ovf > 0) {
+    wa.stats = qstats;
+    wa.exper = 0;
+#ifdef SME_EXPERIMENTS
+    if (const char *qx = getenv("SME_QEXP")) wa.exper = atoi(qx);  // timing only: wrong results
+#endif
+    QFinalArgs fa{nullptr, nq, k, cap, ccnt, cs, ckk, d_out_docno, d_out_score, d_out_tie, th0, thk, ovf, novf};
+    int n_round = nq;
+    const int32_t *round_list = nullptr;
+    // window lists: every 8th window (sample), the rest
+    const int64_t nwin = wa.nwin;
+    int32_t *wl = W[30].as<int32_t>(nwin + 1);
+    int64_t n_samp = 0;
+    {
+      std::vector<int32_t> h((size_t)nwin);
+      for (int64_t xw = 0; xw < nwin; xw += 8) h[(size_t)n_samp++] = (int32_t)xw;
+      int64_t o = n_samp;
+      for (int64_t xw = 0; xw < nwin; xw++)
+        if (xw % 8) h[(size_t)o++] = (int32_t)xw;
+      SME_HIP(hipMemcpyAsync(wl, h.data(), nwin * sizeof(int32_t), hipMemcpyHostToDevice, st));
+      SME_HIP(hipStreamSynchronize(st));
+    }
+    auto launch_win = [&](const int32_t *wlist, int64_t nw) {
+      wa.wlist = wlist;
+      wa.nw = nw;
+      const int64_t G = 8 * (int64_t)wa.nslices;
+      const int64_t wg = ((nw + 7) / 8) * G;
+      if (wg >= (int64_t(1) << 31)) throw Error(SME_ELIMIT, "query batch x windows too large for one launch");
+      if (wg > 0) hipLaunchKernelGGL(k_query_win, dim3((unsigned)wg), dim3(kWNT), 0, st, wa);
+      SME_CHECK_LAUNCH();
+    };
+    for (int round = 0; round < kWinRounds && n_round > 0; round++) {
+      if (round > 0) {
+        hipLaunchKernelGGL(k_reset_cnt, dim3((unsigned)std::min((n_round + 255) / 256, 4096)), dim3(256), 0, st,
+                           round_list, n_round, ccnt);
+        hipLaunchKernelGGL(k_query_pos, dim3((unsigned)std::min((n_round + 255) / 256, 8192)), dim3(256), 0, st,
+                           round_list, d_qoff, n_round, qpos);
+      }
+      wa.nq = n_round;
+      wa.nslices = (int)std::max<int64_t>(1, std::min<int64_t>(n_round / cx->opt_win_slice, 4096));
+      if (round == 0 && cx->opt_win_sample && nwin >= 16) {
+        // sample windows, raised thresholds, then the rest
+        launch_win(wl, n_samp);
+        hipLaunchKernelGGL(k_query_raise, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, nq, k, cap, ccnt, cs,
+                           ckk, th0, thk);
+        SME_CHECK_LAUNCH();
+        launch_win(wl + n_samp, nwin - n_samp);
+      } else {
+        launch_win(nullptr, nwin);
+      }
+      if (round == 0) SME_HIP(hipEventRecord(e2, st));
+      // overflow lists alternate between the two halves of `ovf`
+      int32_t *out_list = ovf + (round & 1) * (nq + 1);
+      SME_HIP(hipMemsetAsync(novf, 0, sizeof(unsigned int), st));
+      fa.qlist = round_list;
+      fa.n = n_round;
+      fa.ovf = out_list;
+      hipLaunchKernelGGL(k_query_final, dim3((unsigned)std::min(n_round, 1 << 16)), dim3(64), 0, st, fa);
+      SME_CHECK_LAUNCH();
+      unsigned int h_novf = 0;
+      SME_HIP(hipMemcpyAsync(&h_novf, novf, sizeof h_novf, hipMemcpyDeviceToHost, st));
+      SME_HIP(hipStreamSynchronize(st));
+      n_round = (int)h_novf;
+      round_list = out_list;
+      n_ovf += round == 0 ? n_round : 0;
+      if (cap < k) break;  // no bound can be raised: every overflowed query to the fallback
+    }
+    if (n_round > 0) {  // still overflowing: the block-max sweep
       QBmArgs ob = qa;
-      ob.qorder = ovf;
-      ob.nq = (int)n_ovf;
+      ob.qorder = round_list;
+      ob.nq = n_round;
       launch_bm(ob);
       SME_CHECK_LAUNCH();
     }
+    cx->last_query_fallback = n_round;
   } else if (tiled) {
     SME_HIP(hipEventRecord(e1, st));
     launch_bm(qa);
@@ -1759,8 +2066,13 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   if (qstats) {
     uint64_t h[8];
     SME_HIP(hipMemcpy(h, qstats, sizeof h, hipMemcpyDeviceToHost));
-    fprintf(stderr, "SME_QSTATS tiles=%llu blocks_gated=%llu candidates=%llu compactions=%llu\n",
-            (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3]);
+    if (win)
+      fprintf(stderr, "SME_QSTATS pairs=%llu sparse_postings=%llu blocks_over_gate=%llu heavy_terms=%llu "
+              "docs_over_gate=%llu kept=%llu\n", (unsigned long long)h[0], (unsigned long long)h[1],
+              (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[4], (unsigned long long)h[5]);
+    else
+      fprintf(stderr, "SME_QSTATS tiles=%llu blocks_gated=%llu candidates=%llu compactions=%llu\n",
+              (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3]);
   }
   if (h_err) throw Error(SME_ELIMIT, "a query has more than 128 terms");
 }

@@ -181,7 +181,7 @@ def test_queries_vs_oracle(sme, synth, idf_mode):
 def _query_opts(ix, terms, qoff, k, **opts):
     """Query with context path options set (sme_set_option), then restore the defaults."""
     defaults = {"query_kernel": 0, "heavy_div": 32, "seed_tiles": 4, "query_order": 1, "cand_cap": 1024,
-                "seed_m": 64}
+                "seed_m": 64, "win_sample": 1}
     try:
         for n, v in opts.items():
             ix.ctx.set_option(n, v)
@@ -201,6 +201,7 @@ def _query_both_kernels(ix, terms, qoff, k):
     dn, sc = ix.query_topk(terms, qoff, k)
     assert ix.ctx.last_build_profile()["query_kernel_name"] in ("k_query_win", "k_query")
     variants = [{"heavy_div": 0}, {"heavy_div": 1 << 30}, {"heavy_div": 1}, {"seed_m": 0}, {"cand_cap": 4},
+                {"win_sample": 0}, {"cand_cap": 16, "seed_m": 0},
                 {"cand_cap": 1, "heavy_div": 1}, {"query_kernel": 2}, {"query_kernel": 2, "seed_tiles": 0},
                 {"query_kernel": 2, "seed_tiles": 8, "query_order": 0}, {"query_kernel": 2, "heavy_div": 0}]
     if k <= 32:
