@@ -1215,11 +1215,22 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
     mc = a.skt[x * a.nrows + D.brow];
     me = a.skt[(x + 1) * a.nrows + D.brow];
   }
+  QPos NP{0, 0, 0};  // next query's position record, loaded a pair ahead
+  if (pos + kWNT / 64 < p_hi) NP = a.qpos[pos + kWNT / 64];
   for (;;) {
     const int npos = pos + kWNT / 64;
     const bool hasn = npos < p_hi;
-    QPos NP{0, 0, 0};
-    if (hasn) NP = a.qpos[npos];
+    // the next query's term records and threshold, and the position record after it
+    QDesc ND{0, 0, 0, -1, 0, 0.0};
+    double nth0 = 0.0;
+    uint64_t nthk = kNoKey;
+    QPos NNP{0, 0, 0};
+    if (hasn) {
+      ND = ld_desc(a.desc, NP.q0, NP.nt, lane);
+      nth0 = a.th0[NP.q];
+      nthk = a.thk[NP.q];
+      if (npos + kWNT / 64 < p_hi) NNP = a.qpos[npos + kWNT / 64];
+    }
     const uint64_t hm = (uint64_t)__ballot(D.hr >= 0);
     const uint64_t sm = (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
     const uint32_t gate = gate_of(th0, a.alpha);
@@ -1266,20 +1277,19 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
         const int32_t e = e0 + lane;
         int64_t pb = 0;
         double wj = 0.0;
-        int rj = 0;
         for (uint64_t m = sm; m; m &= m - 1) {
           const int j = (int)__builtin_ctzll(m);
           const int32_t pj = __builtin_amdgcn_readlane(prej, j);
           if (e >= pj) {
             pb = rl64(plo, j) - pj;
             wj = rld(D.idf, j);
-            rj = __builtin_amdgcn_readlane(D.brow, j);
           }
         }
         if (e < total) {
           const int32_t d = a.docno[pb + e], f = a.tf[pb + e];
           const int r = (int)((int64_t)d - wbase);
-          const uint32_t qv = f <= 255 ? (uint32_t)a.qlut[(int64_t)rj * 256 + f] : impact(a.lut[f], wj, a.alpha);
+          // q(tf) computed here (the batch table would be a second dependent load)
+          const uint32_t qv = impact(f < kLutLds ? s_lut[f] : a.lut[f], wj, a.alpha);
           atomicAdd(&lacc[((r & 63) >> 1) * 64 + (r >> 6)], qv << ((r & 1) << 4));
           // block b = r >> 4 of lane b >> 2: lblk[(b & 3) * 64 + (b >> 2)]
           atomicAdd(&lblk[((r >> 4) & 3) * 64 + (r >> 6)], qv);
@@ -1288,14 +1298,11 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
       }
       qwave_sync();
     }
-    // next query's term records and threshold (in flight during the block phase)
-    QDesc ND{0, 0, 0, -1, 0, 0.0};
-    double nth0 = 0.0;
-    uint64_t nthk = kNoKey;
-    if (hasn) {
-      ND = ld_desc(a.desc, NP.q0, NP.nt, lane);
-      nth0 = a.th0[NP.q];
-      nthk = a.thk[NP.q];
+    // the next query's skip entries (its records arrived during the sparse pass)
+    int32_t nmc = 0, nme = 0;
+    if (ND.mdf > 0 && ND.hr < 0) {
+      nmc = a.skt[x * a.nrows + ND.brow];
+      nme = a.skt[(x + 1) * a.nrows + ND.brow];
     }
     // blocks over the gate: heavy maxima + the block's sparse impact sum
     uint32_t ub[4] = {ub0 & 0xFFFFu, ub0 >> 16, ub1 & 0xFFFFu, ub1 >> 16};
@@ -1449,15 +1456,10 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
       }
     }
     if (!hasn) break;
-    // next query's skip entries, then rotate the pipeline
-    int32_t nmc = 0, nme = 0;
-    if (ND.mdf > 0 && ND.hr < 0) {
-      nmc = a.skt[x * a.nrows + ND.brow];
-      nme = a.skt[(x + 1) * a.nrows + ND.brow];
-    }
     qwave_sync();  // this wave's LDS is rewritten for the next query
     pos = npos;
     P = NP;
+    NP = NNP;
     D = ND;
     th0 = nth0;
     thk = nthk;
