@@ -226,8 +226,8 @@ def write_mapping(docids):
 class CpuOptIndex:
     """The cpu-opt baseline build (oracle/oracle_cpuopt.cc, OpenMP): K = 1, one split."""
 
-    def __init__(self, corpus, mapping, threads=0):
-        import numpy as np
+    @staticmethod
+    def _sigs():
         L = lib()
         L.or_cpuopt_build.restype = C.c_void_p
         L.or_cpuopt_build.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_int]
@@ -237,6 +237,13 @@ class CpuOptIndex:
         L.or_cpuopt_query.restype = C.c_double
         L.or_cpuopt_query.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_void_p, C.c_void_p]
+        L.or_cpuopt_from_csr.restype = C.c_void_p
+        L.or_cpuopt_from_csr.argtypes = [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+        return L
+
+    def __init__(self, corpus, mapping, threads=0):
+        import numpy as np
+        L = self._sigs()
         self._h = L.or_cpuopt_build(corpus, len(corpus), mapping, len(mapping), threads)
         if not self._h:
             raise RuntimeError("cpu-opt build rejected the corpus")
@@ -249,9 +256,7 @@ class CpuOptIndex:
     def from_csr(cls, N, off, docno, tf):
         """Wrap CSR arrays (reduce order) of an index built elsewhere; no term strings."""
         import numpy as np
-        L = lib()
-        L.or_cpuopt_from_csr.restype = C.c_void_p
-        L.or_cpuopt_from_csr.argtypes = [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L = cls._sigs()
         self = cls.__new__(cls)
         off = np.ascontiguousarray(off, np.int64)
         docno = np.ascontiguousarray(docno, np.int32)

@@ -43,3 +43,18 @@ def test_cpuopt_fuzz(seed):
     import common
     corpus, ids = common.fuzz_corpus(seed, 120)
     _check(corpus, ids, 4)
+
+
+def test_cpuopt_from_csr_matches_built_index():
+    """The cpu-opt rank() over an index wrapped from CSR arrays (bench.py's
+    full-index CPU query leg) answers like the cpu-opt index built from text."""
+    import numpy as np
+    n = 400
+    corpus = synth.gen_corpus(n, V=2000, seed=5, len_lo=30, len_hi=90)
+    built = O.CpuOptIndex(corpus, synth.mapping_bytes(n), 2)
+    off, dn, tf, _ = built.csr()
+    wrapped = O.CpuOptIndex.from_csr(built.N, off, dn, tf)
+    tq, qo = synth.queries_by_df(np.diff(off).astype(np.int32), 50, seed=3)
+    d1, s1, _ = built.query(tq, qo, 10, 0, 2)
+    d2, s2, _ = wrapped.query(tq, qo, 10, 0, 2)
+    assert np.array_equal(d1, d2) and np.array_equal(s1, s2)

@@ -43,8 +43,16 @@ def main():
             continue
         # template instantiations of one kernel (e.g. the query kernel's register
         # and LDS paths) are launched together: a "launch" is the sum of their means
-        f = sum(sum(v) / len(v) for v in fk) * 1024
-        w = sum(sum(v) / len(v) for v in wk) * 1024
+        # a kernel launched several times per batch (k_query_win: sample windows,
+        # the rest, overflow rounds) counts per batch: total / k_query_seed dispatches
+        anchor = [v for n, v in fetch.items() if "k_query_seed" in n] if "k_query_win" in k else []
+        if anchor:
+            nb = len(anchor[0])
+            f = sum(sum(v) for v in fk) / nb * 1024
+            w = sum(sum(v) for v in wk) / nb * 1024
+        else:
+            f = sum(sum(v) / len(v) for v in fk) * 1024
+            w = sum(sum(v) / len(v) for v in wk) * 1024
         res["kernels"][k] = {"fetch_bytes_raw": round(f), "write_bytes": round(w), "dispatches": len(fk[0]),
                              "instantiations": len(fk), "hbm_bytes_per_launch": round(2 * f + w)}
     os.makedirs("profiles", exist_ok=True)
