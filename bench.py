@@ -304,8 +304,8 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     gc.disable()  # no cyclic-GC pause inside the timed batches (re-enabled after)
     # a one-off host stall of ~50 ms right after the timed region opens was seen
     # on the GPU box (cause not found: not GC, not the profile read); >= 5
-    # batches amortise it like any other steady-state overhead
-    steps = max(5, a.steps)
+    # batches amortise it like any other steady-state overhead (10 at least)
+    steps = max(10, a.steps)
     kms, pms, kname = [], [], "k_query"
     t0 = time.perf_counter()
     walls = []

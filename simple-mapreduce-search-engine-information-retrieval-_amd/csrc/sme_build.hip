@@ -879,6 +879,15 @@ __device__ __forceinline__ bool slot_hit(const SlotVal &v, const TokSig &g, int3
   return len <= 16 && v.key == g.h && v.rep != 0 && (v.rep & 0xFFFFFFull) == (uint64_t)len && v.w0 == g.w0 &&
          v.w1 == g.w1;
 }
+// The probe's fast path loads only the slot's 16 token bytes (w0, w1; one
+// 16-byte load).  A token of < 16 bytes is its zero-padded (w0, w1) (no token
+// byte is 0), and a slot's (w0, w1) of a token of >= 16 bytes has no zero byte,
+// so equal words mean the same token, whether or not the slot's rep is
+// published yet.  Tokens of >= 16 bytes, and every mismatch, take raw_insert
+// (which re-reads the whole slot coherently).
+__device__ __forceinline__ bool slot_hit16(const ulonglong2 &v, const TokSig &g, int32_t len) {
+  return len < 16 && v.x == g.w0 && v.y == g.w1;
+}
 
 __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n,
                                                      const uint64_t *__restrict__ rs_g,
@@ -1072,7 +1081,7 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
       for (int32_t r0 = (texp & 1) ? nr : tid; r0 < nr; r0 += kTokG * kTokNT) {
         TokSig g[kTokG];
         int32_t len[kTokG], x[kTokG];
-        SlotVal v[kTokG];
+        ulonglong2 v[kTokG];
 #pragma unroll
         for (int u = 0; u < kTokG; u++) {
           const int32_t r = r0 + u * kTokNT;
@@ -1080,14 +1089,15 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
           tok_sig_at(L, t, c_lo, x[u], &g[u], &len[u]);
         }
 #pragma unroll
-        for (int u = 0; u < kTokG; u++) v[u] = ld_slot_plain(&tb.slots[g[u].h & tb.mask]);
+        for (int u = 0; u < kTokG; u++)
+          v[u] = *reinterpret_cast<const ulonglong2 *>(&tb.slots[g[u].h & tb.mask].w0);
 #pragma unroll
         for (int u = 0; u < kTokG; u++) {
           const int32_t r = r0 + u * kTokNT;
           if (r < nr)
-            L.tl[r] = slot_hit(v[u], g[u], len[u])
+            L.tl[r] = slot_hit16(v[u], g[u], len[u])
                           ? (uint32_t)(g[u].h & tb.mask)
-                          : raw_insert(tb, g[u], (uint64_t)(c_lo + x[u]), (uint64_t)len[u], v[u]);
+                          : raw_insert(tb, g[u], (uint64_t)(c_lo + x[u]), (uint64_t)len[u], SlotVal{0, 0, 0, 0});
         }
       }
       __syncthreads();

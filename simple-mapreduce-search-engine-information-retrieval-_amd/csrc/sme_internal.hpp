@@ -28,6 +28,7 @@ struct sme_ctx {
   std::string profile_json;
   std::vector<std::pair<std::string, float>> last_profile;
   std::vector<uint8_t> mapping_out;  // last sme_number_documents result
+  std::vector<int32_t> h_wlist;      // k_query_win window order of the last batch (source of an async copy)
   float last_query_ms = -1.0f;  // device time of the last query kernel launch
   float last_query_prep_ms = -1.0f;  // per-batch tables before it (skip / impact tables, query order)
   float last_query_index_ms = -1.0f;  // one-time heavy-row build of the index it ran on (prepare_queries)

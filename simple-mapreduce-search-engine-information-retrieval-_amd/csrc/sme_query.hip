@@ -1967,13 +1967,13 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     int32_t *wl = W[30].as<int32_t>(nwin + 1);
     int64_t n_samp = 0;
     {
-      std::vector<int32_t> h((size_t)nwin);
+      std::vector<int32_t> &h = cx->h_wlist;  // outlives the async copy
+      h.assign((size_t)nwin, 0);
       for (int64_t xw = 0; xw < nwin; xw += 8) h[(size_t)n_samp++] = (int32_t)xw;
       int64_t o = n_samp;
       for (int64_t xw = 0; xw < nwin; xw++)
         if (xw % 8) h[(size_t)o++] = (int32_t)xw;
       SME_HIP(hipMemcpyAsync(wl, h.data(), nwin * sizeof(int32_t), hipMemcpyHostToDevice, st));
-      SME_HIP(hipStreamSynchronize(st));
     }
     auto launch_win = [&](const int32_t *wlist, int64_t nw) {
       wa.wlist = wlist;

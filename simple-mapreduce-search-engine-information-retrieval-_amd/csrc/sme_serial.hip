@@ -35,9 +35,18 @@ __device__ __forceinline__ int64_t comp_of(const int32_t *gram, int K, int64_t t
   return gram ? (int64_t)gram[t * K + j] : t;
 }
 
-__global__ void k_ser_sizes(const int64_t *toff, const uint16_t *tch, const int32_t *gram, int K, const int64_t *off,
-                            int64_t V, int R, int64_t *rec_bytes, uint32_t *part, uint32_t *idx,
-                            unsigned long long *psum) {
+// Partition byte totals are summed in LDS first (one global atomic per block
+// and partition): with few partitions, per-term global atomics on R addresses
+// serialise (24 ms for the 2 M terms of c2 at R = 1).
+constexpr int kSerLdsParts = 1024;
+__global__ __launch_bounds__(256) void k_ser_sizes(const int64_t *toff, const uint16_t *tch, const int32_t *gram, int K,
+                                                   const int64_t *off, int64_t V, int R, int64_t *rec_bytes,
+                                                   uint32_t *part, uint32_t *idx, unsigned long long *psum) {
+  __shared__ unsigned long long s_ps[kSerLdsParts];
+  const bool lds = R <= kSerLdsParts;
+  if (lds)
+    for (int i = threadIdx.x; i < R; i += blockDim.x) s_ps[i] = 0ull;
+  __syncthreads();
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
     int64_t ul = 0;
     uint32_t ah = 1u;  // Arrays.hashCode: 31 * h + String.hashCode per element, seed 1
@@ -59,7 +68,12 @@ __global__ void k_ser_sizes(const int64_t *toff, const uint16_t *tch, const int3
     const uint32_t p = (uint32_t)((int32_t)(ah & 0x7fffffffu) % R);
     part[t] = p;
     idx[t] = (uint32_t)t;
-    atomicAdd(&psum[p], (unsigned long long)(8 + key + val));
+    atomicAdd(lds ? &s_ps[p] : &psum[p], (unsigned long long)(8 + key + val));
+  }
+  if (lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < R; i += blockDim.x)
+      if (s_ps[i]) atomicAdd(&psum[i], s_ps[i]);
   }
 }
 
@@ -123,9 +137,32 @@ __global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int3
         for (int i = 0; i < kClassLen; i++) q[10 + i] = (uint8_t)"sa.edu.kaust.io.PostingWritable"[i];
       }
     }
-    for (int64_t i = lane; i < df; i += 64) {
-      put_be32(post + 8 * i, (uint32_t)docno_o[p0 + i]);
-      put_be32(post + 8 * i + 4, (uint32_t)tf_o[p0 + i]);
+    // postings: the stream of big-endian (docno, tf) words written as aligned
+    // dwords -- output dword at stream byte b = 4 f + s is v_alignbyte of the
+    // stream words f + 1 and f (each word byte-swapped so that a little-endian
+    // store lays its bytes out big-endian); the unaligned head and tail bytes
+    // singly.  (Byte stores of every posting cost 22 ms on c2.)
+    if (df > 0) {
+      const int64_t nb = 8 * df;
+      const int a = (int)((uintptr_t)post & 3);
+      const int h = (4 - a) & 3;  // head bytes before the first aligned address
+      auto word = [&](int64_t f) -> uint32_t {
+        const uint32_t v = (f & 1) ? (uint32_t)tf_o[p0 + (f >> 1)] : (uint32_t)docno_o[p0 + (f >> 1)];
+        return __builtin_bswap32(v);
+      };
+      if (lane < h && lane < nb) post[lane] = (uint8_t)(word(0) >> (8 * lane));
+      const int64_t nd = (nb - h) >> 2;  // whole aligned dwords
+      uint32_t *dst = reinterpret_cast<uint32_t *>(post + h);
+      for (int64_t k = lane; k < nd; k += 64) {
+        const int64_t b = h + 4 * k, f = b >> 2;
+        const int sft = (int)(b & 3);
+        dst[k] = sft == 0 ? word(f) : __builtin_amdgcn_alignbyte(word(f + 1), word(f), sft);
+      }
+      const int64_t t0 = h + 4 * nd;  // tail bytes
+      if (lane < nb - t0) {
+        const int64_t b = t0 + lane;
+        post[b] = (uint8_t)(word(b >> 2) >> (8 * (b & 3)));
+      }
     }
   }
 }
