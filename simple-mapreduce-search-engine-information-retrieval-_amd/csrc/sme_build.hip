@@ -728,6 +728,10 @@ constexpr int kTokCap = 2560;  // chunk tokens per round (a c2 chunk holds ~1950
 #define SME_TOKG 2
 #endif
 constexpr int kTokG = SME_TOKG;  // tokens per lane step in the probe pass
+#ifndef SME_FASTPROBES
+#define SME_FASTPROBES 4
+#endif
+constexpr int kFastProbes = SME_FASTPROBES;  // slots a probe checks with plain loads before raw_insert
 
 // entity span end: '&' [a-z0-9#]* ';'  (TagTokenizer.onAmpersand 644-662); p if none
 template <typename B>
@@ -1094,10 +1098,27 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
 #pragma unroll
         for (int u = 0; u < kTokG; u++) {
           const int32_t r = r0 + u * kTokNT;
-          if (r < nr)
-            L.tl[r] = slot_hit16(v[u], g[u], len[u])
-                          ? (uint32_t)(g[u].h & tb.mask)
+          if (r < nr) {
+            // linear probing over occupied slots of other tokens with plain
+            // loads (a slot, once filled, never changes); an empty-looking slot,
+            // a token of >= 16 bytes or a long probe run take raw_insert
+            uint64_t sl = g[u].h & tb.mask;
+            bool hit = slot_hit16(v[u], g[u], len[u]);
+            if (!hit && len[u] < 16 && v[u].x != 0) {
+              for (int pr = 1; pr < kFastProbes; pr++) {
+                const uint64_t s2 = (sl + pr) & tb.mask;
+                const ulonglong2 w = *reinterpret_cast<const ulonglong2 *>(&tb.slots[s2].w0);
+                if (slot_hit16(w, g[u], len[u])) {
+                  hit = true;
+                  sl = s2;
+                  break;
+                }
+                if (w.x == 0) break;
+              }
+            }
+            L.tl[r] = hit ? (uint32_t)sl
                           : raw_insert(tb, g[u], (uint64_t)(c_lo + x[u]), (uint64_t)len[u], SlotVal{0, 0, 0, 0});
+          }
         }
       }
       __syncthreads();
