@@ -87,9 +87,15 @@ void sme_destroy(sme_ctx *ctx);
 /* Path options of a context (no reference counterpart: the reference has one
  * code path).  Every value gives bit-identical results; the options exist so
  * tests can hold each device path to the others and benches can sweep them.
- *   "query_kernel"  0 block-max pruned scoring (default), 1 streaming k_query (k <= 32)
- *   "heavy_div"     heavy tf rows for terms with df >= docno span / div (default 32; 0 none)
- *   "seed_tiles"    best-bound tiles scored before the sweep, 0..8 (default 4)
+ *   "query_kernel"  0 window-major scoring with seeded thresholds (default), 1 streaming
+ *                   k_query (k <= 32), 2 per-query block-max sweep k_query_bm
+ *   "heavy_div"     heavy tf / impact rows for terms with df >= docno span / div (default 32; 0 none)
+ *   "seed_m"        seed postings per term for the window path's threshold, 0..4096 (default 64)
+ *   "cand_cap"      candidate list per query of the window path, 1..2048 (default 1024; >= 1024:
+ *                   at least 16 k)
+ *   "win_sample"    1 (default): sample windows first, thresholds raised, then the rest
+ *   "win_slice"     queries per window-path workgroup slice (default 512)
+ *   "seed_tiles"    k_query_bm: best-bound tiles scored before the sweep, 0..8 (default 4)
  *   "query_order"   1 heaviest-term query order (default), 0 batch order
  *   "agg_two_pass"  1 count + emit aggregation passes (default 0: single pass)
  *   "tok_grid"      tokenizer workgroups, >= 1 (default 4096)

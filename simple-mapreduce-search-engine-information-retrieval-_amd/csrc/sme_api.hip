@@ -271,7 +271,7 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
       range(1, int64_t(1) << 30);
       cx->opt_tok_grid = v;
     } else if (n == "cand_cap") {
-      range(1, 1024);
+      range(1, 2048);
       cx->opt_cand_cap = v;
     } else if (n == "win_sample") {
       range(0, 1);

@@ -996,7 +996,7 @@ constexpr int kWDL = kWin / 64;      // documents per lane (64)
 constexpr int kWNT = 256;            // 4 waves per workgroup, each on its own query
 constexpr int kSList = 256;          // a window's sparse postings kept in LDS for exact tf lookups
 constexpr int kSeedSlots = 1024;     // seed documents per query (LDS hash)
-constexpr int kCandMax = 1024;       // largest candidate list per query (final kernel LDS)
+constexpr int kCandMax = 2048;       // largest candidate list per query (final kernel LDS)
 constexpr int kWinRounds = 3;        // window passes before an overflowing query goes to k_query_bm
 constexpr int kCList = 512;          // documents over the gate listed per round of exact scoring
 static_assert(kWDL == 64, "one lane owns 64 documents: four uint4 impact loads per heavy term");
@@ -1489,9 +1489,10 @@ struct QFinalArgs {
 // of the true top k is at least as good as B.  It becomes the query's threshold
 // (score and key) for the next round, which keeps only documents not worse
 // than B (deep exact ties at the score are cut by key).
+template <int CM>
 __global__ __launch_bounds__(64) void k_query_final(QFinalArgs a) {
-  __shared__ double bs[kCandMax];
-  __shared__ uint64_t bk[kCandMax];
+  __shared__ double bs[CM];
+  __shared__ uint64_t bk[CM];
   const int lane = threadIdx.x;
   for (int i = blockIdx.x; i < a.n; i += gridDim.x) {
     const int q = a.qlist ? a.qlist[i] : i;
@@ -1530,14 +1531,16 @@ __global__ __launch_bounds__(64) void k_query_final(QFinalArgs a) {
 // entries, all real documents with exact scores) bounds its k-th best score
 // from below; if it beats the seed threshold it replaces it, so the remaining
 // windows keep far fewer documents.
-__global__ __launch_bounds__(64) void k_query_raise(int nq, int k, int cap, const unsigned int *ccnt, const double *cs,
-                                                    const uint64_t *ck, double *th_s, uint64_t *th_k) {
-  __shared__ double bs[kCandMax];
-  __shared__ uint64_t bk[kCandMax];
+template <int CM>
+__global__ __launch_bounds__(64) void k_query_raise(int nq, int k, int cap, unsigned int *ccnt, double *cs,
+                                                    uint64_t *ck, double *th_s, uint64_t *th_k) {
+  __shared__ double bs[CM];
+  __shared__ uint64_t bk[CM];
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < nq; q += gridDim.x) {
-    const int n = (int)min(ccnt[q], (unsigned int)cap);
-    if (n < k) continue;
+    const unsigned int c = ccnt[q];
+    if (c > (unsigned int)cap || (int)c < k) continue;  // overflowed (re-run later) or too few to bound
+    const int n = (int)c;
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
     for (int j = lane; j < n2; j += 64) {
@@ -1546,9 +1549,19 @@ __global__ __launch_bounds__(64) void k_query_raise(int nq, int k, int cap, cons
     }
     __syncthreads();
     wave_sort(bs, bk, n2);
-    if (lane == 0 && better(bs[k - 1], bk[k - 1], th_s[q], th_k[q])) {
-      th_s[q] = bs[k - 1];
-      th_k[q] = bk[k - 1];
+    // the list keeps only its best k (nothing worse than its k-th best can be in
+    // the top k), so later windows append into free room
+    const bool up = better(bs[k - 1], bk[k - 1], th_s[q], th_k[q]);
+    for (int r = lane; r < k; r += 64) {
+      cs[(int64_t)q * cap + r] = bs[r];
+      ck[(int64_t)q * cap + r] = bk[r];
+    }
+    if (lane == 0) {
+      ccnt[q] = (unsigned int)k;
+      if (up) {
+        th_s[q] = bs[k - 1];
+        th_k[q] = bk[k - 1];
+      }
     }
     __syncthreads();
   }
@@ -1922,7 +1935,10 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     SME_HIP(hipEventRecord(e1, st));
     // 2. windows x query slices; 3. per-query selection.  Overflowed lists run
     // again with the raised threshold (at most kWinRounds rounds), the rest -> k_query_bm
-    const int cap = (int)std::min<int64_t>(cx->opt_cand_cap, kCandMax);
+    // candidate list per query: the option, at least 16 k for large k (deep
+    // exact ties at the k-th score), at most kCandMax
+    const int cap = (int)std::min<int64_t>(std::max<int64_t>(cx->opt_cand_cap, cx->opt_cand_cap >= 1024 ? 16 * (int64_t)k : 0),
+                                           kCandMax);
     unsigned int *ccnt = W[42].as<unsigned int>(nq + 1);
     double *cs = W[43].as<double>((size_t)nq * cap);
     uint64_t *ckk = W[61].as<uint64_t>((size_t)nq * cap);
@@ -1965,14 +1981,22 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     // window lists: every 8th window (sample), the rest
     const int64_t nwin = wa.nwin;
     int32_t *wl = W[30].as<int32_t>(nwin + 1);
-    int64_t n_samp = 0;
+    int64_t n_samp = 0, stage_start[5] = {0, 0, 0, 0, 0};
     {
       std::vector<int32_t> &h = cx->h_wlist;  // outlives the async copy
       h.assign((size_t)nwin, 0);
-      for (int64_t xw = 0; xw < nwin; xw += 8) h[(size_t)n_samp++] = (int32_t)xw;
-      int64_t o = n_samp;
-      for (int64_t xw = 0; xw < nwin; xw++)
-        if (xw % 8) h[(size_t)o++] = (int32_t)xw;
+      // stages: the first two windows (under deep exact ties at the k-th score
+      // the docno tie-break makes the docno prefix decisive) and every 8th, then
+      // the windows 4 mod 8, then 2 mod 4, then the odd ones -- 1/8, 1/8, 1/4,
+      // 1/2 of the windows, each stage after a raise (and a compaction) of every
+      // query's threshold and list
+      auto stage_of = [](int64_t xw) { return (xw < 2 || xw % 8 == 0) ? 0 : xw % 8 == 4 ? 1 : xw % 4 == 2 ? 2 : 3; };
+      for (int sg = 0; sg < 4; sg++) {
+        stage_start[sg] = n_samp;
+        for (int64_t xw = 0; xw < nwin; xw++)
+          if (stage_of(xw) == sg) h[(size_t)n_samp++] = (int32_t)xw;
+      }
+      stage_start[4] = n_samp;
       SME_HIP(hipMemcpyAsync(wl, h.data(), nwin * sizeof(int32_t), hipMemcpyHostToDevice, st));
     }
     auto launch_win = [&](const int32_t *wlist, int64_t nw) {
@@ -1994,12 +2018,18 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       wa.nq = n_round;
       wa.nslices = (int)std::max<int64_t>(1, std::min<int64_t>(n_round / cx->opt_win_slice, 4096));
       if (round == 0 && cx->opt_win_sample && nwin >= 16) {
-        // sample windows, raised thresholds, then the rest
-        launch_win(wl, n_samp);
-        hipLaunchKernelGGL(k_query_raise, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, nq, k, cap, ccnt, cs,
-                           ckk, th0, thk);
-        SME_CHECK_LAUNCH();
-        launch_win(wl + n_samp, nwin - n_samp);
+        for (int sg = 0; sg < 4; sg++) {
+          if (sg > 0) {  // raise thresholds, keep each list's best k
+            if (cap <= 1024)
+              hipLaunchKernelGGL(k_query_raise<1024>, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, nq, k,
+                                 cap, ccnt, cs, ckk, th0, thk);
+            else
+              hipLaunchKernelGGL(k_query_raise<kCandMax>, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, nq,
+                                 k, cap, ccnt, cs, ckk, th0, thk);
+            SME_CHECK_LAUNCH();
+          }
+          launch_win(wl + stage_start[sg], stage_start[sg + 1] - stage_start[sg]);
+        }
       } else {
         launch_win(nullptr, nwin);
       }
@@ -2010,7 +2040,10 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       fa.qlist = round_list;
       fa.n = n_round;
       fa.ovf = out_list;
-      hipLaunchKernelGGL(k_query_final, dim3((unsigned)std::min(n_round, 1 << 16)), dim3(64), 0, st, fa);
+      if (cap <= 1024)
+        hipLaunchKernelGGL(k_query_final<1024>, dim3((unsigned)std::min(n_round, 1 << 16)), dim3(64), 0, st, fa);
+      else
+        hipLaunchKernelGGL(k_query_final<kCandMax>, dim3((unsigned)std::min(n_round, 1 << 16)), dim3(64), 0, st, fa);
       SME_CHECK_LAUNCH();
       unsigned int h_novf = 0;
       SME_HIP(hipMemcpyAsync(&h_novf, novf, sizeof h_novf, hipMemcpyDeviceToHost, st));
