@@ -3001,12 +3001,11 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     const int nwords = std::min(8, (std::max(term_maxlen, 1) + cpw - 1) / cpw);
     uint64_t *kw = W[W_KHI].as<uint64_t>(V), *kw2 = W[W_KLO].as<uint64_t>(V);
     uint32_t *ord_a = vidx, *ord_b = order;
+    uint32_t *rscr = W[W_RADIX].as<uint32_t>(kv_sort_scratch(V) / sizeof(uint32_t) + 1);
     size_t tbb = 0;
     for (int w = nwords - 1; w >= 0; w--) {
       hipLaunchKernelGGL(k_term_word, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V, vcs, co.pool, w, cpw, ub, kw);
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, kw, kw2, ord_a, ord_b, (int)V, 0, kbits, st));
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, kw, kw2, ord_a, ord_b, (int)V, 0, kbits, st));
-      std::swap(ord_a, ord_b);
+      if (kv_sort<uint64_t>(kw, ord_a, kw2, ord_b, V, kbits, rscr, st) != ord_a) std::swap(ord_a, ord_b);
     }
     if (ord_a != order)
       SME_HIP(hipMemcpyAsync(order, ord_a, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
@@ -3038,9 +3037,11 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     uint64_t *ok2 = W[W_T0].as<uint64_t>(novf);
     uint32_t *oi = W[W_T1].as<uint32_t>(novf), *oi2 = W[W_VIDX].as<uint32_t>(novf);
     hipLaunchKernelGGL(k_iota_u32, dim3(grid_for(novf)), dim3(256), 0, st, oi, novf);
-    size_t tbb = 0;
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, co.ovf_key, ok2, oi, oi2, (int)novf, 0, 64, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, co.ovf_key, ok2, oi, oi2, (int)novf, 0, 64, st));
+    uint32_t *rscr = W[W_RADIX].as<uint32_t>(kv_sort_scratch(novf) / sizeof(uint32_t) + 1);
+    if (kv_sort<uint64_t>(co.ovf_key, oi, ok2, oi2, novf, 64, rscr, st, true) == oi) {
+      std::swap(oi, oi2);
+      ok2 = co.ovf_key;
+    }
     hipLaunchKernelGGL(k_raw_multi, dim3(grid_for(novf)), dim3(256), 0, st, ok2, oi2, novf, nraw, cand_final,
                        rank_of_slot, raw_term, multi);
   }

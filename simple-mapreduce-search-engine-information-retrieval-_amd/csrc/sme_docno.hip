@@ -173,13 +173,12 @@ void number_documents(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st,
   for (int64_t i = 0; i < nR; i++) iota[i] = (uint32_t)i;
   if (nR > 0) SME_HIP(hipMemcpyAsync(oa, iota.data(), nR * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   const int nwords = (int)((maxlen + 7) / 8);
+  uint32_t *rscr = W[60].as<uint32_t>(kv_sort_scratch(nR) / sizeof(uint32_t) + 1);
   for (int w = -1; w < nwords && nR > 1; w++) {
     const int pw = w < 0 ? -1 : nwords - 1 - w;  // after the length pass: last word first
     hipLaunchKernelGGL(k_docid_word, grid(nR), dim3(256), 0, st, oa, nR, ids, off, pw, ka);
     const int bits = pw < 0 ? bits_of((uint64_t)maxlen) : 64;
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ka, kb, oa, ob, (int)nR, 0, bits, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tb), tb, ka, kb, oa, ob, (int)nR, 0, bits, st));
-    std::swap(oa, ob);
+    if (kv_sort<uint64_t>(ka, oa, kb, ob, nR, bits, rscr, st) != oa) std::swap(oa, ob);
   }
   uint32_t *flag = W[59].as<uint32_t>(nR + 1);
   if (nR > 0) hipLaunchKernelGGL(k_docid_distinct, grid(nR), dim3(256), 0, st, oa, nR, ids, off, flag);

@@ -176,6 +176,13 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
                     const int64_t *xoff, int64_t P, int bits, int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf,
                     uint32_t *counts, hipStream_t st);
 size_t term_sort_scratch(int64_t P);
+// stable LSD radix sort of (key, u32 value) pairs by the key's low `bits` bits
+// (sme_sort.hip; K = uint32_t or uint64_t); ping-pongs between (k0, v0) and
+// (k1, v1) and returns the sorted values' buffer (keys beside it if keys_out)
+template <typename K>
+uint32_t *kv_sort(K *k0, uint32_t *v0, K *k1, uint32_t *v1, int64_t n, int bits, uint32_t *scratch, hipStream_t st,
+                  bool keys_out = false);
+size_t kv_sort_scratch(int64_t n);
 void serialize_index(sme_index *ix, hipStream_t st);
 void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t st);
 void prepare_queries(sme_index *ix, hipStream_t st);

@@ -371,6 +371,146 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
   }
 }
 
+// Generic stable (key, u32 value) pass for the build's other sorts (vocabulary
+// words, docid words): the same reduce-then-scan structure, plain coalesced
+// loads, 32- or 64-bit keys staged through LDS as 32-bit halves.
+template <typename K>
+__global__ __launch_bounds__(kRsNT) void k_kv_count(const K *__restrict__ key, int64_t n, int shift, int nbins,
+                                                    uint32_t *__restrict__ counts) {
+  __shared__ uint32_t h[kRsMaxBins];
+  const int tid = threadIdx.x;
+  for (int b = tid; b < nbins; b += kRsNT) h[b] = 0;
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * kRsTile;
+  const int m = (int)min((int64_t)kRsTile, n - t0);
+  const uint32_t mask = (uint32_t)nbins - 1u;
+  for (int i = tid; i < m; i += kRsNT) atomicAdd(&h[(uint32_t)(key[t0 + i] >> shift) & mask], 1u);
+  __syncthreads();
+  for (int b = tid; b < nbins; b += kRsNT) counts[(int64_t)blockIdx.x * nbins + b] = h[b];
+}
+
+template <typename K, bool KEYS>
+__global__ __launch_bounds__(kRsNT) void k_kv_scatter(const K *__restrict__ key, const uint32_t *__restrict__ val,
+                                                      int64_t n_all, int shift, int nbits,
+                                                      const uint32_t *__restrict__ offs, K *__restrict__ okey,
+                                                      uint32_t *__restrict__ oval) {
+  __shared__ uint16_t wc[kRsWaves * kRsMaxBins];
+  __shared__ uint32_t gd[kRsMaxBins];
+  __shared__ uint32_t stage[kRsTile];
+  __shared__ uint32_t ws[kRsWaves];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nbins = 1 << nbits;
+  const uint32_t mask = (uint32_t)nbins - 1u;
+  const int64_t per = (int64_t)(gridDim.x >> 3);  // XCD-aware tile order, as k_rs_scatter
+  const int64_t tile = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const int64_t t0 = tile * kRsTile;
+  if (t0 >= n_all) return;
+  const int n = (int)min((int64_t)kRsTile, n_all - t0);
+  for (int i = tid; i < kRsWaves * kRsMaxBins / 2; i += kRsNT) reinterpret_cast<uint32_t *>(wc)[i] = 0u;
+  __syncthreads();
+  uint16_t *mine = wc + w * kRsMaxBins;
+  const int wb = w * kRsWaveItems;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  K k[kRsIPL];
+  uint32_t v[kRsIPL], pos[kRsIPL];
+#pragma unroll
+  for (int s = 0; s < kRsIPL; s++) {
+    const int i = wb + s * 64 + lane;
+    const bool ok = i < n;
+    k[s] = ok ? key[t0 + i] : (K)0;
+    v[s] = ok ? val[t0 + i] : 0u;
+  }
+#pragma unroll
+  for (int s = 0; s < kRsIPL; s++) {
+    const bool ok = wb + s * 64 + lane < n;
+    const uint32_t d = (uint32_t)(k[s] >> shift) & mask;
+    uint64_t peers = (uint64_t)__ballot(ok);
+    for (int b = 0; b < nbits; b++) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = (uint64_t)__ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    uint32_t r = 0;
+    if (ok) {
+      const uint32_t c = mine[d];
+      r = c + (uint32_t)__popcll(peers & lt);
+      if ((peers & lt) == 0) mine[d] = (uint16_t)(c + (uint32_t)__popcll(peers));
+    }
+    pos[s] = r;
+  }
+  __syncthreads();
+  {
+    const int b0 = kRsBPT * tid;
+    uint32_t tc[kRsBPT];
+    uint32_t s2 = 0;
+#pragma unroll
+    for (int q = 0; q < kRsBPT; q++) {
+      tc[q] = 0;
+      if (b0 + q < nbins) {
+#pragma unroll
+        for (int x = 0; x < kRsWaves; x++) tc[q] += wc[x * kRsMaxBins + b0 + q];
+      }
+      s2 += tc[q];
+    }
+    uint32_t incl = s2;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t ex = incl - s2;
+    for (int j = 0; j < w; j++) ex += ws[j];
+#pragma unroll
+    for (int q = 0; q < kRsBPT; q++) {
+      if (b0 + q < nbins) {
+        uint32_t r = ex;
+        gd[b0 + q] = offs[tile * nbins + b0 + q] - r;
+#pragma unroll
+        for (int x = 0; x < kRsWaves; x++) {
+          const uint32_t c = wc[x * kRsMaxBins + b0 + q];
+          wc[x * kRsMaxBins + b0 + q] = (uint16_t)r;
+          r += c;
+        }
+      }
+      ex += tc[q];
+    }
+  }
+  __syncthreads();
+  // each slot's digit through LDS first (its output offset), then the key's
+  // 32-bit halves and the values, each staged in digit order and written out
+#pragma unroll
+  for (int s = 0; s < kRsIPL; s++) {
+    if (wb + s * 64 + lane >= n) continue;
+    pos[s] += mine[(uint32_t)(k[s] >> shift) & mask];
+    stage[pos[s]] = (uint32_t)(k[s] >> shift) & mask;
+  }
+  __syncthreads();
+  uint32_t dst[kRsIPL];
+#pragma unroll
+  for (int j = 0; j < kRsIPL; j++) {
+    const int p = j * kRsNT + tid;
+    if (p < n) dst[j] = gd[stage[p]] + (uint32_t)p;
+  }
+  constexpr int kHalves = KEYS ? (int)(sizeof(K) / 4) : 0;
+#pragma unroll
+  for (int hf = 0; hf <= kHalves; hf++) {
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < kRsIPL; s++)
+      if (wb + s * 64 + lane < n) stage[pos[s]] = hf < kHalves ? (uint32_t)((uint64_t)k[s] >> (32 * hf)) : v[s];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRsIPL; j++) {
+      const int p = j * kRsNT + tid;
+      if (p < n) {
+        if (hf < kHalves) reinterpret_cast<uint32_t *>(okey + dst[j])[hf] = stage[p];
+        else oval[dst[j]] = stage[p];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // Stable sort of P (key, packed value) pairs by the low `bits` bits of key.
@@ -424,5 +564,51 @@ size_t term_sort_scratch(int64_t P) {
   const int64_t ntiles = (std::max<int64_t>(P, 1) + kRsTile - 1) / kRsTile;
   return (size_t)(ntiles * kRsMaxBins + (int64_t)kRsMaxBins * kRsGroups) * sizeof(uint32_t) +
          (size_t)(((std::max<int64_t>(P, 1) + 1023) >> 10) + 1) * sizeof(int64_t);
+}
+// Stable sort of n (key, u32 value) pairs by the low `bits` bits of the key
+// (11-bit digits).  k0/v0 hold the input, k1/v1 are second buffers of the same
+// size; returns the buffer holding the sorted values (v0 or v1).  The sorted
+// keys are in the matching key buffer (k0 or k1) when keys_out, else the last
+// pass does not write them.  scratch: kv_sort_scratch(n) bytes.
+template <typename K>
+uint32_t *kv_sort(K *k0, uint32_t *v0, K *k1, uint32_t *v1, int64_t n, int bits, uint32_t *scratch, hipStream_t st,
+                  bool keys_out) {
+  if (n <= 1) return v0;
+  if (n > 0xFFFFFFFFll) throw Error(SME_ELIMIT, "sort of more than 2^32 pairs");
+  bits = std::min(std::max(bits, 1), (int)(8 * sizeof(K)));
+  const int npass = (bits + kRsMaxBits - 1) / kRsMaxBits;
+  const int64_t ntiles = (n + kRsTile - 1) / kRsTile;
+  const int64_t tpg = (ntiles + kRsGroups - 1) / kRsGroups;
+  uint32_t *counts = scratch, *gsum = scratch + ntiles * kRsMaxBins;
+  int shift = 0;
+  for (int p = 0; p < npass; p++) {
+    const int nb = (bits - shift + (npass - p) - 1) / (npass - p);
+    const int nbins = 1 << nb;
+    hipLaunchKernelGGL(k_kv_count<K>, dim3((unsigned)ntiles), dim3(kRsNT), 0, st, k0, n, shift, nbins, counts);
+    hipLaunchKernelGGL(k_rs_colsum, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
+    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, nbins * kRsGroups);
+    hipLaunchKernelGGL(k_rs_colscan, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
+    const unsigned sgrid = (unsigned)(8 * ((ntiles + 7) / 8));
+    if (p == npass - 1 && !keys_out)
+      hipLaunchKernelGGL((k_kv_scatter<K, false>), dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, n, shift, nb, counts,
+                         k1, v1);
+    else
+      hipLaunchKernelGGL((k_kv_scatter<K, true>), dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, n, shift, nb, counts, k1,
+                         v1);
+    SME_CHECK_LAUNCH();
+    std::swap(k0, k1);
+    std::swap(v0, v1);
+    shift += nb;
+  }
+  return v0;
+}
+template uint32_t *kv_sort<uint64_t>(uint64_t *, uint32_t *, uint64_t *, uint32_t *, int64_t, int, uint32_t *,
+                                     hipStream_t, bool);
+template uint32_t *kv_sort<uint32_t>(uint32_t *, uint32_t *, uint32_t *, uint32_t *, int64_t, int, uint32_t *,
+                                     hipStream_t, bool);
+
+size_t kv_sort_scratch(int64_t n) {
+  const int64_t ntiles = (std::max<int64_t>(n, 1) + kRsTile - 1) / kRsTile;
+  return (size_t)(ntiles * kRsMaxBins + (int64_t)kRsMaxBins * kRsGroups) * sizeof(uint32_t);
 }
 }  // namespace sme

@@ -1,7 +1,7 @@
-# query parity subset, c2 qexp, c5 qexp (1M top-100)
+# GPU test suite (QK: -k filter), c2 qexp, c5 qexp (1M top-100)
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -m gpu -x -q --timeout 300 --timeout-method thread -k "quer or forward or repl or scale or c2_full" > gpurun_out/pytest_q.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${QK:+-k "$QK"} > gpurun_out/pytest_q.log 2>&1; rc=$?
 grep -E "FAILED|Error" gpurun_out/pytest_q.log | head; tail -1 gpurun_out/pytest_q.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/qexp.py --reps 2 > gpurun_out/qexp_c2.log 2>&1 || exit 1
 cut -c1-330 gpurun_out/qexp_c2.log | tail -1
