@@ -1472,6 +1472,7 @@ struct QFinalArgs {
   const int32_t *qlist;       // queries of this round (nullptr: 0 .. n-1)
   int n, k, cap;
   const unsigned int *ccnt;
+  const unsigned int *oflag;  // lists that overflowed in an earlier stage (k_query_raise)
   const double *cs;
   const uint64_t *ck;
   int32_t *out_d;
@@ -1497,12 +1498,12 @@ __global__ __launch_bounds__(64) void k_query_final(QFinalArgs a) {
   for (int i = blockIdx.x; i < a.n; i += gridDim.x) {
     const int q = a.qlist ? a.qlist[i] : i;
     const unsigned int c = a.ccnt[q];
-    const bool over = c > (unsigned int)a.cap;
+    const bool over = c > (unsigned int)a.cap || a.oflag[q] != 0u;
     if (over && a.cap < a.k) {  // too few to bound anything: straight to the fallback
       if (lane == 0) a.ovf[atomicAdd(a.novf, 1u)] = q;
       continue;
     }
-    const int n = over ? a.cap : (int)c;
+    const int n = min((int)c, a.cap);
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
     for (int j = lane; j < n2; j += 64) {
@@ -1527,20 +1528,24 @@ __global__ __launch_bounds__(64) void k_query_final(QFinalArgs a) {
     __syncthreads();
   }
 }
-// After the sample windows: every query's k-th best candidate so far (stored
+// Between window stages: every query's k-th best candidate so far (stored
 // entries, all real documents with exact scores) bounds its k-th best score
-// from below; if it beats the seed threshold it replaces it, so the remaining
-// windows keep far fewer documents.
+// from below; if it beats the threshold it replaces it, so the later stages
+// keep far fewer documents.  A list that overflowed lost candidates: its cap
+// stored entries still bound the threshold, it is compacted like the others
+// and flagged, so the final pass sends the query to another round (with the
+// threshold the later stages raised further).
 template <int CM>
-__global__ __launch_bounds__(64) void k_query_raise(int nq, int k, int cap, unsigned int *ccnt, double *cs,
-                                                    uint64_t *ck, double *th_s, uint64_t *th_k) {
+__global__ __launch_bounds__(64) void k_query_raise(int nq, int k, int cap, unsigned int *ccnt, unsigned int *oflag,
+                                                    double *cs, uint64_t *ck, double *th_s, uint64_t *th_k) {
   __shared__ double bs[CM];
   __shared__ uint64_t bk[CM];
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < nq; q += gridDim.x) {
     const unsigned int c = ccnt[q];
-    if (c > (unsigned int)cap || (int)c < k) continue;  // overflowed (re-run later) or too few to bound
-    const int n = (int)c;
+    const bool over = c > (unsigned int)cap;
+    const int n = over ? cap : (int)c;
+    if (n < k) continue;  // too few to bound (cap >= k here)
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
     for (int j = lane; j < n2; j += 64) {
@@ -1558,6 +1563,7 @@ __global__ __launch_bounds__(64) void k_query_raise(int nq, int k, int cap, unsi
     }
     if (lane == 0) {
       ccnt[q] = (unsigned int)k;
+      if (over) oflag[q] = 1u;
       if (up) {
         th_s[q] = bs[k - 1];
         th_k[q] = bk[k - 1];
@@ -1566,8 +1572,11 @@ __global__ __launch_bounds__(64) void k_query_raise(int nq, int k, int cap, unsi
     __syncthreads();
   }
 }
-__global__ void k_reset_cnt(const int32_t *qlist, int n, unsigned int *ccnt) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) ccnt[qlist[i]] = 0;
+__global__ void k_reset_cnt(const int32_t *qlist, int n, unsigned int *ccnt, unsigned int *oflag) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    ccnt[qlist[i]] = 0;
+    oflag[qlist[i]] = 0;
+  }
 }
 
 // impact rows from tf rows: q(tf) = floor(lut[tf] * idf * alpha) + 1 (0 for tf = 0)
@@ -1939,12 +1948,12 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     // exact ties at the k-th score), at most kCandMax
     const int cap = (int)std::min<int64_t>(std::max<int64_t>(cx->opt_cand_cap, cx->opt_cand_cap >= 1024 ? 16 * (int64_t)k : 0),
                                            kCandMax);
-    unsigned int *ccnt = W[42].as<unsigned int>(nq + 1);
+    unsigned int *ccnt = W[42].as<unsigned int>(2 * (size_t)nq + 1);
     double *cs = W[43].as<double>((size_t)nq * cap);
     uint64_t *ckk = W[61].as<uint64_t>((size_t)nq * cap);
     int32_t *ovf = W[62].as<int32_t>(2 * (size_t)nq + 2);
-    unsigned int *novf = ccnt + nq;
-    SME_HIP(hipMemsetAsync(ccnt, 0, (nq + 1) * sizeof(unsigned int), st));
+    unsigned int *novf = ccnt + nq, *oflag = ccnt + nq + 1;
+    SME_HIP(hipMemsetAsync(ccnt, 0, (2 * (size_t)nq + 1) * sizeof(unsigned int), st));
     QWinArgs wa;
     wa.desc = qdesc;
     wa.qpos = qpos;
@@ -1975,28 +1984,37 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
 #ifdef SME_EXPERIMENTS
     if (const char *qx = getenv("SME_QEXP")) wa.exper = atoi(qx);  // timing only: wrong results
 #endif
-    QFinalArgs fa{nullptr, nq, k, cap, ccnt, cs, ckk, d_out_docno, d_out_score, d_out_tie, th0, thk, ovf, novf};
+    QFinalArgs fa{nullptr, nq, k, cap, ccnt, oflag, cs, ckk, d_out_docno, d_out_score, d_out_tie, th0, thk, ovf, novf};
     int n_round = nq;
     const int32_t *round_list = nullptr;
     // window lists: every 8th window (sample), the rest
     const int64_t nwin = wa.nwin;
     int32_t *wl = W[30].as<int32_t>(nwin + 1);
-    int64_t n_samp = 0, stage_start[5] = {0, 0, 0, 0, 0};
+    // stages: the first two windows (under deep exact ties at the k-th score the
+    // docno tie-break makes the docno prefix decisive) and every 2^L-th window,
+    // then the windows 2^(L-1) mod 2^L, ..., then the odd ones -- 1/2^L, 1/2^L,
+    // 1/2^(L-1), ..., 1/2 of the windows, each stage after a raise (and a
+    // compaction) of every query's threshold and list.  Each stage doubles the
+    // windows seen, so it appends about k documents over the raised threshold;
+    // only the first one runs on the seed threshold, and L makes it small (about
+    // 16 windows, 1/8 .. 1/64 of the index).
+    int L = 3;
+    while (L < 6 && (nwin >> (L + 1)) >= 16) L++;
+    int64_t n_samp = 0, stage_start[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     {
       std::vector<int32_t> &h = cx->h_wlist;  // outlives the async copy
       h.assign((size_t)nwin, 0);
-      // stages: the first two windows (under deep exact ties at the k-th score
-      // the docno tie-break makes the docno prefix decisive) and every 8th, then
-      // the windows 4 mod 8, then 2 mod 4, then the odd ones -- 1/8, 1/8, 1/4,
-      // 1/2 of the windows, each stage after a raise (and a compaction) of every
-      // query's threshold and list
-      auto stage_of = [](int64_t xw) { return (xw < 2 || xw % 8 == 0) ? 0 : xw % 8 == 4 ? 1 : xw % 4 == 2 ? 2 : 3; };
-      for (int sg = 0; sg < 4; sg++) {
+      auto stage_of = [L](int64_t xw) {
+        if (xw < 2) return 0;
+        const int t = __builtin_ctzll((unsigned long long)xw);
+        return t >= L ? 0 : L - t;
+      };
+      for (int sg = 0; sg <= L; sg++) {
         stage_start[sg] = n_samp;
         for (int64_t xw = 0; xw < nwin; xw++)
           if (stage_of(xw) == sg) h[(size_t)n_samp++] = (int32_t)xw;
       }
-      stage_start[4] = n_samp;
+      stage_start[L + 1] = n_samp;
       SME_HIP(hipMemcpyAsync(wl, h.data(), nwin * sizeof(int32_t), hipMemcpyHostToDevice, st));
     }
     auto launch_win = [&](const int32_t *wlist, int64_t nw) {
@@ -2011,21 +2029,21 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     for (int round = 0; round < kWinRounds && n_round > 0; round++) {
       if (round > 0) {
         hipLaunchKernelGGL(k_reset_cnt, dim3((unsigned)std::min((n_round + 255) / 256, 4096)), dim3(256), 0, st,
-                           round_list, n_round, ccnt);
+                           round_list, n_round, ccnt, oflag);
         hipLaunchKernelGGL(k_query_pos, dim3((unsigned)std::min((n_round + 255) / 256, 8192)), dim3(256), 0, st,
                            round_list, d_qoff, n_round, qpos);
       }
       wa.nq = n_round;
       wa.nslices = (int)std::max<int64_t>(1, std::min<int64_t>(n_round / cx->opt_win_slice, 4096));
       if (round == 0 && cx->opt_win_sample && nwin >= 16) {
-        for (int sg = 0; sg < 4; sg++) {
+        for (int sg = 0; sg <= L; sg++) {
           if (sg > 0) {  // raise thresholds, keep each list's best k
             if (cap <= 1024)
               hipLaunchKernelGGL(k_query_raise<1024>, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, nq, k,
-                                 cap, ccnt, cs, ckk, th0, thk);
+                                 cap, ccnt, oflag, cs, ckk, th0, thk);
             else
               hipLaunchKernelGGL(k_query_raise<kCandMax>, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, nq,
-                                 k, cap, ccnt, cs, ckk, th0, thk);
+                                 k, cap, ccnt, oflag, cs, ckk, th0, thk);
             SME_CHECK_LAUNCH();
           }
           launch_win(wl + stage_start[sg], stage_start[sg + 1] - stage_start[sg]);
