@@ -1042,6 +1042,29 @@ __global__ void k_query_pos(const int32_t *qorder, const int64_t *qoff, int nq, 
     out[p] = QPos{qoff[q], q, (int32_t)(qoff[q + 1] - qoff[q])};
   }
 }
+// Streamed records (term / position records, thresholds): every window pass
+// reads the whole batch's once, with no reuse inside the pass, so they are
+// loaded non-temporally and do not evict the window's index rows from L2.
+typedef uint32_t qu32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ QDesc ld_desc_nt(const QDesc *d, int64_t q0, int nt, int lane) {
+  if (lane < nt) {
+    const qu32x4 *p = reinterpret_cast<const qu32x4 *>(d + q0 + lane);
+    const qu32x4 u = __builtin_nontemporal_load(p), v = __builtin_nontemporal_load(p + 1);
+    QDesc r;
+    r.mb = (int64_t)(((uint64_t)u.y << 32) | u.x);
+    r.mdf = (int32_t)u.z;
+    r.brow = (int32_t)u.w;
+    r.hr = (int32_t)v.x;
+    r.pad = (int32_t)v.y;
+    r.idf = __longlong_as_double((long long)(((uint64_t)v.w << 32) | v.z));
+    return r;
+  }
+  return QDesc{0, 0, 0, -1, 0, 0.0};
+}
+__device__ __forceinline__ QPos ld_pos_nt(const QPos *p) {
+  const qu32x4 u = __builtin_nontemporal_load(reinterpret_cast<const qu32x4 *>(p));
+  return QPos{(int64_t)(((uint64_t)u.y << 32) | u.x), (int32_t)u.z, (int32_t)u.w};
+}
 __device__ __forceinline__ QDesc ld_desc(const QDesc *d, int64_t q0, int nt, int lane) {
   if (lane < nt) return d[q0 + lane];
   return QDesc{0, 0, 0, -1, 0, 0.0};
@@ -1206,17 +1229,17 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
   if (pos >= p_hi) return;
   // software pipeline over this wave's queries: the next query's position
   // record, term records, threshold and skip entries load while this one runs
-  QPos P = a.qpos[pos];
-  QDesc D = ld_desc(a.desc, P.q0, P.nt, lane);
-  double th0 = a.th0[P.q];
-  uint64_t thk = a.thk[P.q];
+  QPos P = ld_pos_nt(a.qpos + pos);
+  QDesc D = ld_desc_nt(a.desc, P.q0, P.nt, lane);
+  double th0 = __builtin_nontemporal_load(a.th0 + P.q);
+  uint64_t thk = __builtin_nontemporal_load(a.thk + P.q);
   int32_t mc = 0, me = 0;
   if (D.mdf > 0 && D.hr < 0) {
     mc = a.skt[x * a.nrows + D.brow];
     me = a.skt[(x + 1) * a.nrows + D.brow];
   }
   QPos NP{0, 0, 0};  // next query's position record, loaded a pair ahead
-  if (pos + kWNT / 64 < p_hi) NP = a.qpos[pos + kWNT / 64];
+  if (pos + kWNT / 64 < p_hi) NP = ld_pos_nt(a.qpos + pos + kWNT / 64);
   for (;;) {
     const int npos = pos + kWNT / 64;
     const bool hasn = npos < p_hi;
@@ -1226,13 +1249,18 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
     uint64_t nthk = kNoKey;
     QPos NNP{0, 0, 0};
     if (hasn) {
-      ND = ld_desc(a.desc, NP.q0, NP.nt, lane);
-      nth0 = a.th0[NP.q];
-      nthk = a.thk[NP.q];
-      if (npos + kWNT / 64 < p_hi) NNP = a.qpos[npos + kWNT / 64];
+      ND = ld_desc_nt(a.desc, NP.q0, NP.nt, lane);
+      nth0 = __builtin_nontemporal_load(a.th0 + NP.q);
+      nthk = __builtin_nontemporal_load(a.thk + NP.q);
+      if (npos + kWNT / 64 < p_hi) NNP = ld_pos_nt(a.qpos + npos + kWNT / 64);
     }
+#ifdef SME_EXPERIMENTS  // timing switches: 4 = no sparse terms, 8 = no heavy terms
+    const uint64_t hm = (a.exper & 8) ? 0ull : (uint64_t)__ballot(D.hr >= 0);
+    const uint64_t sm = (a.exper & 4) ? 0ull : (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
+#else
     const uint64_t hm = (uint64_t)__ballot(D.hr >= 0);
     const uint64_t sm = (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
+#endif
     const uint32_t gate = gate_of(th0, a.alpha);
     // heavy terms' block maxima: one dword per term = the impact bound of this
     // lane's four 16-document blocks (index-resident bmq rows), all loads in flight

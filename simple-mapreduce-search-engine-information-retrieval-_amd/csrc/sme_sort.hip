@@ -37,7 +37,20 @@ constexpr int kRsWaveItems = 64 * kRsIPL;   // 1024 contiguous items per wave
 constexpr int kRsMaxBits = 11;
 constexpr int kRsMaxBins = 1 << kRsMaxBits;
 constexpr int kRsBPT = kRsMaxBins / kRsNT;  // digits per thread in the scatter's tile scan
-constexpr int kRsGroups = 256;              // tile groups of the column scan
+constexpr int kRsGroups = 256;              // most tile groups of the column scan
+
+// Tile groups of the column scan: at least 4 tiles a group, so the one-block
+// scan over (digit, group) sums stays short for small sorts; a multiple of 16
+// (the scan's granule; groups past the last tile sum to 0).
+struct RsGroups {
+  int64_t tpg;
+  int G;
+};
+static RsGroups rs_groups(int64_t ntiles) {
+  const int64_t tpg = std::max<int64_t>(4, (ntiles + kRsGroups - 1) / kRsGroups);
+  const int64_t g = (ntiles + tpg - 1) / tpg;
+  return RsGroups{tpg, (int)((g + 15) / 16 * 16)};
+}
 
 // Gather mode (first pass after the single-pass aggregation): pair x of the
 // docno order lives in the region of the record i holding it,
@@ -143,37 +156,43 @@ __global__ __launch_bounds__(kRsNT) void k_rs_count(const uint32_t *__restrict__
 
 // gsum[b * G + g] = sum of counts[t][b] over the tiles t of group g
 __global__ __launch_bounds__(kRsNT) void k_rs_colsum(const uint32_t *__restrict__ counts, int64_t ntiles, int nbins,
-                                                     int64_t tpg, uint32_t *__restrict__ gsum) {
+                                                     int64_t tpg, int G, uint32_t *__restrict__ gsum) {
   const int g = blockIdx.x;
   const int64_t ta = (int64_t)g * tpg, tb = min(ntiles, ta + tpg);
   for (int b = threadIdx.x; b < nbins; b += kRsNT) {
     uint32_t s = 0;
     for (int64_t t = ta; t < tb; t++) s += counts[t * nbins + b];
-    gsum[(int64_t)b * kRsGroups + g] = s;
+    gsum[(int64_t)b * G + g] = s;
   }
 }
 
 // in-place exclusive scan of n u32 (one block; n a multiple of 16): rounds
-// of 16384, 16 contiguous elements per thread (four 16-byte loads)
+// of 8192, 16 contiguous elements per thread (four 16-byte loads); the next
+// round's loads are issued before this round's barriers (latency-bound kernel)
 __global__ __launch_bounds__(kRsNT) void k_rs_scan(uint32_t *__restrict__ a, int n) {
   __shared__ uint32_t ws[kRsWaves];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t carry = 0;
+  uint4 x[4];
+  auto load = [&](int r0, uint4 *y) {
+    const int i0 = r0 + 16 * tid;
+#pragma unroll
+    for (int c = 0; c < 4; c++) y[c] = i0 < n ? reinterpret_cast<const uint4 *>(a + i0)[c] : make_uint4(0, 0, 0, 0);
+  };
+  load(0, x);
   for (int r0 = 0; r0 < n; r0 += 16 * kRsNT) {
     const int i0 = r0 + 16 * tid;
-    uint4 x[4];
     uint32_t s = 0;
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      x[c] = i0 < n ? reinterpret_cast<const uint4 *>(a + i0)[c] : make_uint4(0, 0, 0, 0);
-      s += x[c].x + x[c].y + x[c].z + x[c].w;
-    }
+    for (int c = 0; c < 4; c++) s += x[c].x + x[c].y + x[c].z + x[c].w;
     uint32_t incl = s;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(incl, o, 64);
       if (lane >= o) incl += u;
     }
     if (lane == 63) ws[w] = incl;
+    uint4 xn[4];
+    load(r0 + 16 * kRsNT, xn);
     __syncthreads();
     uint32_t wb = carry, tot = 0;
     for (int j = 0; j < kRsWaves; j++) {
@@ -199,16 +218,18 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scan(uint32_t *__restrict__ a, int
     }
     carry += tot;
     __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; c++) x[c] = xn[c];
   }
 }
 
 // counts[t][b] <- global offset of digit b's items of tile t
 __global__ __launch_bounds__(kRsNT) void k_rs_colscan(uint32_t *__restrict__ counts, int64_t ntiles, int nbins,
-                                                      int64_t tpg, const uint32_t *__restrict__ gsum) {
+                                                      int64_t tpg, int G, const uint32_t *__restrict__ gsum) {
   const int g = blockIdx.x;
   const int64_t ta = (int64_t)g * tpg, tb = min(ntiles, ta + tpg);
   for (int b = threadIdx.x; b < nbins; b += kRsNT) {
-    uint32_t run = gsum[(int64_t)b * kRsGroups + g];
+    uint32_t run = gsum[(int64_t)b * G + g];
     for (int64_t t = ta; t < tb; t++) {
       const uint32_t c = counts[t * nbins + b];
       counts[t * nbins + b] = run;
@@ -525,7 +546,9 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
   bits = std::max(bits, 1);
   const int npass = (bits + kRsMaxBits - 1) / kRsMaxBits;
   const int64_t ntiles = (P + kRsTile - 1) / kRsTile;
-  const int64_t tpg = (ntiles + kRsGroups - 1) / kRsGroups;
+  const RsGroups rg = rs_groups(ntiles);
+  const int64_t tpg = rg.tpg;
+  const int G = rg.G;
   uint32_t *gsum = counts + ntiles * kRsMaxBins;
   Gather g0{nullptr, nullptr, nullptr, 0};
   if (reg != nullptr) {
@@ -542,9 +565,9 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
     const int nbins = 1 << nb;
     const bool last = p == npass - 1;
     hipLaunchKernelGGL(k_rs_count, dim3((unsigned)ntiles), dim3(kRsNT), 0, st, k0, P, shift, nbins, counts, g);
-    hipLaunchKernelGGL(k_rs_colsum, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
-    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, nbins * kRsGroups);
-    hipLaunchKernelGGL(k_rs_colscan, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
+    hipLaunchKernelGGL(k_rs_colsum, dim3(G), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, G, gsum);
+    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, nbins * G);
+    hipLaunchKernelGGL(k_rs_colscan, dim3(G), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, G, gsum);
     const unsigned sgrid = (unsigned)(8 * ((ntiles + 7) / 8));  // see the XCD tile order in k_rs_scatter
     if (last)
       hipLaunchKernelGGL(k_rs_scatter<true>, dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, P, shift, nb, counts,
@@ -578,16 +601,18 @@ uint32_t *kv_sort(K *k0, uint32_t *v0, K *k1, uint32_t *v1, int64_t n, int bits,
   bits = std::min(std::max(bits, 1), (int)(8 * sizeof(K)));
   const int npass = (bits + kRsMaxBits - 1) / kRsMaxBits;
   const int64_t ntiles = (n + kRsTile - 1) / kRsTile;
-  const int64_t tpg = (ntiles + kRsGroups - 1) / kRsGroups;
+  const RsGroups rg = rs_groups(ntiles);
+  const int64_t tpg = rg.tpg;
+  const int G = rg.G;
   uint32_t *counts = scratch, *gsum = scratch + ntiles * kRsMaxBins;
   int shift = 0;
   for (int p = 0; p < npass; p++) {
     const int nb = (bits - shift + (npass - p) - 1) / (npass - p);
     const int nbins = 1 << nb;
     hipLaunchKernelGGL(k_kv_count<K>, dim3((unsigned)ntiles), dim3(kRsNT), 0, st, k0, n, shift, nbins, counts);
-    hipLaunchKernelGGL(k_rs_colsum, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
-    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, nbins * kRsGroups);
-    hipLaunchKernelGGL(k_rs_colscan, dim3(kRsGroups), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, gsum);
+    hipLaunchKernelGGL(k_rs_colsum, dim3(G), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, G, gsum);
+    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, nbins * G);
+    hipLaunchKernelGGL(k_rs_colscan, dim3(G), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, G, gsum);
     const unsigned sgrid = (unsigned)(8 * ((ntiles + 7) / 8));
     if (p == npass - 1 && !keys_out)
       hipLaunchKernelGGL((k_kv_scatter<K, false>), dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, n, shift, nb, counts,
