@@ -998,7 +998,8 @@ constexpr int kSList = 256;          // a window's sparse postings kept in LDS f
 constexpr int kSeedSlots = 1024;     // seed documents per query (LDS hash)
 constexpr int kCandMax = 2048;       // largest candidate list per query (final kernel LDS)
 constexpr int kWinRounds = 3;        // window passes before an overflowing query goes to k_query_bm
-constexpr int kCList = 512;          // documents over the gate listed per round of exact scoring
+constexpr int kCList = 128;          // documents over the gate listed per round of exact scoring
+constexpr int kWinLut = 128;         // k_query_win: 1 + ln(tf) for tf < 128 from LDS
 static_assert(kWDL == 64, "one lane owns 64 documents: four uint4 impact loads per heavy term");
 
 __device__ __forceinline__ uint32_t gate_of(double th0, double alpha) {
@@ -1204,16 +1205,17 @@ struct QWinArgs {
 };
 
 __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
+  // LDS: 9.8 KB per wave + the LUT = 40 KB per workgroup, four workgroups per CU
+  // (the VGPR limit of 4 waves per SIMD; LDS-bound occupancy 3 measured 26 % slower)
   __shared__ uint32_t lacc_all[kWNT / 64][kWin / 2];  // sparse impact sums, u16 pairs (see below)
   __shared__ uint32_t slist_all[kWNT / 64][kSList];   // the window's sparse postings: r | tf << 12
-  __shared__ uint32_t lblk_all[kWNT / 64][kWin / 16];  // sparse impact sums per 16-document block
   __shared__ uint16_t blist_all[kWNT / 64][kWin / 16];  // blocks over the gate
   __shared__ uint16_t clist_all[kWNT / 64][kCList];     // documents over the gate
-  __shared__ double s_lut[kLutLds];                    // 1 + ln(tf) for tf < 256
+  __shared__ double s_lut[kWinLut];                    // 1 + ln(tf) for tf < 128
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t *lacc = lacc_all[wv], *slist = slist_all[wv], *lblk = lblk_all[wv];
+  uint32_t *lacc = lacc_all[wv], *slist = slist_all[wv];
   uint16_t *blist = blist_all[wv], *clist = clist_all[wv];
-  for (int i = threadIdx.x; i < kLutLds; i += kWNT) s_lut[i] = i <= a.max_tf ? a.lut[i] : 0.0;
+  for (int i = threadIdx.x; i < kWinLut; i += kWNT) s_lut[i] = i <= a.max_tf ? a.lut[i] : 0.0;
   __syncthreads();
   // workgroup -> (window, query slice): the 8 XCDs (b % 8) on 8 windows, every
   // slice of one window on one XCD
@@ -1297,8 +1299,6 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
       // 32 words are a conflict-free column
 #pragma unroll
       for (int m = 0; m < kWDL / 2; m++) lacc[m * 64 + lane] = 0;
-#pragma unroll
-      for (int m = 0; m < 4; m++) lblk[m * 64 + lane] = 0;
       qwave_sync();
       const int64_t plo = D.mb + mc;
       for (int32_t e0 = 0; e0 < total; e0 += 64) {
@@ -1317,10 +1317,8 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
           const int32_t d = a.docno[pb + e], f = a.tf[pb + e];
           const int r = (int)((int64_t)d - wbase);
           // q(tf) computed here (the batch table would be a second dependent load)
-          const uint32_t qv = impact(f < kLutLds ? s_lut[f] : a.lut[f], wj, a.alpha);
+          const uint32_t qv = impact(f < kWinLut ? s_lut[f] : a.lut[f], wj, a.alpha);
           atomicAdd(&lacc[((r & 63) >> 1) * 64 + (r >> 6)], qv << ((r & 1) << 4));
-          // block b = r >> 4 of lane b >> 2: lblk[(b & 3) * 64 + (b >> 2)]
-          atomicAdd(&lblk[((r >> 4) & 3) * 64 + (r >> 6)], qv);
           if (listed) slist[e] = (uint32_t)r | ((uint32_t)min(f, 0xFFFFF) << 12);
         }
       }
@@ -1335,8 +1333,18 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
     // blocks over the gate: heavy maxima + the block's sparse impact sum
     uint32_t ub[4] = {ub0 & 0xFFFFu, ub0 >> 16, ub1 & 0xFFFFu, ub1 >> 16};
     if (total > 0) {
+      // + the largest sparse sum of each block's documents (lane l's column of
+      // lacc: documents 64 l .. 64 l + 63, block m = words 8 m .. 8 m + 7)
 #pragma unroll
-      for (int m = 0; m < 4; m++) ub[m] += lblk[m * 64 + lane];
+      for (int m = 0; m < 4; m++) {
+        uint32_t mx = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const uint32_t v = lacc[(8 * m + i) * 64 + lane];
+          mx = max(mx, max(v & 0xFFFFu, v >> 16));
+        }
+        ub[m] += mx;
+      }
     }
     uint32_t bm = 0;
 #pragma unroll
@@ -1458,7 +1466,7 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
                   f = (lo < e && a.docno[lo] == d) ? a.tf[lo] : 0;
                 }
                 if (f != 0) {
-                  S = __dadd_rn(S, __dmul_rn(f < kLutLds ? s_lut[f] : a.lut[f], rld(D.idf, j)));
+                  S = __dadd_rn(S, __dmul_rn(f < kWinLut ? s_lut[f] : a.lut[f], rld(D.idf, j)));
                   if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f);
                 }
               }
@@ -2051,7 +2059,13 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       const int64_t G = 8 * (int64_t)wa.nslices;
       const int64_t wg = ((nw + 7) / 8) * G;
       if (wg >= (int64_t(1) << 31)) throw Error(SME_ELIMIT, "query batch x windows too large for one launch");
-      if (wg > 0) hipLaunchKernelGGL(k_query_win, dim3((unsigned)wg), dim3(kWNT), 0, st, wa);
+      size_t dyn_lds = 0;
+#ifdef SME_EXPERIMENTS
+      // occupancy experiments: unused dynamic LDS per workgroup lowers the
+      // workgroups per CU without changing the kernel's code
+      if (const char *ql = getenv("SME_QLDS")) dyn_lds = (size_t)atoi(ql);
+#endif
+      if (wg > 0) hipLaunchKernelGGL(k_query_win, dim3((unsigned)wg), dim3(kWNT), dyn_lds, st, wa);
       SME_CHECK_LAUNCH();
     };
     for (int round = 0; round < kWinRounds && n_round > 0; round++) {
