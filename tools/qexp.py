@@ -7,7 +7,7 @@ first one's (docnos + score bits).  With an experiment build
 (SME_LIB_PATH=.../libsme_exp.so, compiled with -DSME_EXPERIMENTS) SME_QSTATS=1
 makes the kernel print its visit counters.
     python tools/qexp.py [--docs N] [--queries Q] [--k K] [--config c2|c5] \
-        [--opts "heavy_div=32,seed_tiles=4;heavy_div=0"]
+        [--opts "heavy_div=64,seed_tiles=4;heavy_div=0"]
 """
 import argparse
 import importlib
@@ -85,7 +85,7 @@ def main():
                           "split": {x: prof.get(x) for x in ("query_seed", "query_final", "query_overflow",
                                                              "query_total") if x in prof}}), flush=True)
         for n in opts:  # restore defaults
-            ctx.set_option(n.strip(), {"heavy_div": 32, "seed_tiles": 4, "query_order": 1, "query_kernel": 0,
+            ctx.set_option(n.strip(), {"heavy_div": 64, "seed_tiles": 4, "query_order": 1, "query_kernel": 0,
                                        "cand_cap": 1024, "seed_m": 64, "win_slice": 512, "win_sample": 1}[n.strip()])
     ix.close()
     ctx.close()
