@@ -1,0 +1,105 @@
+"""df exchange (dist.global_df_index) at c4 vocabulary size, on one GPU.
+
+c4 is 50 M docs doc-sharded over 8 GPUs: one shard is 6.25 M docs of
+the c4 distribution (V_w = 2^22, 200-360 tokens, Zipf s = 1, seed 44) with about
+6.8 M local terms (the words it holds + its 6.25 M docid terms).  This builds
+such a shard in HBM, runs the real global_df_index on a world-1 RCCL group
+(fingerprints + offsets, gather, unique, reduce), and then times the part that
+grows with the world on the device: torch.unique + index_add + gather over the
+8-shard gathered fingerprint set, emulated from this shard's own fingerprints
+(rows with df > 1 -- the words -- shared by all 8 shards, the df = 1 rows --
+docid terms and rare words -- made shard-private by xoring the shard number
+into the fingerprint).  The all-gather itself needs 8 GPUs; its volume is
+reported.  Writes profiles/r03_dfx_c4.json.
+    python tools/dfx_c4.py [--docs 6250000] [--world 8]
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "simple-mapreduce-search-engine-information-retrieval-_amd"
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--docs", type=int, default=6_250_000)
+    p.add_argument("--world", type=int, default=8)
+    a = p.parse_args()
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29561")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    sme = importlib.import_module(PKG)
+    D = importlib.import_module(PKG + ".dist")
+    synth = importlib.import_module(PKG + ".synth")
+    t0 = time.perf_counter()
+    corpus = sme.DeviceCorpus(a.docs, V=1 << 22, seed=44, len_lo=200, len_hi=360)
+    ctx = sme.Context(1, 1, 1)
+    ctx.load_docno_mapping(synth.mapping_bytes(a.docs))
+    ix = ctx.build_device(corpus.ptr, corpus.nbytes)
+    torch.cuda.synchronize()
+    print("shard built: N=%d V=%d P=%d (%.1f s)" % (ix.N, ix.V, ix.P, time.perf_counter() - t0), flush=True)
+    out = {"shard_docs": a.docs, "text_bytes": int(corpus.nbytes), "local_terms": int(ix.V), "postings": int(ix.P)}
+    runs = []
+    for _ in range(3):
+        t = {}
+        ts = time.perf_counter()
+        gdf = D.global_df_index(ix, timings=t)
+        t["total_ms"] = (time.perf_counter() - ts) * 1e3
+        runs.append(t)
+    out["world1_global_df_index"] = runs[-1]
+    # emulated world-W gather: the device-side dedup that grows with the world
+    V = int(ix.V)
+    fp = torch.empty((V, 2), dtype=torch.int64, device="cuda")
+    ix.term_fingerprints(fp.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    o_ptr, _, _ = ix.device_arrays()
+    offs = torch.empty(V + 1, dtype=torch.int64, device="cuda")
+    sme.memcpy(offs.data_ptr(), o_ptr, 8 * (V + 1), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    df = offs[1:] - offs[:-1]
+    private = df == 1
+    parts = []
+    for s in range(a.world):
+        f = fp.clone()
+        f[private, 1] ^= (s + 1) << 40
+        parts.append(f)
+    allfp = torch.cat(parts, 0)
+    del parts
+    times = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        uniq, inv = torch.unique(allfp, dim=0, return_inverse=True)
+        mine = inv[:V]
+        g = torch.zeros(uniq.shape[0], dtype=torch.int64, device="cuda")
+        g.index_add_(0, mine, df)
+        res = g[mine].contiguous()
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - ts) * 1e3)
+    out["emulated_world"] = a.world
+    out["emulated_gathered_terms"] = int(allfp.shape[0])
+    out["emulated_global_terms"] = int(uniq.shape[0])
+    out["emulated_unique_reduce_ms"] = round(min(times), 3)
+    out["all_gather_bytes_per_rank"] = int(a.world * V * 16)
+    out["private_terms"] = int(private.sum().item())
+    out["what"] = ("world-1 global_df_index at c4 shard size (real path), then torch.unique + index_add + gather "
+                   "over an emulated %d-shard fingerprint set (df>1 rows shared, df=1 rows shard-private); the "
+                   "all-gather needs %d GPUs and is reported as bytes" % (a.world, a.world))
+    del res, gdf
+    print(json.dumps(out), flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "dfx_c4.json"), "w"), indent=1)
+    ix.close()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -12,4 +12,6 @@ rm -rf $R/gpurun_out/prof $R/gpurun_out/pmc_f $R/gpurun_out/pmc_w
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-docs 0 --no-checks --no-e2e > $R/gpurun_out/bench_prof.log 2>&1 || { echo PROF_FAIL; tail -20 $R/gpurun_out/bench_prof.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_tok_fast|k_query_win|k_query_seed" --output-format csv -d $R/gpurun_out/pmc_f -o run -- python3 $R/bench.py --steps 1 --warmup 1 --cpu-docs 0 --no-checks --no-e2e > $R/gpurun_out/pmc_f.log 2>&1 || { echo PMC_F_FAIL; tail -5 $R/gpurun_out/pmc_f.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_tok_fast|k_query_win|k_query_seed" --output-format csv -d $R/gpurun_out/pmc_w -o run -- python3 $R/bench.py --steps 1 --warmup 1 --cpu-docs 0 --no-checks --no-e2e > $R/gpurun_out/pmc_w.log 2>&1 || { echo PMC_W_FAIL; tail -5 $R/gpurun_out/pmc_w.log; exit 1; }
+rm -rf $R/gpurun_out/pmc_sq
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-include-regex "k_tok_fast|k_query_win" --output-format csv -d $R/gpurun_out/pmc_sq -o run -- python3 $R/bench.py --steps 1 --warmup 1 --cpu-docs 0 --no-checks --no-e2e > $R/gpurun_out/pmc_sq.log 2>&1 || { echo PMC_SQ_FAIL; tail -5 $R/gpurun_out/pmc_sq.log; exit 1; }
 echo MEASURE_OK
