@@ -343,7 +343,34 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     touched = 8 * int(df[tv].sum())
     t_k = (qk_ms * 1e-3) if qk_ms else dt
     qtr = pmc_traffic(kname, a, detail=True)
-    return {"metric": "top-%d queries/sec" % k, "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
+    uni = None
+    if dist is None:
+        try:
+            # c3's uniform-over-vocabulary variant (seed 8): same batch
+            # size and k, terms drawn uniformly over the index's term ids; timed
+            # after the headline batches, not part of `value`
+            tu, qu = synth.queries_by_df(df, a.queries, seed=8, uniform=True)
+            du, dq = torch.from_numpy(tu).cuda(), torch.from_numpy(qu).cuda()
+            ud, us = torch.empty_like(out_d), torch.empty_like(out_s)  # the headline batch's results stay for post_checks
+
+            def ustep():
+                ix.query_topk_device(du.data_ptr(), dq.data_ptr(), a.queries, k, ud.data_ptr(), us.data_ptr(), stream)
+            ustep()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(5):
+                ustep()
+            torch.cuda.synchronize()
+            du_ms = (time.perf_counter() - t1) / 5 * 1e3
+            up = ix.ctx.last_build_profile()
+            uni = {"value": round(a.queries / (du_ms * 1e-3), 1), "unit": "queries/s", "ms_per_batch": round(du_ms, 3),
+                   "kernel_ms": up.get("query_kernel"), "terms_per_query": "U{2..8} uniform over the %d term ids (seed 8)"
+                   % len(df), "what": "c3 uniform-vocabulary variant, 5 batches after the timed ones (not in value)"}
+            del du, dq, ud, us
+        except Exception as e:  # an extra measurement: never fails the bench line
+            uni = {"error": repr(e)[:200]}
+
+    return {"metric": "top-%d queries/sec" % k, "uniform_vocab": uni, "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
             "terms_per_query": "U{2..8} drawn by df (seed %d)" % a.cfg["qseed"], "ms_per_batch": round(dt * 1e3, 3),
             "prep_ms": qp_ms, "query_index_build_ms": round(qidx_ms, 3),
             "query_index_what": "once per index, not per batch: tf byte rows + 16/1024-doc block maxima of the "

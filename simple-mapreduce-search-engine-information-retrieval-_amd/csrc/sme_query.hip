@@ -1229,6 +1229,8 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
   const int64_t wbase = a.dmin + (x << kWinB);  // first docno of the window
   int pos = p_lo + wv;
   if (pos >= p_hi) return;
+#pragma unroll
+  for (int m = 0; m < kWDL / 2; m++) lacc[m * 64 + lane] = 0;
   // software pipeline over this wave's queries: the next query's position
   // record, term records, threshold and skip entries load while this one runs
   QPos P = ld_pos_nt(a.qpos + pos);
@@ -1296,10 +1298,7 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
     const bool listed = total <= kSList;  // else exact tf lookups search the global postings
     if (total > 0) {
       // lacc[m * 64 + l] holds documents 64 l + 2m (low), + 1 (high): lane l's
-      // 32 words are a conflict-free column
-#pragma unroll
-      for (int m = 0; m < kWDL / 2; m++) lacc[m * 64 + lane] = 0;
-      qwave_sync();
+      // 32 words are a conflict-free column (zero here: cleared after each pair)
       const int64_t plo = D.mb + mc;
       for (int32_t e0 = 0; e0 < total; e0 += 64) {
         const int32_t e = e0 + lane;
@@ -1492,6 +1491,17 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
       }
     }
     if (!hasn) break;
+    if (total > 0) {  // clear the sums this pair wrote: its listed documents' words, else all
+      if (listed) {
+        for (int32_t e = lane; e < total; e += 64) {
+          const int r = (int)(slist[e] & 0xFFFu);
+          lacc[((r & 63) >> 1) * 64 + (r >> 6)] = 0u;
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < kWDL / 2; m++) lacc[m * 64 + lane] = 0;
+      }
+    }
     qwave_sync();  // this wave's LDS is rewritten for the next query
     pos = npos;
     P = NP;
@@ -1884,10 +1894,9 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     int32_t *qi = W[45].as<int32_t>(2 * (size_t)nq);
     hipLaunchKernelGGL(k_query_keys, dim3(std::min((nq + 255) / 256, 4096)), dim3(256), 0, st, d_terms, d_qoff, nq, off,
                        V, qk, qi);
-    size_t tbb = 0;
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, qk, qk + nq, qi, qi + nq, nq, 0, 64, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cx->cub_tmp.get(tbb), tbb, qk, qk + nq, qi, qi + nq, nq, 0, 64, st));
-    qord = qi + nq;
+    uint32_t *rscr = W[35].as<uint32_t>(kv_sort_scratch(nq) / sizeof(uint32_t) + 1);
+    qord = reinterpret_cast<const int32_t *>(kv_sort<uint64_t>(qk, reinterpret_cast<uint32_t *>(qi), qk + nq,
+                                                               reinterpret_cast<uint32_t *>(qi + nq), nq, 64, rscr, st));
   }
   // events on the launch stream bracket the scoring kernel (bench.py roofline)
   hipEvent_t e0, e1, e2, e3;
@@ -2033,10 +2042,10 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     // compaction) of every query's threshold and list.  Each stage doubles the
     // windows seen, so it appends about k documents over the raised threshold;
     // only the first one runs on the seed threshold, and L makes it small (about
-    // 16 windows, 1/8 .. 1/64 of the index).
+    // 16 windows, 1/8 .. 1/256 of the index).
     int L = 3;
-    while (L < 6 && (nwin >> (L + 1)) >= 16) L++;
-    int64_t n_samp = 0, stage_start[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    while (L < 8 && (nwin >> (L + 1)) >= 16) L++;
+    int64_t n_samp = 0, stage_start[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     {
       std::vector<int32_t> &h = cx->h_wlist;  // outlives the async copy
       h.assign((size_t)nwin, 0);
