@@ -19,13 +19,22 @@ import sys
 
 
 def per_kernel(d, counter):
-    out = {}
+    """{kernel name: [value per dispatch]} in dispatch order.  SME_PMC_BATCHES=n keeps
+    only the dispatches before the (n+1)-th k_query_seed (the bench's headline query
+    batches: warm-up + timed; the uniform-vocabulary batches follow them)."""
+    rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter:
-                continue
-            name = r["Kernel_Name"]
-            out.setdefault(name, []).append(float(r["Counter_Value"]))
+        rows += [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    nb = int(os.environ.get("SME_PMC_BATCHES", "0"))
+    out, seeds = {}, 0
+    for r in rows:
+        name = r["Kernel_Name"]
+        if "k_query_seed" in name:
+            seeds += 1
+        if nb and seeds > nb and "k_query" in name:
+            continue
+        out.setdefault(name, []).append(float(r["Counter_Value"]))
     return out
 
 
