@@ -48,7 +48,7 @@ struct sme_ctx {
   int64_t opt_raw_load_pct = 40;  // "raw_load_pct": raw-vocabulary table load of the next build (10..90)
   int64_t opt_cand_cap = 1024;    // "cand_cap": candidate list per query of k_query_win (1..2048; >= 1024: at least 16 k)
   int64_t opt_seed_m = 64;        // "seed_m": seed postings per term (k_query_seed; 0 = no seed)
-  int64_t opt_win_slice = 512;    // "win_slice": queries per k_query_win workgroup slice (>= 1)
+  int64_t opt_win_slice = 256;    // "win_slice": queries per k_query_win workgroup slice (>= 1)
   int64_t opt_win_sample = 1;     // "win_sample": 1 = every 8th window first, thresholds raised, then the rest
   // pinned host staging of device -> host record copies into pageable caller
   // memory (sme_index_copy_records): two buffers, DMA into one while the host
