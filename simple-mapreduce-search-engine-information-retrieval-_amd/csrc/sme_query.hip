@@ -24,6 +24,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <functional>
+
 #include "sme_internal.hpp"
 #include "sme_text.hpp"
 
@@ -1022,6 +1024,58 @@ struct QPos {
   int32_t q, nt;
 };
 static_assert(sizeof(QDesc) == 32 && sizeof(QPos) == 16, "record sizes");
+// Window-granular skip table of the k_query_win path, built directly (no tile
+// table, no transpose): skt[w * nrows + row] = first posting (term-relative) of
+// the row's term in window w or later; skt[nwin * nrows + row] = df.  Change
+// points as in k_skip_fill, then a suffix minimum per row over the windows.
+__global__ __launch_bounds__(256) void k_skipw_fill(const int64_t *rpre, int64_t nrows, const int32_t *term_of_row,
+                                                    const int64_t *off, const int32_t *docno, int64_t dmin,
+                                                    int64_t nwin, int32_t *skt) {
+  const int64_t total = rpre[nrows];
+  for (int64_t x0 = (int64_t)blockIdx.x * kSkipChunk; x0 < total; x0 += (int64_t)gridDim.x * kSkipChunk) {
+    const int64_t x1 = x0 + kSkipChunk < total ? x0 + kSkipChunk : total;
+    int64_t lo = 0, hi = nrows;  // row of x0: rpre[lo] <= x0 < rpre[hi]
+    while (hi - lo > 1) {
+      const int64_t m = (lo + hi) >> 1;
+      if (rpre[m] <= x0) lo = m;
+      else hi = m;
+    }
+    int64_t row = lo, rb = rpre[row], re = rpre[row + 1], b = off[term_of_row[row]];
+    for (int64_t x = x0 + threadIdx.x; x < x1; x += blockDim.x) {
+      while (x >= re) {
+        row++;
+        rb = re;
+        re = rpre[row + 1];
+        b = off[term_of_row[row]];
+      }
+      const int64_t i = x - rb, n = re - rb;
+      const int64_t j = ((int64_t)docno[b + i] - dmin) >> kWinB;
+      const int64_t jp = i == 0 ? -1 : (((int64_t)docno[b + i - 1] - dmin) >> kWinB);
+      if (jp < j) skt[j * nrows + row] = (int32_t)i;
+      if (i == n - 1) skt[nwin * nrows + row] = (int32_t)n;
+    }
+  }
+}
+// one thread per row (neighbouring rows: neighbouring words), eight windows'
+// loads in flight at a time; rows with df = 0 are all zeros
+__global__ __launch_bounds__(256) void k_skipw_suffix(const int64_t *rdf, int64_t nrows, int64_t nwin, int32_t *skt) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
+    const bool empty = rdf[r] == 0;
+    int32_t v = 0x7FFFFFFF;
+    for (int64_t w1 = nwin + 1; w1 > 0; w1 -= 8) {
+      int32_t u[8];
+#pragma unroll
+      for (int c = 0; c < 8; c++) u[c] = w1 - 1 - c >= 0 ? skt[(w1 - 1 - c) * nrows + r] : 0;
+#pragma unroll
+      for (int c = 0; c < 8; c++) {
+        if (w1 - 1 - c < 0) break;
+        v = min(v, u[c]);
+        skt[(w1 - 1 - c) * nrows + r] = empty ? 0 : v;
+      }
+    }
+  }
+}
+
 __global__ void k_query_desc(const int32_t *terms, int64_t n, int64_t V, const int64_t *off, const double *idf,
                              const int32_t *row_of, const int32_t *hrow_of, QDesc *out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1826,6 +1880,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   const uint8_t *qlut = nullptr;
   int64_t nrows_b = 0;      // distinct batch terms (rows of the skip / impact tables)
   int32_t *skt = nullptr;   // k_query_win: window skip table, transposed
+  std::function<void()> build_sk;  // the tile skip table `sk` (k_query_bm), built on demand on the window path
   int h_mx = 0;
   if (tiled) {
     hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
@@ -1865,17 +1920,28 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           SME_HIP(hipMemsetAsync(rdf + nrows, 0, sizeof(int64_t), st));
           SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, rdf, rpre, (int)nrows + 1, st));
           SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, rdf, rpre, (int)nrows + 1, st));
-          SME_HIP(hipMemsetAsync(skw, 0x7F, (size_t)nrows * (T + 1) * sizeof(int32_t), st));
-          hipLaunchKernelGGL(k_skip_zero_rows, dim3((unsigned)std::min<int64_t>(nrows, 4096)), dim3(256), 0, st, rdf,
-                             nrows, T, skw);
-          hipLaunchKernelGGL(k_skip_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T, skw);
-          hipLaunchKernelGGL(k_skip_suffix, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 16384)), dim3(256), 0,
-                             st, nrows, T, skw);
+          // tile skip table (k_query_bm); the window path builds its window
+          // table directly and the tile table only if a query falls back
+          build_sk = [=]() {
+            SME_HIP(hipMemsetAsync(skw, 0x7F, (size_t)nrows * (T + 1) * sizeof(int32_t), st));
+            hipLaunchKernelGGL(k_skip_zero_rows, dim3((unsigned)std::min<int64_t>(nrows, 4096)), dim3(256), 0, st,
+                               rdf, nrows, T, skw);
+            hipLaunchKernelGGL(k_skip_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, T,
+                               skw);
+            hipLaunchKernelGGL(k_skip_suffix, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 16384)), dim3(256),
+                               0, st, nrows, T, skw);
+            SME_CHECK_LAUNCH();
+          };
           if (cx->opt_query_kernel == 0) {
             const int64_t nwin = T >> 2, ne = nrows * (nwin + 1);
             skt = W[31].as<int32_t>(ne);
-            hipLaunchKernelGGL(k_skip_win, dim3((unsigned)std::min<int64_t>((ne + 255) / 256, 65536)), dim3(256), 0,
-                               st, skw, nrows, T, nwin, skt);
+            SME_HIP(hipMemsetAsync(skt, 0x7F, (size_t)ne * sizeof(int32_t), st));
+            hipLaunchKernelGGL(k_skipw_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, nwin,
+                               skt);
+            hipLaunchKernelGGL(k_skipw_suffix, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 16384)),
+                               dim3(256), 0, st, rdf, nrows, nwin, skt);
+          } else {
+            build_sk();
           }
           // impact scale: the index's (prepare_queries), shared by every batch
           SME_HIP(hipMemcpyAsync(wmax, &ix->q_wmax_bits, sizeof(uint64_t), hipMemcpyHostToDevice, st));
@@ -2122,7 +2188,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       n_ovf += round == 0 ? n_round : 0;
       if (cap < k) break;  // no bound can be raised: every overflowed query to the fallback
     }
-    if (n_round > 0) {  // still overflowing: the block-max sweep
+    if (n_round > 0) {  // still overflowing: the block-max sweep (on the tile skip table)
+      if (build_sk) build_sk();
       QBmArgs ob = qa;
       ob.qorder = round_list;
       ob.nq = n_round;
