@@ -305,7 +305,18 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     # a one-off host stall of ~50 ms right after the timed region opens was seen
     # on the GPU box (cause not found: not GC, not the profile read); >= 5
     # batches amortise it like any other steady-state overhead (10 at least)
-    steps = max(10, a.steps)
+    # batches: at least 10 and enough for ~1.5 s of query work (a one-off stall
+    # then moves the mean by < 4 %), at most 50; every rank runs the same count
+    ts1 = time.perf_counter()
+    qstep()
+    torch.cuda.synchronize()
+    t_one = time.perf_counter() - ts1
+    if dist is not None:
+        tt1 = torch.tensor([t_one], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt1, op=dist.ReduceOp.MAX)
+        t_one = float(tt1.item())
+    barrier()
+    steps = max(a.steps, min(50, max(10, int(1.5 / max(t_one, 1e-6)))))
     kms, pms, kname = [], [], "k_query"
     t0 = time.perf_counter()
     walls = []
@@ -370,7 +381,7 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
         except Exception as e:  # an extra measurement: never fails the bench line
             uni = {"error": repr(e)[:200]}
 
-    return {"metric": "top-%d queries/sec" % k, "uniform_vocab": uni, "value": round(qps, 1), "unit": "queries/s", "queries": a.queries,
+    return {"metric": "top-%d queries/sec" % k, "uniform_vocab": uni, "value": round(qps, 1), "unit": "queries/s", "queries": a.queries, "batches": steps,
             "terms_per_query": "U{2..8} drawn by df (seed %d)" % a.cfg["qseed"], "ms_per_batch": round(dt * 1e3, 3),
             "prep_ms": qp_ms, "query_index_build_ms": round(qidx_ms, 3),
             "query_index_what": "once per index, not per batch: tf byte rows + 16/1024-doc block maxima of the "
