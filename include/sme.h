@@ -100,6 +100,17 @@ void sme_destroy(sme_ctx *ctx);
  *   "agg_two_pass"  1 count + emit aggregation passes (default 0: single pass)
  *   "tok_grid"      tokenizer workgroups, >= 1 (default 4096)
  *   "raw_load_pct"  raw-vocabulary table load of the next build, 10..90 (default 40)
+ *   "query_table_budget"  bytes a batch's skip table may take (default 0 =
+ *                   a quarter of the free HBM); a batch over it is split by
+ *                   query range, and queries still overflowing their
+ *                   candidate lists whose tile table does not fit run as their
+ *                   own compact batch -- every batch of queries of <= 64 terms
+ *                   is answered by the window-major scorer, for any k <= 448
+ *   "corpus_keep_bytes"  sme_build_index keeps its device copy of the host
+ *                   corpus for the next build (no hipMalloc) only up to this
+ *                   many bytes (default 16 GiB); larger copies are freed after
+ *                   the build, since HBM held there also shrinks the heavy-row
+ *                   budget of sme_index_prepare_queries (1/8 of free HBM)
  * Unknown names and out-of-range values are SME_EINVAL. */
 int sme_set_option(sme_ctx *ctx, const char *name, int64_t value);
 
@@ -220,9 +231,10 @@ int sme_query_topk_tie(sme_index *ix, const int32_t *term_ids, const int64_t *q_
 
 /* Query-side structures of an index (the role the reference's forward index,
  * BuildIntDocVectorsForwardIndex.java:84-158, plays for rank()): heavy-term tf
- * rows and block maxima for the block-max scorer.  Built once per index (tf
- * based: sme_index_reweight keeps them); sme_query_topk* builds them on first
- * use when this was not called.  *ms (may be NULL) gets the device time. */
+ * rows and block maxima for the block-max scorer.  Built once per index; the
+ * impact rows and their scale depend on idf, so sme_index_reweight DROPS them:
+ * call this after the last reweight (sme_query_topk* rebuilds them on first
+ * use otherwise, inside that call).  *ms (may be NULL) gets the device time. */
 int sme_index_prepare_queries(sme_index *ix, void *stream, float *ms);
 
 /* Same with all arrays already in device memory (timed path). */

@@ -265,11 +265,13 @@ class Index:
         self.close()
 
     def partition_records(self, part):
-        """Record bytes of reduce partition `part` (bytes; one D2H copy into them)."""
+        """Record bytes of reduce partition `part`, always as a bytearray (one D2H
+        copy into it; large partitions are not copied again into immutable bytes --
+        wrap with bytes() where an immutable/hashable object is needed)."""
         offs, _ = self.serialize()
         out = bytearray(int(offs[part + 1] - offs[part]))
         self.copy_records(part, out)
-        return bytes(out) if len(out) < (1 << 26) else out
+        return out
 
     def serialize(self):
         """Device serialization of every partition (once per index):

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include <algorithm>
+#include <system_error>
 #include <thread>
 
 #include "sme_internal.hpp"
@@ -174,12 +175,23 @@ void copy_d2h(sme_ctx *cx, void *dst, const void *d, size_t n, hipStream_t st) {
       const unsigned t = len >= (size_t(8) << 20) ? nth : 1u;
       const size_t per = (len + t - 1) / t;
       std::vector<std::thread> th;
+      struct Joiner {  // joins every started thread on any exit (a joinable std::thread's destructor aborts)
+        std::vector<std::thread> &v;
+        ~Joiner() {
+          for (auto &x : v)
+            if (x.joinable()) x.join();
+        }
+      } joiner{th};
       for (unsigned i = 1; i < t; i++) {
         const size_t lo = std::min(len, i * per), hi = std::min(len, lo + per);
-        if (hi > lo) th.emplace_back([=] { memcpy(out + lo, src + lo, hi - lo); });
+        if (hi <= lo) continue;
+        try {
+          th.emplace_back([=] { memcpy(out + lo, src + lo, hi - lo); });
+        } catch (const std::system_error &) {  // no thread (EAGAIN): copy this slice here
+          memcpy(out + lo, src + lo, hi - lo);
+        }
       }
       memcpy(out, src, std::min(len, per));
-      for (auto &x : th) x.join();
     }
   } catch (...) {
     (void)hipStreamSynchronize(st);
@@ -282,6 +294,12 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
     } else if (n == "seed_m") {
       range(0, 4096);
       cx->opt_seed_m = v;
+    } else if (n == "query_table_budget") {
+      range(0, int64_t(1) << 50);
+      cx->opt_query_budget = v;
+    } else if (n == "corpus_keep_bytes") {
+      range(0, int64_t(1) << 50);
+      cx->opt_corpus_keep = v;
     } else if (n == "raw_load_pct") {
       range(10, 90);
       cx->opt_raw_load_pct = v;
@@ -446,6 +464,9 @@ int sme_build_index(sme_ctx *cx, const uint8_t *corpus, size_t nbytes, sme_index
     if (nbytes) SME_HIP(hipMemcpyAsync(d, corpus, nbytes, hipMemcpyHostToDevice, st));
     sme_index *ix = sme::build_index(cx, d, nbytes, st);
     SME_HIP(hipStreamSynchronize(st));
+    // a large copy is not held for the context's lifetime: it would also shrink
+    // the HBM that sme_index_prepare_queries sizes its heavy rows from
+    if ((int64_t)nbytes > cx->opt_corpus_keep) cx->h_corpus_dev.release();
     cx->last_profile = ix->profile;
     *out = ix;
   });
@@ -699,7 +720,7 @@ int sme_last_build_profile(const sme_ctx *cx, const char **json) {
     if (cx->last_query_ms >= 0) os << ",\"query_kernel_name\":\"" << cx->last_query_name << "\"";
     if (cx->last_query_ms >= 0 && cx->last_query_name == std::string("k_query_win"))
       os << ",\"query_seed\":" << cx->last_query_seed_ms << ",\"query_final\":" << cx->last_query_final_ms
-         << ",\"query_overflow\":" << cx->last_query_overflow << ",\"query_fallback\":" << cx->last_query_fallback << ",\"query_total\":" << cx->last_query_total_ms;
+         << ",\"query_overflow\":" << cx->last_query_overflow << ",\"query_fallback\":" << cx->last_query_fallback << ",\"query_split\":" << (cx->last_query_split ? 1 : 0) << ",\"query_total\":" << cx->last_query_total_ms;
     os << "}";
     const_cast<sme_ctx *>(cx)->profile_json = os.str();
     *json = cx->profile_json.c_str();

@@ -725,9 +725,9 @@ constexpr int kTokCap = 2560;  // chunk tokens per round (a c2 chunk holds ~1950
 #define SME_TOKOCC 4
 #endif
 #ifndef SME_TOKG
-#define SME_TOKG 2
+#define SME_TOKG 8
 #endif
-constexpr int kTokG = SME_TOKG;  // tokens per lane step in the probe pass
+constexpr int kTokG = SME_TOKG;  // tokens per lane step in the probe pass (all their slot loads in flight)
 #ifndef SME_FASTPROBES
 #define SME_FASTPROBES 4
 #endif
@@ -875,6 +875,37 @@ __device__ __forceinline__ void tok_sig_at(const TokLds &L, const uint8_t *t, in
     g->w0 = s.w0;
     g->w1 = s.w1;
     len = s.len;
+  }
+  *len_o = len;
+}
+
+// Words and length of the token at chunk-relative x, without the hash: the probe
+// pass re-derives them from LDS after its slot loads return, so a token in
+// flight holds only its loaded slot words and slot index in registers.  len is
+// 99 for a token longer than 16 bytes (only the byte path knows its length).
+__device__ __forceinline__ void tok_words_at(const TokLds &L, int32_t x, uint64_t *w0, uint64_t *w1, int32_t *len_o) {
+  const int ln = x >> 6, bi = x & 63;
+  const uint64_t rest = L.emask[ln] >> bi >> 1;
+  int32_t len = 99;
+  if (rest) {
+    len = __ffsll((unsigned long long)rest);
+  } else if (ln + 1 < kTokNT) {
+    const uint64_t m = L.emask[ln + 1];
+    if (m) len = 64 - bi + __ffsll((unsigned long long)m) - 1;
+  }
+  if (len <= 16) {
+    const uint32_t *st32 = reinterpret_cast<const uint32_t *>(L.st4);
+    const int a = x >> 2, r = x & 3;
+    const uint32_t d0 = st32[a], d1 = st32[a + 1], d2 = st32[a + 2], d3 = st32[a + 3], d4 = st32[a + 4];
+    const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, r) |
+                        ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32);
+    const uint64_t hi = (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, r) |
+                        ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, r) << 32);
+    *w0 = len >= 8 ? lo : (lo & ((1ull << (8 * len)) - 1ull));
+    *w1 = len <= 8 ? 0ull : (len >= 16 ? hi : (hi & ((1ull << (8 * (len - 8))) - 1ull)));
+  } else {
+    *w0 = 0;
+    *w1 = 0;
   }
   *len_o = len;
 }
@@ -1080,46 +1111,69 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
         }
       }
       __syncthreads();
-      // pass 3: signature + raw-vocabulary slot, kTokG tokens per lane step (their
-      // home-slot loads in flight together)
+      // pass 3: raw-vocabulary slot of every token.  A lane holds up to kTokG
+      // tokens (a c2 chunk's ~1950 tokens are one step of 256 lanes) and all
+      // their home-slot loads are in flight together; the loaded words and the
+      // slot index are all a token keeps in registers (its words and length are
+      // re-read from LDS to compare).  Tokens whose home slot holds another
+      // token advance together, one slot per round, with plain loads (a slot,
+      // once filled, never changes); an empty-looking slot, a token of >= 16
+      // bytes or a long probe run take raw_insert.
       for (int32_t r0 = (texp & 1) ? nr : tid; r0 < nr; r0 += kTokG * kTokNT) {
-        TokSig g[kTokG];
-        int32_t len[kTokG], x[kTokG];
         ulonglong2 v[kTokG];
-#pragma unroll
-        for (int u = 0; u < kTokG; u++) {
-          const int32_t r = r0 + u * kTokNT;
-          x[u] = (int32_t)L.tl[r < nr ? r : r0];
-          tok_sig_at(L, t, c_lo, x[u], &g[u], &len[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < kTokG; u++)
-          v[u] = *reinterpret_cast<const ulonglong2 *>(&tb.slots[g[u].h & tb.mask].w0);
+        uint32_t sl[kTokG];
+        uint32_t live = 0, ins = 0;  // bit u: token u still probing / to raw_insert
 #pragma unroll
         for (int u = 0; u < kTokG; u++) {
           const int32_t r = r0 + u * kTokNT;
           if (r < nr) {
-            // linear probing over occupied slots of other tokens with plain
-            // loads (a slot, once filled, never changes); an empty-looking slot,
-            // a token of >= 16 bytes or a long probe run take raw_insert
-            uint64_t sl = g[u].h & tb.mask;
-            bool hit = slot_hit16(v[u], g[u], len[u]);
-            if (!hit && len[u] < 16 && v[u].x != 0) {
-              for (int pr = 1; pr < kFastProbes; pr++) {
-                const uint64_t s2 = (sl + pr) & tb.mask;
-                const ulonglong2 w = *reinterpret_cast<const ulonglong2 *>(&tb.slots[s2].w0);
-                if (slot_hit16(w, g[u], len[u])) {
-                  hit = true;
-                  sl = s2;
-                  break;
-                }
-                if (w.x == 0) break;
-              }
+            uint64_t w0, w1;
+            int32_t len;
+            tok_words_at(L, (int32_t)L.tl[r], &w0, &w1, &len);  // no calls while loads are in flight
+            if (len < 16) {
+              sl[u] = (uint32_t)(sig_head(w0, w1) & tb.mask);
+              v[u] = *reinterpret_cast<const ulonglong2 *>(&tb.slots[sl[u]].w0);
+              live |= 1u << u;
+            } else {
+              ins |= 1u << u;
             }
-            L.tl[r] = hit ? (uint32_t)sl
-                          : raw_insert(tb, g[u], (uint64_t)(c_lo + x[u]), (uint64_t)len[u], SlotVal{0, 0, 0, 0});
           }
         }
+        for (int pr = 0; pr < kFastProbes && live; pr++) {
+          if (pr > 0) {
+#pragma unroll
+            for (int u = 0; u < kTokG; u++)
+              if (live >> u & 1u) {
+                sl[u] = (uint32_t)((sl[u] + 1) & tb.mask);
+                v[u] = *reinterpret_cast<const ulonglong2 *>(&tb.slots[sl[u]].w0);
+              }
+          }
+#pragma unroll
+          for (int u = 0; u < kTokG; u++)
+            if (live >> u & 1u) {
+              const int32_t r = r0 + u * kTokNT;
+              uint64_t w0, w1;
+              int32_t len;
+              tok_words_at(L, (int32_t)L.tl[r], &w0, &w1, &len);
+              if (v[u].x == w0 && v[u].y == w1) {
+                L.tl[r] = sl[u];
+                live &= ~(1u << u);
+              } else if (v[u].x == 0) {
+                live &= ~(1u << u);
+                ins |= 1u << u;
+              }
+            }
+        }
+        ins |= live;
+        for (int u = 0; u < kTokG; u++)
+          if (ins >> u & 1u) {
+            const int32_t r = r0 + u * kTokNT;
+            const int32_t x = (int32_t)L.tl[r];
+            TokSig g;
+            int32_t len;
+            tok_sig_at(L, t, c_lo, x, &g, &len);
+            L.tl[r] = raw_insert(tb, g, (uint64_t)(c_lo + x), (uint64_t)len, SlotVal{0, 0, 0, 0});
+          }
       }
       __syncthreads();
       // pass 4: coalesced stores: chunk token i belongs to the last window record

@@ -37,6 +37,7 @@ struct sme_ctx {
   float last_query_seed_ms = 0.0f, last_query_final_ms = 0.0f, last_query_total_ms = 0.0f;
   int64_t last_query_overflow = 0;  // k_query_win queries whose first candidate list overflowed
   int64_t last_query_fallback = 0;  // of those, queries finally scored by k_query_bm
+  bool last_query_split = false;     // the batch was split by query range (table budget)
   // Path options (sme_set_option).  Every setting gives identical results; they
   // exist so tests can hold each path to the others and benches can sweep them.
   int64_t opt_query_kernel = 0;   // "query_kernel": 0 window-major (auto), 1 streaming k_query, 2 block-max sweep
@@ -50,6 +51,9 @@ struct sme_ctx {
   int64_t opt_seed_m = 64;        // "seed_m": seed postings per term (k_query_seed; 0 = no seed)
   int64_t opt_win_slice = 256;    // "win_slice": queries per k_query_win workgroup slice (>= 1)
   int64_t opt_win_sample = 1;     // "win_sample": 1 = every 8th window first, thresholds raised, then the rest
+  int64_t opt_query_budget = 0;  // "query_table_budget": per-batch skip-table bytes (0: a quarter of free HBM)
+  int64_t opt_corpus_keep = int64_t(16) << 30;  // "corpus_keep_bytes": host-corpus builds keep their device copy
+                                                // (no hipMalloc next build) only up to this size
   // pinned host staging of device -> host record copies into pageable caller
   // memory (sme_index_copy_records): two buffers, DMA into one while the host
   // copies out of the other

@@ -1848,6 +1848,52 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
   ix->q_ready = true;
 }
 
+// rows of a sub-batch's results back into the batch's output rows
+__global__ void k_scatter_rows(const int32_t *qlist, int n, int k, const int32_t *sd, const double *ss,
+                               const uint32_t *st_, int32_t *d, double *s, uint32_t *t) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (int64_t)n * k;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = qlist[i / k], j = i % k;
+    d[q * k + j] = sd[i];
+    s[q * k + j] = ss[i];
+    if (t) t[q * k + j] = st_[i];
+  }
+}
+
+namespace {
+struct QTimes {  // the per-call query timings of the context, summed over sub-batches
+  float ms = 0, prep = 0, seed = 0, fin = 0, tot = 0;
+  int64_t ovf = 0, fb = 0;
+  void add(const sme_ctx *cx) {
+    ms += cx->last_query_ms;
+    prep += cx->last_query_prep_ms;
+    seed += cx->last_query_seed_ms;
+    fin += cx->last_query_final_ms;
+    tot += cx->last_query_total_ms;
+    ovf += cx->last_query_overflow;
+    fb += cx->last_query_fallback;
+  }
+  void store(sme_ctx *cx) const {
+    cx->last_query_ms = ms;
+    cx->last_query_prep_ms = prep;
+    cx->last_query_seed_ms = seed;
+    cx->last_query_final_ms = fin;
+    cx->last_query_total_ms = tot;
+    cx->last_query_overflow = ovf;
+    cx->last_query_fallback = fb;
+  }
+};
+}  // namespace
+
+// Queries `qlist` (device, n entries: rows of this batch) as their own compact
+// batch, results scattered back into the batch's output rows.  The rare path
+// for queries whose candidate lists still overflow after the window rounds
+// when the batch's tile table does not fit in HBM: the subset's distinct terms
+// are few, so its own tables fit (a single query of <= 64 terms always does).
+static void query_subset(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, const int32_t *h_qlist,
+                         int n, int k, int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie,
+                         hipStream_t st);
+
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k, int32_t *d_out_docno,
                 double *d_out_score, uint32_t *d_out_tie, hipStream_t st) {
   if (k < 1) throw Error(SME_EINVAL, "k must be >= 1");
@@ -1885,17 +1931,18 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   if (tiled) {
     hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
     SME_HIP(hipMemcpyAsync(&h_mx, err + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-    int64_t nterm = 0;
+    int64_t nterm = 0, tbase = 0;  // the batch's terms are d_terms[tbase, nterm) (a sub-batch: tbase > 0)
     SME_HIP(hipMemcpyAsync(&nterm, d_qoff + nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipMemcpyAsync(&tbase, d_qoff, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
     tiled = h_mx <= kIMaxTerms;
     if (tiled) {
       // distinct batch terms -> rows of the skip and impact tables
       int32_t *mark = W[55].as<int32_t>(V + 1), *rowo = W[56].as<int32_t>(V + 1);
       SME_HIP(hipMemsetAsync(mark, 0, (V + 1) * sizeof(int32_t), st));
-      if (nterm > 0)
-        hipLaunchKernelGGL(k_mark_terms, dim3((unsigned)std::min<int64_t>((nterm + 255) / 256, 8192)), dim3(256), 0, st,
-                           d_terms, nterm, V, mark);
+      if (nterm > tbase)
+        hipLaunchKernelGGL(k_mark_terms, dim3((unsigned)std::min<int64_t>((nterm - tbase + 255) / 256, 8192)), dim3(256),
+                           0, st, d_terms + tbase, nterm - tbase, V, mark);
       size_t tbb = 0;
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, mark, rowo, (int)V + 1, st));
       SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, mark, rowo, (int)V + 1, st));
@@ -1904,13 +1951,32 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       SME_HIP(hipStreamSynchronize(st));
       const int64_t nrows = nrows32;
       nrows_b = nrows;
-      if ((double)nrows * (double)(T + 1) * 4.0 > 8.0e9) {
-        tiled = false;
-      } else {
+      // per-batch table budget: a quarter of the free HBM (plus the table
+      // buffer this context already holds); a batch over it is split by query
+      // range (each half has fewer distinct terms), so every batch of queries
+      // of <= 64 terms is answered on this path
+      size_t fr = 0, tot = 0;
+      SME_HIP(hipMemGetInfo(&fr, &tot));
+      const bool winp = cx->opt_query_kernel == 0;
+      const double need = (double)nrows * (double)((winp ? (T >> 2) : T) + 1) * 4.0;
+      const double budget = cx->opt_query_budget > 0 ? (double)cx->opt_query_budget
+                                                     : (double)fr / 4.0 + (double)W[winp ? 31 : 60].cap;
+      if (need > budget && nq > 1) {
+        SME_HIP(hipEventDestroy(ep));
+        QTimes acc;
+        const int h = nq / 2;
+        query_topk(ix, d_terms, d_qoff, h, k, d_out_docno, d_out_score, d_out_tie, st);
+        acc.add(cx);
+        query_topk(ix, d_terms, d_qoff + h, nq - h, k, d_out_docno + (int64_t)h * k, d_out_score + (int64_t)h * k,
+                   d_out_tie ? d_out_tie + (int64_t)h * k : nullptr, st);
+        acc.add(cx);
+        acc.store(cx);
+        cx->last_query_split = true;
+        return;
+      }
+      {  // (a single query's tables are always built: <= 64 rows)
         row_of = rowo;
-        int32_t *skw = W[60].as<int32_t>(std::max<int64_t>(nrows, 1) * (T + 1));
         uint8_t *ql = W[44].as<uint8_t>(std::max<int64_t>(nrows, 1) * 256);
-        sk = skw;
         qlut = ql;
         if (nrows > 0) {
           int32_t *tor = W[57].as<int32_t>(nrows + 1);
@@ -1922,7 +1988,9 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, rdf, rpre, (int)nrows + 1, st));
           // tile skip table (k_query_bm); the window path builds its window
           // table directly and the tile table only if a query falls back
-          build_sk = [=]() {
+          build_sk = [=, &W, &sk]() {
+            int32_t *skw = W[60].as<int32_t>(std::max<int64_t>(nrows, 1) * (T + 1));  // allocated on first use
+            sk = skw;
             SME_HIP(hipMemsetAsync(skw, 0x7F, (size_t)nrows * (T + 1) * sizeof(int32_t), st));
             hipLaunchKernelGGL(k_skip_zero_rows, dim3((unsigned)std::min<int64_t>(nrows, 4096)), dim3(256), 0, st,
                                rdf, nrows, T, skw);
@@ -1948,6 +2016,11 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           hipLaunchKernelGGL(k_row_qlut, dim3((unsigned)std::min<int64_t>(nrows, 16384)), dim3(256), 0, st, tor, nrows,
                              lut, ix->max_tf, idf, (const unsigned long long *)wmax, ql);
           SME_CHECK_LAUNCH();
+        }
+        if (!sk && !winp) {  // no valid term in the batch: an empty (all 'none') table row for k_query_bm
+          int32_t *skw = W[60].as<int32_t>(T + 1);
+          SME_HIP(hipMemsetAsync(skw, 0x7F, (size_t)(T + 1) * sizeof(int32_t), st));
+          sk = skw;
         }
       }
     }
@@ -2188,13 +2261,33 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       n_ovf += round == 0 ? n_round : 0;
       if (cap < k) break;  // no bound can be raised: every overflowed query to the fallback
     }
-    if (n_round > 0) {  // still overflowing: the block-max sweep (on the tile skip table)
-      if (build_sk) build_sk();
-      QBmArgs ob = qa;
-      ob.qorder = round_list;
-      ob.nq = n_round;
-      launch_bm(ob);
-      SME_CHECK_LAUNCH();
+    if (n_round > 0) {  // still overflowing: the block-max sweep (on the tile skip table) if it fits
+      size_t fr2 = 0, tot2 = 0;
+      SME_HIP(hipMemGetInfo(&fr2, &tot2));
+      const double tbudget = cx->opt_query_budget > 0 ? (double)cx->opt_query_budget
+                                                      : (double)fr2 / 2.0 + (double)W[60].cap;
+      if ((double)nrows_b * (double)(T + 1) * 4.0 <= tbudget || nq == 1) {
+        if (build_sk) build_sk();
+        QBmArgs ob = qa;
+        ob.sk = sk;
+        ob.qorder = round_list;
+        ob.nq = n_round;
+        launch_bm(ob);
+        SME_CHECK_LAUNCH();
+      } else {
+        // the list lives in this context's workspace, which the sub-batches reuse
+        std::vector<int32_t> hl((size_t)n_round);
+        SME_HIP(hipMemcpyAsync(hl.data(), round_list, n_round * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        SME_HIP(hipStreamSynchronize(st));
+        if (n_round < nq) {
+          query_subset(ix, d_terms, d_qoff, nq, hl.data(), n_round, k, d_out_docno, d_out_score, d_out_tie, st);
+        } else {  // every query of the batch: two compact halves (each recursion has fewer queries)
+          const int h = n_round / 2;
+          query_subset(ix, d_terms, d_qoff, nq, hl.data(), h, k, d_out_docno, d_out_score, d_out_tie, st);
+          query_subset(ix, d_terms, d_qoff, nq, hl.data() + h, n_round - h, k, d_out_docno, d_out_score, d_out_tie,
+                       st);
+        }
+      }
     }
     cx->last_query_fallback = n_round;
   } else if (tiled) {
@@ -2232,6 +2325,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   cx->last_query_index_ms = tiled ? ix->q_prep_ms : 0.0f;
   cx->last_query_tiled = tiled;
   cx->last_query_name = win ? "k_query_win" : tiled ? "k_query_bm" : "k_query";
+  cx->last_query_split = false;
   (void)hipEventDestroy(ep);
   for (hipEvent_t e : {e0, e1, e2, e3}) (void)hipEventDestroy(e);
   if (qstats) {
@@ -2246,6 +2340,41 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
               (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3]);
   }
   if (h_err) throw Error(SME_ELIMIT, "a query has more than 128 terms");
+}
+
+static void query_subset(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, const int32_t *h_qlist,
+                         int n, int k, int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie,
+                         hipStream_t st) {
+  const std::vector<int32_t> ql(h_qlist, h_qlist + n);
+  std::vector<int64_t> qo((size_t)nq + 1);
+  SME_HIP(hipMemcpyAsync(qo.data(), d_qoff, (nq + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  SME_HIP(hipStreamSynchronize(st));
+  const int64_t t0 = qo[0], nt = qo[nq] - t0;
+  std::vector<int32_t> all((size_t)std::max<int64_t>(nt, 1));
+  if (nt > 0) SME_HIP(hipMemcpy(all.data(), d_terms + t0, nt * sizeof(int32_t), hipMemcpyDeviceToHost));
+  std::vector<int32_t> sterms;
+  std::vector<int64_t> soff(1, 0);
+  for (int i = 0; i < n; i++) {
+    const int64_t q = ql[i];
+    for (int64_t j = qo[q]; j < qo[q + 1]; j++) sterms.push_back(all[(size_t)(j - t0)]);
+    soff.push_back((int64_t)sterms.size());
+  }
+  DevBuf b_terms, b_off, b_d, b_s, b_t, b_l;
+  int32_t *dt = b_terms.as<int32_t>(std::max<size_t>(sterms.size(), 1));
+  int64_t *doff = b_off.as<int64_t>(soff.size());
+  int32_t *od = b_d.as<int32_t>((size_t)n * k);
+  double *os = b_s.as<double>((size_t)n * k);
+  uint32_t *ot = d_out_tie ? b_t.as<uint32_t>((size_t)n * k) : nullptr;
+  int32_t *dl = b_l.as<int32_t>(n);
+  if (!sterms.empty())
+    SME_HIP(hipMemcpyAsync(dt, sterms.data(), sterms.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+  SME_HIP(hipMemcpyAsync(doff, soff.data(), soff.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
+  SME_HIP(hipMemcpyAsync(dl, ql.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st));
+  query_topk(ix, dt, doff, n, k, od, os, ot, st);  // splits by itself until a subset's tables fit
+  hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)std::min<int64_t>(((int64_t)n * k + 255) / 256, 4096)), dim3(256),
+                     0, st, dl, n, k, od, os, ot, d_out_docno, d_out_score, d_out_tie);
+  SME_CHECK_LAUNCH();
+  SME_HIP(hipStreamSynchronize(st));  // the staging buffers are freed on return
 }
 
 

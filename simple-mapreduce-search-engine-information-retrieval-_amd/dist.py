@@ -15,7 +15,8 @@ the small global statistics and the query results:
   global_df        df per global term = sum of shard postings lengths (all_reduce);
                    returned per LOCAL term for sme_index_reweight
   global_df_index  the same for a libsme shard, keyed by 128-bit device term
-                   fingerprints (all_gather + torch.unique, no host strings)
+                   fingerprints, exchanged by owner rank (df_exchange: all_to_all
+                   to the owner, dedup of 1/W of the terms, all_to_all back)
   merge_topk_owner per-shard top-k -> global top-k of the queries a rank owns
                    (query-owner all_to_all of Q x k x (4 + 8) B, score desc,
                    docno asc); merge_topk also all_gathers the merged slices
@@ -135,70 +136,111 @@ def global_df(local_df, l2g, n_global_terms, group=None):
     return g[torch.from_numpy(l2g).to(dev)] if len(l2g) else g[:0]
 
 
-def _hip_d2d(dst, src, nbytes, stream):
-    """device -> device copy on `stream` through libsme's HIP runtime."""
-    importlib.import_module(__package__).memcpy(dst, src, nbytes, stream)
+def _unique_rows(fp):
+    """(unique rows, inverse) of an int64 [n, 2] fingerprint tensor.  Sorts on the
+    first word only (a 1-D unique is far cheaper than unique(dim=0)); rows whose
+    first words agree but second words differ (2^-64 per pair) take the exact
+    row-wise unique instead."""
+    if fp.shape[0] == 0:
+        return fp, torch.zeros(0, dtype=torch.int64, device=fp.device)
+    u0, inv = torch.unique(fp[:, 0], return_inverse=True)
+    lo = torch.full((u0.shape[0],), torch.iinfo(torch.int64).max, dtype=torch.int64, device=fp.device)
+    hi = torch.full((u0.shape[0],), torch.iinfo(torch.int64).min, dtype=torch.int64, device=fp.device)
+    lo.scatter_reduce_(0, inv, fp[:, 1], "amin")
+    hi.scatter_reduce_(0, inv, fp[:, 1], "amax")
+    if bool((lo != hi).any()):
+        return torch.unique(fp, dim=0, return_inverse=True)
+    return torch.stack([u0, lo], 1), inv
+
+
+def df_exchange(fp, df, group=None, timings=None):
+    """Global df per local term, keyed by term fingerprints (int64 [V, 2]; df int64
+    [V], on the collective's device).  Each fingerprint has ONE owner rank
+    (first word mod W): one all_to_all sends every local (fingerprint, df) to its
+    owner, each owner deduplicates and sums only the ~1/W of the terms it owns,
+    and a second all_to_all returns the summed df to the senders.  Per rank that
+    moves 24 B per local term out and 8 B back, and sorts ~(sum of shard
+    vocabularies) / W rows -- where an all_gather + unique on every rank would
+    move and sort all of them (the reducer's view of df, TermKGramDocIndexer.java
+    :175-183, is the postings length summed over the map outputs)."""
+    import time
+    world = dist.get_world_size(group)
+    dev = fp.device
+    V = int(fp.shape[0])
+    t0 = time.perf_counter()
+    owner = torch.remainder(fp[:, 0], world) if V else torch.zeros(0, dtype=torch.int64, device=dev)
+    order = torch.argsort(owner, stable=True)
+    send_fp = fp[order].contiguous()
+    send_df = df[order].contiguous()
+    counts = torch.bincount(owner, minlength=world).to(torch.int64)
+    rcounts = torch.empty_like(counts)
+    dist.all_to_all_single(rcounts, counts, group=group)
+    cs, rc = counts.tolist(), rcounts.tolist()
+    nrecv = int(sum(rc))
+    recv_fp = torch.empty((nrecv, 2), dtype=torch.int64, device=dev)
+    recv_df = torch.empty(nrecv, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv_fp.view(-1), send_fp.view(-1), [2 * c for c in rc], [2 * c for c in cs], group=group)
+    dist.all_to_all_single(recv_df, send_df, rc, cs, group=group)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    uniq, inv = _unique_rows(recv_fp)
+    g = torch.zeros(uniq.shape[0], dtype=torch.int64, device=dev)
+    g.index_add_(0, inv, recv_df)
+    back = g[inv].contiguous()
+    n_owned = torch.tensor([int(uniq.shape[0])], dtype=torch.int64, device=dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    ret = torch.empty(V, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(ret, back, cs, rc, group=group)
+    dist.all_reduce(n_owned, group=group)
+    out = torch.empty(V, dtype=torch.int64, device=dev)
+    out[order] = ret
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    if timings is not None:
+        timings.update(exchange_ms=(t1 - t0) * 1e3, dedup_ms=(t2 - t1) * 1e3, return_ms=(t3 - t2) * 1e3,
+                       local_terms=V, owned_rows=nrecv, owned_terms=int(uniq.shape[0]),
+                       global_terms=int(n_owned.item()), bytes_out_per_rank=24 * V, bytes_back_per_rank=8 * V)
+    return out
 
 
 def global_df_index(ix, group=None, timings=None):
     """All-reduced df per LOCAL term of a libsme shard index, as a CUDA int64 tensor
     ready for sme_index_reweight: shards agree on terms through their 128-bit device
-    fingerprints (sme_index_term_fingerprints), gathered and deduplicated with
-    torch.unique on the collective's device -- no term strings on the host, and the
-    shard's df comes from its device offsets (never through host memory).
+    fingerprints (sme_index_term_fingerprints), exchanged by owner (df_exchange) --
+    no term strings on the host, and the shard's df comes from its device offsets
+    (never through host memory).
 
-    Everything runs on torch's current stream (the fingerprints and the offsets copy
-    are issued on it), and the stream is synchronized before returning, so the
-    result is ready for a reweight on any stream.  `timings` (a dict) receives the
-    wall ms of the fingerprint, gather, unique and reduce steps."""
+    The fingerprints and the offsets copy run on libsme's own stream of the index's
+    context (sme_index_term_fingerprints / sme_memcpy with a null stream), which is
+    synchronized before torch reads them, so no stream handle crosses between
+    torch's HIP runtime and libsme's.  `timings` (a dict) receives the wall ms of
+    the fingerprint, exchange, dedup and return steps."""
     import time
+    sme = importlib.import_module(__package__)
     dev = _dev(group)
-    world = dist.get_world_size(group)
     V = int(ix.V)
-    cs = torch.cuda.current_stream()
     t0 = time.perf_counter()
     fp = torch.empty((max(V, 1), 2), dtype=torch.int64, device="cuda")
     offs = torch.empty(V + 1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # the tensors exist before libsme's stream writes them
     if V:
-        ix.term_fingerprints(fp.data_ptr(), cs.cuda_stream)  # every row written
+        ix.term_fingerprints(fp.data_ptr(), None)  # every row written, libsme's stream (synchronized)
         o_ptr, _, _ = ix.device_arrays()
-        _hip_d2d(offs.data_ptr(), o_ptr, 8 * (V + 1), cs.cuda_stream)
+        sme.memcpy(offs.data_ptr(), o_ptr, 8 * (V + 1), None)
     else:
         offs.zero_()
     df = (offs[1:] - offs[:-1]).to(dev)
     fp = fp[:V].to(dev)
-    cs.synchronize()
     t1 = time.perf_counter()
-    n = torch.tensor([V], dtype=torch.int64, device=dev)
-    ns = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(ns, n, group=group)
-    ns = [int(x.item()) for x in ns]
-    m = max(max(ns), 1)
-    pad = torch.zeros((m, 2), dtype=torch.int64, device=dev)
-    pad[:V] = fp
-    outs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(outs, pad, group=group)
-    allfp = torch.cat([o[:c] for o, c in zip(outs, ns)], 0)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    uniq, inv = torch.unique(allfp, dim=0, return_inverse=True)
-    r = dist.get_rank(group)
-    mine = inv[sum(ns[:r]):sum(ns[:r]) + V]
-    g = torch.zeros(uniq.shape[0], dtype=torch.int64, device=dev)
-    if V:
-        g.index_add_(0, mine, df)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t3 = time.perf_counter()
-    dist.all_reduce(g, group=group)
-    out = g[mine].to("cuda").contiguous()
+    out = df_exchange(fp, df, group, timings)
+    out = out.to("cuda").contiguous()
     torch.cuda.current_stream().synchronize()
-    t4 = time.perf_counter()
     if timings is not None:
-        timings.update(fingerprints_ms=(t1 - t0) * 1e3, all_gather_ms=(t2 - t1) * 1e3, unique_ms=(t3 - t2) * 1e3,
-                       all_reduce_ms=(t4 - t3) * 1e3, local_terms=V, gathered_terms=int(allfp.shape[0]),
-                       global_terms=int(uniq.shape[0]))
+        timings.update(fingerprints_ms=(t1 - t0) * 1e3)
     return out
 
 

@@ -78,7 +78,7 @@ def write_sequence_file(path, records, sync=None):
 
 def key_of(records, off):
     kl = struct.unpack_from(">i", records, off + 4)[0]
-    return records[off + 8:off + 8 + kl]
+    return bytes(records[off + 8:off + 8 + kl])
 
 
 def write_index_dir(ix, out_dir, sync=None):

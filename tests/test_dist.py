@@ -136,3 +136,43 @@ def test_cuts_own_every_record_and_quirks():
             for a, b in zip(cuts, cuts[1:]):
                 got += [(a + o, ln) for o, ln in O.split_records(corpus[a:b])]
             assert got == recs, w
+
+
+def _dfx_worker(rank, world, port, out_dir, collide):
+    """df_exchange over random shard vocabularies: every local term's result must be
+    the df summed over every shard holding its fingerprint."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        D = importlib.import_module(PKG + ".dist")
+        g = np.random.default_rng(11)
+        universe = g.integers(-(1 << 62), 1 << 62, size=(3000, 2), dtype=np.int64)
+        if collide:  # equal first words, different second words: the exact row-wise path
+            universe[1::7, 0] = universe[0::7, 0][:universe[1::7].shape[0]]
+        shards = []
+        for r in range(world):
+            gr = np.random.default_rng(100 + r)
+            ids = np.sort(gr.choice(3000, size=int(gr.integers(0, 1200)), replace=False))
+            shards.append((ids, gr.integers(1, 50, size=ids.shape[0]).astype(np.int64)))
+        ids, df = shards[rank]
+        t = {}
+        out = D.df_exchange(torch.from_numpy(universe[ids].copy()), torch.from_numpy(df), timings=t).numpy()
+        want = {}
+        for i2, d2 in shards:
+            for i, d in zip(i2.tolist(), d2.tolist()):
+                key = tuple(universe[i].tolist())
+                want[key] = want.get(key, 0) + d
+        exp = np.array([want[tuple(universe[i].tolist())] for i in ids.tolist()], np.int64)
+        assert np.array_equal(out, exp)
+        assert t["global_terms"] == len(want)
+        open(os.path.join(out_dir, "ok%d" % rank), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,collide", [(2, False), (3, True), (4, False)])
+def test_df_exchange_owner_gloo(tmp_path, world, collide):
+    """The owner-partitioned df exchange (all_to_all to the fingerprint's owner,
+    dedup there, all_to_all back) equals the brute-force sum over shards."""
+    mp.spawn(_dfx_worker, args=(world, _free_port(), str(tmp_path), collide), nprocs=world, join=True)
+    assert all((tmp_path / ("ok%d" % r)).exists() for r in range(world))

@@ -599,3 +599,37 @@ def test_repl_contract(sme):
     fm = sme.IntDocVectorsForwardIndex(ix, mb)
     ids = [""] + list(KAT["index_mapping"])
     assert fm.query_line("cat dog") == "cat dog: " + ids[1] + " " + ids[2] + " "
+
+
+@pytest.mark.parametrize("budget,cap", [(1, 1024), (8192, 4)])
+def test_queries_table_budget(sme, synth, budget, cap):
+    """Batches whose skip tables exceed the table budget (sme_set_option
+    "query_table_budget") are split by query range, and queries that still
+    overflow their candidate lists without room for the tile table run as their
+    own compact batches: k = 100 over a uniform-vocabulary batch answers every
+    query (no SME_ENOTIMPL), bit-identical to the default path and to the
+    oracle's rank().  budget 1 splits down to single queries; 8 KiB fits the
+    window table but not the tile table, and cand_cap 4 < k sends every query
+    to that fallback."""
+    n = 9000
+    c = synth.gen_corpus(n, V=3000, seed=13, len_lo=8, len_hi=30)
+    ix, ref = _check_build(sme, c, synth.docids(n), R=1)
+    _, _, _, df = ix.csr()
+    names = [ix.term(i) for i in range(ix.V)]
+    terms, qoff = synth.queries_by_df(df, 60, seed=5, uniform=True)
+    k = 100
+    dn0, sc0 = ix.query_topk(terms, qoff, k)
+    try:
+        ix.ctx.set_option("query_table_budget", budget)
+        dn, sc = _query_opts(ix, terms, qoff, k, cand_cap=cap)
+        prof = ix.ctx.last_build_profile()
+    finally:
+        ix.ctx.set_option("query_table_budget", 0)
+    assert prof["query_kernel_name"] == "k_query_win"
+    assert np.array_equal(dn, dn0) and np.array_equal(sc, sc0)
+    for q in range(len(qoff) - 1):
+        tl = [names[t] for t in terms[qoff[q]:qoff[q + 1]]]
+        rd, rs = ref.query(tl, k, 0, 0)
+        assert dn[q, :len(rd)].tolist() == rd, q
+        assert np.array_equal(sc[q, :len(rd)], np.array(rs)), q
+        assert (dn[q, len(rd):] == -1).all()
