@@ -274,6 +274,26 @@ void sme_synth_free(void *d_corpus);
  * `bytes` (x reps, after a warm-up); *gbps = read + write bytes / kernel time. */
 int sme_hbm_copy_bench(int device, size_t bytes, int reps, double *gbps);
 
+/* Reference-layout output from doc shards (the job's R part files,
+ * TermKGramDocIndexer.java:189-211,246-275): partition p is reduced by rank
+ * p % world.  pack: this shard's terms grouped by owner rank as `world` blobs
+ * laid out back to back at d_out (device memory; NULL = only fill sizes[world],
+ * each blob's bytes): the terms (String.compareTo order), their postings in
+ * reduce order, and the shard's record docnos for the owner of the " " doc
+ * counter's partition.  merge: the n blobs a rank received (one per shard, in
+ * shard order, back to back at d_blobs) -> a records-only index whose
+ * partitions p with p % world == rank hold exactly what the reference's single
+ * reducer writes for the shards' map tasks (postings merged per term by
+ * MyReducer.reduce, :189-211: docno sort, equal docnos summed, stable tf-desc
+ * sort; one doc-counter list per map task).  Read it with sme_index_serialize /
+ * sme_index_copy_records; it has no query side (query entry points: SME_EINVAL). */
+int sme_index_pack_pieces(sme_index *ix, int world, void *d_out, uint64_t *sizes, void *stream);
+/* Device pointer to the docnos of the index's records in input order (*n = N;
+ * the map task's doc-counter postings, TermKGramDocIndexer.java:84-90,126). */
+int sme_index_record_docnos(sme_index *ix, const int32_t **d_docno, int64_t *n);
+int sme_merge_pieces(sme_ctx *ctx, const void *d_blobs, const uint64_t *sizes, int n, void *stream,
+                     sme_index **out);
+
 /* Timing of the last build, per stage, in milliseconds (device events on the
  * build stream), as a JSON object; "tok_kernel" brackets exactly the tokenizer
  * launch and "query_kernel" (if a query batch ran) the last scoring launch. */

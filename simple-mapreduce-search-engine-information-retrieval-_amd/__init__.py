@@ -48,7 +48,8 @@ EXPORTS = [
     "sme_query_topk_device", "sme_query_topk_device_tie", "sme_query_topk_tie", "sme_last_build_profile", "sme_index_reweight", "sme_number_documents",
     "sme_build_chargram", "sme_build_chargram_device", "sme_chargram_partition_text", "sme_chargram_stats",
     "sme_split_points", "sme_split_points_device", "sme_index_term_fingerprints", "sme_set_option",
-    "sme_index_prepare_queries", "sme_hbm_copy_bench",
+    "sme_index_prepare_queries", "sme_hbm_copy_bench", "sme_index_pack_pieces", "sme_merge_pieces",
+    "sme_index_record_docnos",
 ]
 
 
@@ -106,6 +107,9 @@ def lib():
     L.sme_synth_free.argtypes = [vp]
     L.sme_hbm_copy_bench.argtypes = [C.c_int, sz, C.c_int, C.POINTER(C.c_double)]
     L.sme_synth_free.restype = None
+    L.sme_index_pack_pieces.argtypes = [vp, C.c_int, vp, C.POINTER(C.c_uint64), vp]
+    L.sme_merge_pieces.argtypes = [vp, vp, C.POINTER(C.c_uint64), C.c_int, vp, C.POINTER(vp)]
+    L.sme_index_record_docnos.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_int64)]
     _lib = L
     return L
 
@@ -217,6 +221,17 @@ class Context:
                                             C.byref(h)))
         return Index(h, self)
 
+    def merge_pieces(self, d_blobs, sizes):
+        """sme_merge_pieces: the blobs one rank received from every shard (device
+        memory at d_blobs, back to back, `sizes` bytes each, shard order) -> a
+        records-only Index whose partitions p with p % world == rank are the
+        reference's reduce output for those partitions (include/sme.h)."""
+        n = len(sizes)
+        arr = (C.c_uint64 * max(n, 1))(*[int(x) for x in sizes])
+        h = C.c_void_p()
+        _check(lib().sme_merge_pieces(self._h, C.c_void_p(d_blobs), arr, n, None, C.byref(h)))
+        return Index(h, self)
+
     def build_chargram(self, corpus):
         """CharKGramTermIndexer over host bytes (k = this context's k, R = num_partitions)."""
         h = C.c_void_p()
@@ -272,6 +287,19 @@ class Index:
         out = bytearray(int(offs[part + 1] - offs[part]))
         self.copy_records(part, out)
         return out
+
+    def record_docnos_ptr(self):
+        """(device pointer, N): the docnos of the index's records in input order."""
+        p, n = C.c_void_p(), C.c_int64()
+        _check(lib().sme_index_record_docnos(self._h, C.byref(p), C.byref(n)))
+        return p.value or 0, n.value
+
+    def pack_pieces(self, world, d_out=None):
+        """sme_index_pack_pieces: sizes of this shard's `world` per-owner blobs
+        (d_out None), or write them back to back at device address d_out."""
+        arr = (C.c_uint64 * world)()
+        _check(lib().sme_index_pack_pieces(self._h, int(world), C.c_void_p(d_out or 0), arr, None))
+        return [int(x) for x in arr]
 
     def serialize(self):
         """Device serialization of every partition (once per index):

@@ -38,6 +38,12 @@ int guard(F &&f) {
 
 hipStream_t stream_of(sme_ctx *cx, void *s) { return s ? (hipStream_t)s : cx->own_stream; }
 
+// merged shard pieces (sme_merge_pieces) hold the reduce output only
+void need_query_side(const sme_index *ix) {
+  if (ix->records_only)
+    throw sme::Error(SME_EINVAL, "records-only index (merged shard pieces): query the shard indexes");
+}
+
 void set_device(sme_ctx *cx) { SME_HIP(hipSetDevice(cx->device)); }
 
 // DataInput.readUTF body -> UTF-16
@@ -563,6 +569,7 @@ int sme_index_device_arrays(sme_index *ix, const int64_t **d_offsets, const int3
                             const double **d_weight) {
   return guard([&] {
     if (!ix) throw sme::Error(SME_EINVAL, "null index");
+    need_query_side(ix);
     if (d_offsets) *d_offsets = (const int64_t *)ix->d_off.p;
     if (d_docno) *d_docno = (const int32_t *)ix->d_docno_d.p;
     if (d_weight) *d_weight = (const double *)ix->d_w.p;
@@ -617,6 +624,7 @@ int sme_lookup_terms(sme_index *ix, const uint8_t *terms, const int64_t *offs, i
 int sme_index_prepare_queries(sme_index *ix, void *stream, float *ms) {
   return guard([&] {
     if (!ix) throw sme::Error(SME_EINVAL, "null index");
+    need_query_side(ix);
     if (ix->job != 0) throw sme::Error(SME_EINVAL, "not a TermKGramDocIndexer index");
     set_device(ix->ctx);
     sme::prepare_queries(ix, stream_of(ix->ctx, stream));
@@ -629,6 +637,7 @@ int sme_query_topk_device(sme_index *ix, const int32_t *d_term_ids, const int64_
   return guard([&] {
     if (!ix || (nq > 0 && (!d_term_ids || !d_q_offsets || !d_out_docno || !d_out_score)))
       throw sme::Error(SME_EINVAL, "null argument");
+    need_query_side(ix);
     set_device(ix->ctx);
     sme::query_topk(ix, d_term_ids, d_q_offsets, nq, k, d_out_docno, d_out_score, nullptr,
                     stream_of(ix->ctx, stream));
@@ -640,6 +649,7 @@ int sme_query_topk_device_tie(sme_index *ix, const int32_t *d_term_ids, const in
   return guard([&] {
     if (!ix || (nq > 0 && (!d_term_ids || !d_q_offsets || !d_out_docno || !d_out_score || !d_out_tie)))
       throw sme::Error(SME_EINVAL, "null argument");
+    need_query_side(ix);
     set_device(ix->ctx);
     sme::query_topk(ix, d_term_ids, d_q_offsets, nq, k, d_out_docno, d_out_score, d_out_tie,
                     stream_of(ix->ctx, stream));
@@ -651,6 +661,7 @@ static int query_topk_host(sme_index *ix, const int32_t *term_ids, const int64_t
   return guard([&] {
     if (!ix || (nq > 0 && (!term_ids || !q_offsets || !out_docno || !out_score)))
       throw sme::Error(SME_EINVAL, "null argument");
+    need_query_side(ix);
     if (nq <= 0) return;
     set_device(ix->ctx);
     hipStream_t st = ix->ctx->own_stream;
@@ -702,8 +713,37 @@ int sme_index_term_fingerprints(sme_index *ix, uint64_t *d_out, void *stream) {
 int sme_index_reweight(sme_index *ix, int64_t n_global, const int64_t *d_df_global, void *stream) {
   return guard([&] {
     if (!ix || n_global < 0) throw sme::Error(SME_EINVAL, "bad argument");
+    need_query_side(ix);
     set_device(ix->ctx);
     sme::reweight_index(ix, n_global, d_df_global, stream_of(ix->ctx, stream));
+  });
+}
+
+int sme_index_record_docnos(sme_index *ix, const int32_t **d_docno, int64_t *n) {
+  return guard([&] {
+    if (!ix || !d_docno || !n) throw sme::Error(SME_EINVAL, "null argument");
+    if (ix->job != 0) throw sme::Error(SME_EINVAL, "not a TermKGramDocIndexer index");
+    *d_docno = (const int32_t *)ix->d_rec_docno.p;
+    *n = ix->N;
+  });
+}
+
+int sme_index_pack_pieces(sme_index *ix, int world, void *d_out, uint64_t *sizes, void *stream) {
+  return guard([&] {
+    if (!ix || !sizes) throw sme::Error(SME_EINVAL, "null argument");
+    need_query_side(ix);
+    set_device(ix->ctx);
+    hipStream_t st = stream_of(ix->ctx, stream);
+    sme::pack_pieces(ix, world, (uint8_t *)d_out, sizes, st);
+    SME_HIP(hipStreamSynchronize(st));
+  });
+}
+
+int sme_merge_pieces(sme_ctx *cx, const void *d_blobs, const uint64_t *sizes, int n, void *stream, sme_index **out) {
+  return guard([&] {
+    if (!cx || !d_blobs || !sizes || !out || n < 1) throw sme::Error(SME_EINVAL, "bad argument");
+    set_device(cx);
+    *out = sme::merge_pieces(cx, (const uint8_t *)d_blobs, sizes, n, stream_of(cx, stream));
   });
 }
 

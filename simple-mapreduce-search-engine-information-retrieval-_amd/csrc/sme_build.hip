@@ -2093,11 +2093,15 @@ __global__ void k_composite_tf(const uint64_t *ck, int64_t P, uint64_t tfmask, i
     tf[i] = (int32_t)(tfmask - (ck[i] & tfmask));
 }
 
-__global__ void k_docno_keys(const int32_t *docno, int64_t nR, uint32_t *k, int64_t *v) {
+__global__ void k_docno_keys(const int32_t *docno, int64_t nR, uint32_t *k, uint32_t *v) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nR; i += (int64_t)gridDim.x * blockDim.x) {
     k[i] = (uint32_t)docno[i] ^ 0x80000000u;  // signed order
-    v[i] = i;
+    v[i] = (uint32_t)i;
   }
+}
+__global__ void k_widen_u32(const uint32_t *a, int64_t n, int64_t *b) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    b[i] = (int64_t)a[i];
 }
 __global__ void k_adjacent_equal(const uint32_t *k, int64_t n, unsigned long long *cnt) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -2741,13 +2745,13 @@ RecordSpans find_records(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t 
 
   // sort S, E, C positions
   // sorted copies land in spare workspace slots (no device-to-device copy back)
+  // (hand-written LSD radix, sme_sort.hip; the values ride along unused)
   auto sort_u64 = [&](uint64_t *buf, int64_t cnt_, int slot_alt) -> uint64_t * {
     if (cnt_ < 2) return buf;
     uint64_t *alt = W[slot_alt].as<uint64_t>(cnt_);
-    size_t tb = 0;
-    SME_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, buf, alt, (int)cnt_, 0, bits_for(n), st));
-    SME_HIP(hipcub::DeviceRadixSort::SortKeys(cub_tmp(tb), tb, buf, alt, (int)cnt_, 0, bits_for(n), st));
-    return alt;
+    uint32_t *va = cx->ws[26].as<uint32_t>(cnt_), *vb = cx->ws[27].as<uint32_t>(cnt_);
+    uint32_t *rscr = cx->ws[24].as<uint32_t>(kv_sort_scratch(cnt_) / sizeof(uint32_t) + 1);
+    return kv_sort<uint64_t>(buf, va, alt, vb, cnt_, bits_for(n), rscr, st, true) == va ? buf : alt;
   };
   uint64_t *S = sort_u64(W[W_S].as<uint64_t>(capS), nS, W_SS);
   uint64_t *E = sort_u64(W[W_E].as<uint64_t>(capE), nE, W_SE);
@@ -2838,13 +2842,14 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   bool dup_docno = false;
   if (nR > 0) {
     uint32_t *k0 = W[W_T0].as<uint32_t>(nR), *k1 = W[W_T1].as<uint32_t>(nR);
-    int64_t *v0 = W[W_T2].as<int64_t>(nR);
+    uint32_t *v0 = W[W_T2].as<uint32_t>(nR), *v1 = W[W_T3].as<uint32_t>(nR);
     hipLaunchKernelGGL(k_docno_keys, dim3(grid_for(nR)), dim3(256), 0, st, docno, nR, k0, v0);
-    size_t tb = 0;
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, perm, (int)nR, 0, 32, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tb), tb, k0, k1, v0, perm, (int)nR, 0, 32, st));
+    uint32_t *rscr = cx->ws[24].as<uint32_t>(kv_sort_scratch(nR) / sizeof(uint32_t) + 1);
+    uint32_t *vs = kv_sort<uint32_t>(k0, v0, k1, v1, nR, 32, rscr, st, true);
+    const uint32_t *ks = vs == v0 ? k0 : k1;
+    hipLaunchKernelGGL(k_widen_u32, dim3(grid_for(nR)), dim3(256), 0, st, vs, nR, perm);
     SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_adjacent_equal, dim3(grid_for(nR)), dim3(256), 0, st, k1, nR, cnt);
+    hipLaunchKernelGGL(k_adjacent_equal, dim3(grid_for(nR)), dim3(256), 0, st, ks, nR, cnt);
     dup_docno = d2h(cnt, st) != 0;
   }
   prof.mark("docno_sort");
@@ -2866,11 +2871,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   if (nR > 0) {
     uint8_t *fflag = W[W_RFLAG].as<uint8_t>(nR);
     hipLaunchKernelGGL(k_not_flags, dim3(grid_for(nR)), dim3(256), 0, st, slow, nR, fflag);
-    size_t tbb = 0;
-    hipcub::CountingInputIterator<int32_t> it(0);
     int32_t *d_nf = reinterpret_cast<int32_t *>(cnt + 14);
-    SME_HIP(hipcub::DeviceSelect::Flagged(nullptr, tbb, it, fflag, frec, d_nf, (int)nR, st));
-    SME_HIP(hipcub::DeviceSelect::Flagged(cub_tmp(tbb), tbb, it, fflag, frec, d_nf, (int)nR, st));
+    select_flagged(fflag, nR, frec, d_nf, cx->ws[25], cx->ws[23], st);
     nF = d2h(d_nf, st);
   }
   for (int attempt = 0;; attempt++) {
@@ -2905,9 +2907,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       int64_t *lens = W[W_T0].as<int64_t>(nslow + 1), *soff = W[W_SCROFF].as<int64_t>(nslow + 1);
       hipLaunchKernelGGL(k_fill_slow_lens, dim3(grid_for(nslow)), dim3(256), 0, st, slist, nslow, rs, re, lens);
       size_t tbb = 0;
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, lens, soff, (int)nslow + 1, st));
       SME_HIP(hipMemsetAsync(lens + nslow, 0, sizeof(int64_t), st));
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, lens, soff, (int)nslow + 1, st));
+      excl_scan(lens, soff, (int64_t)(nslow + 1), cx->ws[23], st);
       int64_t tot = d2h(soff + nslow, st);
       uint16_t *u16s = W[W_U16].as<uint16_t>(tot + 1);
       uint32_t *boffs = W[W_BOFF].as<uint32_t>(tot + 1);
@@ -2929,12 +2930,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   int32_t *rlist = W[W_RLIST].as<int32_t>(rcap);
   int32_t *d_nsel = reinterpret_cast<int32_t *>(cnt + 13);
   hipLaunchKernelGGL(k_raw_flags, dim3(grid_for((int64_t)rcap)), dim3(256), 0, st, tb.slots, rcap, rflag);
-  {
-    size_t tbb = 0;
-    hipcub::CountingInputIterator<int32_t> it(0);
-    SME_HIP(hipcub::DeviceSelect::Flagged(nullptr, tbb, it, rflag, rlist, d_nsel, (int)rcap, st));
-    SME_HIP(hipcub::DeviceSelect::Flagged(cub_tmp(tbb), tbb, it, rflag, rlist, d_nsel, (int)rcap, st));
-  }
+  select_flagged(rflag, (int64_t)rcap, rlist, d_nsel, cx->ws[25], cx->ws[23], st);
   const int64_t nraw = d2h(d_nsel, st);
   // next build's raw table: load <= 40 % (fewer probe collisions: c2 tokenizes in 9.2 ms at 8 M
   // slots vs 10.0 ms at 4 M; option raw_load_pct)
@@ -2947,8 +2943,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     int64_t *lens = W[W_T0].as<int64_t>(nraw + 1);
     hipLaunchKernelGGL(k_raw_lens, dim3(grid_for(nraw + 1)), dim3(256), 0, st, tb.slots, rlist, nraw, lens);
     size_t tbb = 0;
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, lens, poff, (int)nraw + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, lens, poff, (int)nraw + 1, st));
+    excl_scan(lens, poff, (int64_t)(nraw + 1), cx->ws[23], st);
   }
   const int64_t pool_units = d2h(poff + nraw, st);
   CandOut co;
@@ -2986,8 +2981,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
                          lens);
       SME_HIP(hipMemsetAsync(lens + nlong, 0, sizeof(int64_t), st));
       size_t tbb = 0;
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, lens, soff, (int)nlong + 1, st));
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, lens, soff, (int)nlong + 1, st));
+      excl_scan(lens, soff, (int64_t)(nlong + 1), cx->ws[23], st);
       int64_t tot = d2h(soff + nlong, st);
       uint16_t *scr = W[W_U16].as<uint16_t>(tot + 1);
       hipLaunchKernelGGL(k_vocab_long, dim3(grid_for(nlong, 64)), dim3(64), 0, st, tb, rlist, co, long_list, nlong,
@@ -3069,8 +3063,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     int64_t *tlen = W[W_T0].as<int64_t>(V + 1);
     hipLaunchKernelGGL(k_final_rank, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, vcs, rank_of_slot, tlen);
     SME_HIP(hipMemsetAsync(tlen + V, 0, sizeof(int64_t), st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, tlen, term_off, (int)V + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, tlen, term_off, (int)V + 1, st));
+    excl_scan(tlen, term_off, (int64_t)(V + 1), cx->ws[23], st);
     int64_t tchars = d2h(term_off + V, st);
     uint16_t *term_chars = ix->d_term_chars.as<uint16_t>(tchars + 1);
     hipLaunchKernelGGL(k_final_gather, dim3(grid_for(V)), dim3(256), 0, st, order, V, vcs, co.pool, term_off,
@@ -3117,8 +3110,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     if (nR > 0) hipLaunchKernelGGL(k_tcount, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, tcnt);
     SME_HIP(hipMemsetAsync(tcnt + nR, 0, sizeof(int64_t), st));
     size_t tbb = 0;
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, tcnt, toff, (int)nR + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, tcnt, toff, (int)nR + 1, st));
+    excl_scan(tcnt, toff, (int64_t)(nR + 1), cx->ws[23], st);
     const int64_t M = d2h(toff + nR, st);
     int32_t *tstream = W[W_U16].as<int32_t>(M + 1);
     if (nR > 0) hipLaunchKernelGGL(k_twrite, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, toff, tstream);
@@ -3174,8 +3166,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
                        cnt + 24);
     SME_HIP(hipMemsetAsync(reg + nR, 0, sizeof(int64_t), st));
     size_t tbb = 0;
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, reg, reg_off, (int)nR + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, reg, reg_off, (int)nR + 1, st));
+    excl_scan(reg, reg_off, (int64_t)(nR + 1), cx->ws[23], st);
     int64_t Pb = 0;
     unsigned long long h_rmx = 0;
     SME_HIP(hipMemcpyAsync(&Pb, reg_off + nR, sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -3207,8 +3198,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
         int64_t *bcap = W[W_BIGCAP].as<int64_t>(nbig + 1), *boff = W[W_RLIST].as<int64_t>(nbig + 1);
         hipLaunchKernelGGL(k_big_caps, dim3(grid_for(nbig)), dim3(256), 0, st, bl2, nbig, perm, ntok, max_nout, bcap);
         SME_HIP(hipMemsetAsync(bcap + nbig, 0, sizeof(int64_t), st));
-        SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, bcap, boff, (int)nbig + 1, st));
-        SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, bcap, boff, (int)nbig + 1, st));
+        excl_scan(bcap, boff, (int64_t)(nbig + 1), cx->ws[23], st);
         const int64_t gtot = d2h(boff + nbig, st);
         int32_t *gkeys = W[W_U16].as<int32_t>(gtot), *gcnt = W[W_BOFF].as<int32_t>(gtot);
         hipLaunchKernelGGL(k_agg_big, dim3((unsigned)std::min<int64_t>(nbig, 4096)), dim3(kAggNT), 0, st, ai, bl2,
@@ -3218,8 +3208,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       // exact pair offsets of the records (docno order)
       int64_t *xoff = W[W_NTOK2].as<int64_t>(nR + 1);
       SME_HIP(hipMemsetAsync(ai.dcnt + nR, 0, sizeof(int64_t), st));
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, ai.dcnt, xoff, (int)nR + 1, st));
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, ai.dcnt, xoff, (int)nR + 1, st));
+      excl_scan(ai.dcnt, xoff, (int64_t)(nR + 1), cx->ws[23], st);
       SME_HIP(hipMemcpyAsync(&P, xoff + nR, sizeof(int64_t), hipMemcpyDeviceToHost, st));
       SME_HIP(hipMemcpyAsync(&h_mtf, mtf, sizeof(int32_t), hipMemcpyDeviceToHost, st));
       SME_HIP(hipStreamSynchronize(st));
@@ -3255,8 +3244,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     boff = W[W_T1].as<int64_t>(nbig + 1);
     hipLaunchKernelGGL(k_big_caps, dim3(grid_for(nbig)), dim3(256), 0, st, big_list, nbig, perm, ntok, max_nout, bcap);
     SME_HIP(hipMemsetAsync(bcap + nbig, 0, sizeof(int64_t), st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, bcap, boff, (int)nbig + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, bcap, boff, (int)nbig + 1, st));
+    excl_scan(bcap, boff, (int64_t)(nbig + 1), cx->ws[23], st);
     int64_t gtot = d2h(boff + nbig, st);
     gkeys = W[W_U16].as<int32_t>(gtot);
     gcnt = W[W_BOFF].as<int32_t>(gtot);
@@ -3272,8 +3260,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   SME_HIP(hipMemsetAsync(prec64 + nR, 0, sizeof(int64_t), st));
   {
     size_t tbb = 0;
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, prec64, pair_off, (int)nR + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, prec64, pair_off, (int)nR + 1, st));
+    excl_scan(prec64, pair_off, (int64_t)(nR + 1), cx->ws[23], st);
   }
   SME_HIP(hipMemcpyAsync(&P, pair_off + nR, sizeof(int64_t), hipMemcpyDeviceToHost, st));
   if (want_packed) {
@@ -3313,8 +3300,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     if (nR > 0) hipLaunchKernelGGL(k_tcount, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, tcnt);
     SME_HIP(hipMemsetAsync(tcnt + nR, 0, sizeof(int64_t), st));
     size_t tbb = 0;
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, tcnt, toff, (int)nR + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, tcnt, toff, (int)nR + 1, st));
+    excl_scan(tcnt, toff, (int64_t)(nR + 1), cx->ws[23], st);
     const int64_t M = d2h(toff + nR, st);
     int32_t *tstream = W[W_U16].as<int32_t>(M + 1);
     if (nR > 0) hipLaunchKernelGGL(k_twrite, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, toff, tstream);
@@ -3324,8 +3310,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       hipLaunchKernelGGL(k_gram_agg<false>, dim3(g_grid), dim3(kAggNT), 0, st, tstream, toff, nR, perm, docno, K, tb,
                          pcount, bigf, nullptr, nullptr, nullptr);
     SME_HIP(hipMemsetAsync(pcount + nR, 0, sizeof(int64_t), st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, pcount, pair_off, (int)nR + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, pcount, pair_off, (int)nR + 1, st));
+    excl_scan(pcount, pair_off, (int64_t)(nR + 1), cx->ws[23], st);
     const int64_t Pg = d2h(pair_off + nR, st);
     uint64_t *pkey = W[W_KHI].as<uint64_t>(Pg + 1), *pval0 = W[W_KLO].as<uint64_t>(Pg + 1);
     if (nR > 0)
@@ -3507,8 +3492,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     // large segments: tiles spread over the whole chip
     hipLaunchKernelGGL(k_tf_ntiles, dim3(grid_for(Vi + 1)), dim3(256), 0, st, off, seg_large, nseg + 1, Vi, ntl);
     size_t tbb = 0;
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, ntl, toff, (int)Vi + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tbb), tbb, ntl, toff, (int)Vi + 1, st));
+    excl_scan(ntl, toff, (int64_t)(Vi + 1), cx->ws[23], st);
     const int64_t ntiles = d2h(toff + Vi, st);
     if (ntiles > 0) {
       const int F = max_tf + 1;

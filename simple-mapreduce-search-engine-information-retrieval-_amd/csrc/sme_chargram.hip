@@ -306,8 +306,7 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   int32_t *jh = W[53].as<int32_t>(V), *u8len = W[54].as<int32_t>(V);
   int64_t *ng = W[55].as<int64_t>(V + 1), *goff = W[56].as<int64_t>(V + 1);
   hipLaunchKernelGGL(k_term_props, dim3(cg_grid(V + 1)), dim3(256), 0, st, term_off, tch, V, K, jh, u8len, ng);
-  SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, ng, goff, (int)V + 1, st));
-  SME_HIP(hipcub::DeviceScan::ExclusiveSum(tmp(tbb), tbb, ng, goff, (int)V + 1, st));
+  excl_scan(ng, goff, (int64_t)(V + 1), cx->ws[23], st);
   const int64_t NP = cg_d2h(goff + V, st);
   SME_CHECK_LAUNCH();
   if (prof) prof->mark("cg_terms");
@@ -372,8 +371,7 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   // line lengths, partitions, offsets
   int64_t *elen = W[53].as<int64_t>(n + 1), *escan = W[54].as<int64_t>(n + 1);
   hipLaunchKernelGGL(k_cg_elen, dim3(cg_grid(n + 1)), dim3(256), 0, st, u3, kterm, u8len, n, elen);
-  SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, elen, escan, (int)n + 1, st));
-  SME_HIP(hipcub::DeviceScan::ExclusiveSum(tmp(tbb), tbb, elen, escan, (int)n + 1, st));
+  excl_scan(elen, escan, (int64_t)(n + 1), cx->ws[23], st);
   // khi/klo/kterm (slots 57, 58, 60) stay live until the lines are written
   DevBuf b_llen, b_loff, b_part;
   int64_t *llen = b_llen.as<int64_t>(ngr + 1), *loff = b_loff.as<int64_t>(ngr + 1);
@@ -387,8 +385,7 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   int64_t *llen_s = W[52].as<int64_t>(ngr + 1);
   hipLaunchKernelGGL(k_gather<int64_t>, dim3(cg_grid(ngr)), dim3(256), 0, st, llen, gorder, ngr, llen_s);
   SME_HIP(hipMemsetAsync(llen_s + ngr, 0, sizeof(int64_t), st));
-  SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, llen_s, loff, (int)ngr + 1, st));
-  SME_HIP(hipcub::DeviceScan::ExclusiveSum(tmp(tbb), tbb, llen_s, loff, (int)ngr + 1, st));
+  excl_scan(llen_s, loff, (int64_t)(ngr + 1), cx->ws[23], st);
   const int64_t total = cg_d2h(loff + ngr, st);
   uint32_t *rank_of_g = W[51].as<uint32_t>(ngr + 1);  // gseq no longer needed
   hipLaunchKernelGGL(k_rank_of, dim3(cg_grid(ngr)), dim3(256), 0, st, gorder, ngr, rank_of_g);

@@ -146,8 +146,7 @@ void number_documents(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st,
   if (nR > 0) hipLaunchKernelGGL(k_docid_len, grid(nR), dim3(256), 0, st, t, rsp.rs, rsp.re, nR, ib, ie, len, err);
   SME_HIP(hipMemsetAsync(len + nR, 0, sizeof(int64_t), st));
   size_t tb = 0;
-  SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len, off, (int)nR + 1, st));
-  SME_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp(tb), tb, len, off, (int)nR + 1, st));
+  excl_scan(len, off, (int64_t)(nR + 1), cx->ws[23], st);
   int64_t h2[1];
   unsigned long long h_err = 0;
   SME_HIP(hipMemcpyAsync(h2, off + nR, sizeof(int64_t), hipMemcpyDeviceToHost, st));

@@ -92,6 +92,8 @@ struct sme_index {
   sme::DevBuf d_tf_o;     // int32 [P]
   // docno of every record in input order (for the " " doc-counter postings)
   sme::DevBuf d_rec_docno;  // int32 [N]
+  sme::DevBuf d_rec_first;  // u8 [N]: record starts a map task (split) -- merged shard pieces only
+  bool records_only = false;  // merged shard pieces (sme_merge_pieces): reduce-order CSR + records, no query side
   // serialized partitions (lazily built)
   sme::DevBuf d_ser;
   std::vector<int64_t> part_start;  // R+1
@@ -125,7 +127,7 @@ struct sme_index {
   explicit sme_index(sme_ctx *c) : ctx(c) {
     c->live_indexes++;
     for (sme::DevBuf *b : {&d_term_off, &d_term_chars, &d_off, &d_docno_d, &d_tf_d, &d_w, &d_idf, &d_lut, &d_gram, &d_docno_o,
-                           &d_tf_o, &d_rec_docno, &d_ser, &d_hrow_of, &d_heavy})
+                           &d_tf_o, &d_rec_docno, &d_rec_first, &d_ser, &d_hrow_of, &d_heavy})
       b->pool = &c->pool;
   }
 };
@@ -187,7 +189,18 @@ template <typename K>
 uint32_t *kv_sort(K *k0, uint32_t *v0, K *k1, uint32_t *v1, int64_t n, int bits, uint32_t *scratch, hipStream_t st,
                   bool keys_out = false);
 size_t kv_sort_scratch(int64_t n);
+// device-wide exclusive scan out[i] = sum in[0..i) (in == out allowed; scratch:
+// one T per 4096 items), and flag compaction (ascending indices of the nonzero
+// flags, their count to *d_count) -- hand-written, sme_sort.hip
+template <typename T>
+void excl_scan(const T *in, T *out, int64_t n, DevBuf &scratch, hipStream_t st);
+void select_flagged(const uint8_t *flag, int64_t n, int32_t *out, int32_t *d_count, DevBuf &s1, DevBuf &s2,
+                    hipStream_t st);
 void serialize_index(sme_index *ix, hipStream_t st);
+// reference-layout output from doc shards (sme_merge.hip): per-owner blobs of a
+// shard's terms and postings, and the owner's merge of the received blobs
+void pack_pieces(sme_index *ix, int world, uint8_t *d_out, uint64_t *sizes, hipStream_t st);
+sme_index *merge_pieces(sme_ctx *cx, const uint8_t *d_blobs, const uint64_t *sizes, int np, hipStream_t st);
 void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t st);
 void prepare_queries(sme_index *ix, hipStream_t st);
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k,

@@ -1792,8 +1792,7 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     hipLaunchKernelGGL(k_heavy_flags, dim3(gV), dim3(256), 0, st, off, (const int32_t *)ix->d_tf_o.p, V, span, div,
                        flag);
     size_t tbb = 0;
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, flag, scan, (int)V + 1, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, flag, scan, (int)V + 1, st));
+    excl_scan(flag, scan, (int64_t)(V + 1), cx->ws[23], st);
     int32_t nh = 0;
     SME_HIP(hipMemcpyAsync(&nh, scan + V, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
@@ -1810,8 +1809,7 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     SME_CHECK_LAUNCH();
     if (H > 0) {
       SME_HIP(hipMemsetAsync(hdf + H, 0, sizeof(int64_t), st));
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, hdf, hpre, (int)H + 1, st));
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, hdf, hpre, (int)H + 1, st));
+      excl_scan(hdf, hpre, (int64_t)(H + 1), cx->ws[23], st);
       uint8_t *buf = ix->d_heavy.as<uint8_t>((size_t)H * (size_t)per_row + 128);
       uint8_t *tfrow = buf, *imp = buf + H * stride, *bm16 = imp + H * stride, *bm1k = bm16 + H * (T << 6);
       uint8_t *bmq = bm1k + H * T + 64 - ((H * T) & 15);  // 16-byte aligned
@@ -1944,8 +1942,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
         hipLaunchKernelGGL(k_mark_terms, dim3((unsigned)std::min<int64_t>((nterm - tbase + 255) / 256, 8192)), dim3(256),
                            0, st, d_terms + tbase, nterm - tbase, V, mark);
       size_t tbb = 0;
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, mark, rowo, (int)V + 1, st));
-      SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, mark, rowo, (int)V + 1, st));
+      excl_scan(mark, rowo, (int64_t)(V + 1), cx->ws[23], st);
       int32_t nrows32 = 0;
       SME_HIP(hipMemcpyAsync(&nrows32, rowo + V, sizeof(int32_t), hipMemcpyDeviceToHost, st));
       SME_HIP(hipStreamSynchronize(st));
@@ -1984,8 +1981,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           const unsigned gV = (unsigned)std::min<int64_t>((V + 255) / 256, 8192);
           hipLaunchKernelGGL(k_term_rows, dim3(gV), dim3(256), 0, st, mark, rowo, V, off, tor, rdf);
           SME_HIP(hipMemsetAsync(rdf + nrows, 0, sizeof(int64_t), st));
-          SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tbb, rdf, rpre, (int)nrows + 1, st));
-          SME_HIP(hipcub::DeviceScan::ExclusiveSum(cx->cub_tmp.get(tbb), tbb, rdf, rpre, (int)nrows + 1, st));
+          excl_scan(rdf, rpre, (int64_t)(nrows + 1), cx->ws[23], st);
           // tile skip table (k_query_bm); the window path builds its window
           // table directly and the tile table only if a query falls back
           build_sk = [=, &W, &sk]() {

@@ -11,7 +11,6 @@
 //   " " record postings: (0,0) then the previous record's (docno,1) for every later record
 //              (the mapper's shared posting object, TermKGramDocIndexer.java:84-90,126,132-133)
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
@@ -94,14 +93,47 @@ __global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int3
   for (int64_t t = blockIdx.x * wpb + (threadIdx.x >> 6); t < V; t += (int64_t)gridDim.x * wpb) {
     const int64_t p0 = off[t], df = off[t + 1] - off[t];
     uint8_t *o = out + rec_off[t];
+    // K = 1 and an all-ASCII term (every c2 / c5 term): each modified-UTF-8 byte
+    // is one unit, and the lanes write the record header one byte each (a lane-0
+    // byte loop per term cost most of the pass on c5's 8.9 M short terms)
+    bool ascii = K == 1;
+    if (ascii) {
+      for (int64_t i = toff[t] + lane; i < toff[t + 1]; i += 64) ascii &= tch[i] >= 1 && tch[i] <= 0x7F;
+      ascii = __all(ascii);
+    }
     int64_t ul = 0;
-    for (int j = 0; j < K; j++) {
-      const int64_t c = comp_of(gram, K, t, j);
-      for (int64_t i = toff[c]; i < toff[c + 1]; i++) ul += mutf8_unit_len(tch[i]);
+    if (ascii) {
+      ul = toff[t + 1] - toff[t];
+    } else {
+      for (int j = 0; j < K; j++) {
+        const int64_t c = comp_of(gram, K, t, j);
+        for (int64_t i = toff[c]; i < toff[c + 1]; i++) ul += mutf8_unit_len(tch[i]);
+      }
     }
     const int64_t key = 4 + 2 * (int64_t)K + ul + 4, val = 4 + (df > 0 ? 2 + kClassLen + 8 * df : 0);
     uint8_t *post = o + 8 + key + 4 + 2 + kClassLen;
-    if (lane == 0) {
+    if (ascii) {
+      const int64_t hdr = 14 + ul + 8 + (df > 0 ? 2 + kClassLen : 0);
+      const uint16_t *u = tch + toff[t];
+      for (int64_t j = lane; j < hdr; j += 64) {
+        uint32_t b;
+        auto be = [](uint32_t v, int64_t i) { return (v >> (8 * (3 - i))) & 0xFFu; };
+        if (j < 4) b = be((uint32_t)(key + val), j);
+        else if (j < 8) b = be((uint32_t)key, j - 4);
+        else if (j < 12) b = be(1u, j - 8);
+        else if (j < 14) b = j == 12 ? (uint32_t)(ul >> 8) & 0xFFu : (uint32_t)ul & 0xFFu;
+        else if (j < 14 + ul) b = u[j - 14];
+        else {
+          const int64_t q = j - 14 - ul;
+          if (q < 4) b = be(1u, q);  // stored df of a real term (T1)
+          else if (q < 8) b = be((uint32_t)df, q - 4);
+          else if (q == 8) b = 0;
+          else if (q == 9) b = (uint32_t)kClassLen;
+          else b = (uint8_t)"sa.edu.kaust.io.PostingWritable"[q - 10];
+        }
+        o[j] = (uint8_t)b;
+      }
+    } else if (lane == 0) {
       put_be32(o, (uint32_t)(key + val));
       put_be32(o + 4, (uint32_t)key);
       put_be32(o + 8, (uint32_t)K);
@@ -167,7 +199,7 @@ __global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int3
   }
 }
 
-__global__ void k_ser_space(const int32_t *rec_docno, int64_t N, uint8_t *o) {
+__global__ void k_ser_space(const int32_t *rec_docno, const uint8_t *first, int64_t N, uint8_t *o) {
   // key: k=1, writeUTF(" "), df = N ; value: n = N, class, postings
   const int64_t key = 11, val = 4 + 2 + kClassLen + 8 * N;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -185,9 +217,11 @@ __global__ void k_ser_space(const int32_t *rec_docno, int64_t N, uint8_t *o) {
   }
   uint8_t *post = o + 25 + kClassLen;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t d = i == 0 ? 0u : (uint32_t)rec_docno[i - 1];
-    put_be32(post + 8 * i, d);
-    put_be32(post + 8 * i + 4, i == 0 ? 0u : 1u);
+    // every map task's list starts with the fresh (0, 0) posting (merged shard
+    // pieces: several tasks, `first` marks their first records)
+    const bool f = i == 0 || (first && first[i]);
+    put_be32(post + 8 * i, f ? 0u : (uint32_t)rec_docno[i - 1]);
+    put_be32(post + 8 * i + 4, f ? 0u : 1u);
   }
 }
 
@@ -235,13 +269,15 @@ void serialize_index(sme_index *ix, hipStream_t st) {
   if (V > 0) {
     int bits = 1;
     while ((1 << bits) < R) bits++;
-    size_t tb = 0;
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, part, part2, idx, idx2, (int)V, 0, bits, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortPairs(ix->ctx->cub_tmp.get(tb), tb, part, part2, idx, idx2, (int)V, 0, bits,
-                                               st));
+    // terms grouped by partition, term order kept (stable LSD radix, sme_sort.hip);
+    // the sort runs on a copy of the partition ids (part stays per term)
+    uint32_t *pk = W[21].as<uint32_t>(V + 1);
+    SME_HIP(hipMemcpyAsync(pk, part, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    uint32_t *rscr = W[20].as<uint32_t>(kv_sort_scratch(V) / sizeof(uint32_t) + 1);
+    uint32_t *grp = kv_sort<uint32_t>(pk, idx, part2, idx2, V, bits, rscr, st, false);
+    idx2 = grp;
     hipLaunchKernelGGL(k_gather_bytes, dim3(G), dim3(256), 0, st, idx2, rec_bytes, V, grp_bytes);
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, grp_bytes, scan, (int)V, st));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(ix->ctx->cub_tmp.get(tb), tb, grp_bytes, scan, (int)V, st));
+    excl_scan<int64_t>(grp_bytes, scan, V, W[22], st);
     int64_t *rec_off = grp_bytes;  // reuse after scan
     hipLaunchKernelGGL(k_ser_offsets, dim3(G), dim3(256), 0, st, idx2, scan, V, part, part_sp, sp_bytes, rec_off);
     hipLaunchKernelGGL(k_ser_write, dim3((unsigned)std::min<int64_t>((V + 3) / 4, 65536)), dim3(256), 0, st,
@@ -252,7 +288,8 @@ void serialize_index(sme_index *ix, hipStream_t st) {
   }
   if (N > 0) {
     hipLaunchKernelGGL(k_ser_space, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 8192)), dim3(256), 0, st,
-                       (const int32_t *)ix->d_rec_docno.p, N, out + ix->part_start[part_sp]);
+                       (const int32_t *)ix->d_rec_docno.p, (const uint8_t *)ix->d_rec_first.p, N,
+                       out + ix->part_start[part_sp]);
     SME_CHECK_LAUNCH();
   }
   SME_HIP(hipEventRecord(ev[3], st));

@@ -532,6 +532,121 @@ __global__ __launch_bounds__(kRsNT) void k_kv_scatter(const K *__restrict__ key,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Device-wide exclusive scan (reduce-then-scan, no inter-block waiting): one
+// 4096-item tile per 256-thread block.  k_sc_sums: each tile's sum (coalesced
+// loads, a wave reduction); k_sc_carry: one block scans the tile sums in place
+// (rounds of 4096, a running carry); k_sc_apply: each tile staged in LDS, each
+// thread scans 16 contiguous items, the block scans the thread totals, and the
+// results go out with the tile's carry.  in == out is allowed.
+constexpr int kScNT = 256, kScIPT = 16, kScTile = kScNT * kScIPT;
+
+template <typename T>
+__device__ __forceinline__ T sc_block_excl(T v, T *ws, T *total) {  // 256 threads
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  T incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const T u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) ws[w] = incl;
+  __syncthreads();
+  T base = 0, tot = 0;
+  for (int j = 0; j < kScNT / 64; j++) {
+    if (j < w) base += ws[j];
+    tot += ws[j];
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScNT) void k_sc_sums(const T *__restrict__ in, int64_t n, T *__restrict__ sums) {
+  __shared__ T ws[kScNT / 64];
+  const int64_t t0 = (int64_t)blockIdx.x * kScTile;
+  T s = 0;
+#pragma unroll
+  for (int j = 0; j < kScIPT; j++) {
+    const int64_t i = t0 + j * kScNT + threadIdx.x;
+    if (i < n) s += in[i];
+  }
+  T tot;
+  (void)sc_block_excl<T>(s, ws, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScNT) void k_sc_carry(T *__restrict__ a, int64_t n) {
+  __shared__ T ws[kScNT / 64];
+  T carry = 0;
+  for (int64_t r0 = 0; r0 < n; r0 += kScTile) {
+    const int64_t i0 = r0 + (int64_t)threadIdx.x * kScIPT;
+    T x[kScIPT], s = 0;
+#pragma unroll
+    for (int j = 0; j < kScIPT; j++) {
+      x[j] = i0 + j < n ? a[i0 + j] : (T)0;
+      s += x[j];
+    }
+    T tot;
+    T run = carry + sc_block_excl<T>(s, ws, &tot);
+#pragma unroll
+    for (int j = 0; j < kScIPT; j++) {
+      if (i0 + j < n) a[i0 + j] = run;
+      run += x[j];
+    }
+    carry += tot;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScNT) void k_sc_apply(const T *in, T *out, int64_t n, const T *__restrict__ carry) {
+  // one pad slot every 16 items: thread t's 16 contiguous items start at bank 17 t
+  __shared__ T st[kScTile + kScTile / 16];
+  __shared__ T ws[kScNT / 64];
+  auto P = [](int i) { return i + (i >> 4); };
+  const int64_t t0 = (int64_t)blockIdx.x * kScTile;
+#pragma unroll
+  for (int j = 0; j < kScIPT; j++) {
+    const int64_t i = t0 + j * kScNT + threadIdx.x;
+    st[P(j * kScNT + threadIdx.x)] = i < n ? in[i] : (T)0;
+  }
+  __syncthreads();
+  T x[kScIPT], s = 0;
+#pragma unroll
+  for (int j = 0; j < kScIPT; j++) {
+    x[j] = st[P(threadIdx.x * kScIPT + j)];
+    s += x[j];
+  }
+  T tot;
+  T run = carry[blockIdx.x] + sc_block_excl<T>(s, ws, &tot);
+#pragma unroll
+  for (int j = 0; j < kScIPT; j++) {
+    st[P(threadIdx.x * kScIPT + j)] = run;
+    run += x[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kScIPT; j++) {
+    const int64_t i = t0 + j * kScNT + threadIdx.x;
+    if (i < n) out[i] = st[P(j * kScNT + threadIdx.x)];
+  }
+}
+
+// compaction: out[k] = i for the k-th i in [0, n) with flag[i] != 0 (ascending),
+// *count = the number of them; pos = exclusive scan of the flags (as int64)
+__global__ void k_flags_i64(const uint8_t *__restrict__ f, int64_t n, int64_t *__restrict__ v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[i] = f[i] ? 1 : 0;
+}
+__global__ void k_select_scatter(const uint8_t *__restrict__ f, const int64_t *__restrict__ pos, int64_t n,
+                                 int32_t *__restrict__ out, int32_t *__restrict__ count) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (f[i]) out[pos[i]] = (int32_t)i;
+    if (i == n - 1) *count = (int32_t)(pos[i] + (f[i] ? 1 : 0));
+  }
+}
+
 }  // namespace
 
 // Stable sort of P (key, packed value) pairs by the low `bits` bits of key.
@@ -631,6 +746,34 @@ template uint32_t *kv_sort<uint64_t>(uint64_t *, uint32_t *, uint64_t *, uint32_
                                      hipStream_t, bool);
 template uint32_t *kv_sort<uint32_t>(uint32_t *, uint32_t *, uint32_t *, uint32_t *, int64_t, int, uint32_t *,
                                      hipStream_t, bool);
+
+template <typename T>
+void excl_scan(const T *in, T *out, int64_t n, DevBuf &scratch, hipStream_t st) {
+  if (n <= 0) return;
+  const int64_t nt = (n + kScTile - 1) / kScTile;
+  T *sums = scratch.as<T>((size_t)nt + 1);
+  hipLaunchKernelGGL(k_sc_sums<T>, dim3((unsigned)nt), dim3(kScNT), 0, st, in, n, sums);
+  hipLaunchKernelGGL(k_sc_carry<T>, dim3(1), dim3(kScNT), 0, st, sums, nt);
+  hipLaunchKernelGGL(k_sc_apply<T>, dim3((unsigned)nt), dim3(kScNT), 0, st, in, out, n, (const T *)sums);
+  SME_CHECK_LAUNCH();
+}
+template void excl_scan<int64_t>(const int64_t *, int64_t *, int64_t, DevBuf &, hipStream_t);
+template void excl_scan<int32_t>(const int32_t *, int32_t *, int64_t, DevBuf &, hipStream_t);
+template void excl_scan<uint32_t>(const uint32_t *, uint32_t *, int64_t, DevBuf &, hipStream_t);
+
+void select_flagged(const uint8_t *flag, int64_t n, int32_t *out, int32_t *d_count, DevBuf &s1, DevBuf &s2,
+                    hipStream_t st) {
+  if (n <= 0) {
+    SME_HIP(hipMemsetAsync(d_count, 0, sizeof(int32_t), st));
+    return;
+  }
+  int64_t *pos = s1.as<int64_t>((size_t)n);
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_flags_i64, dim3(g), dim3(256), 0, st, flag, n, pos);
+  excl_scan<int64_t>(pos, pos, n, s2, st);
+  hipLaunchKernelGGL(k_select_scatter, dim3(g), dim3(256), 0, st, flag, pos, n, out, d_count);
+  SME_CHECK_LAUNCH();
+}
 
 size_t kv_sort_scratch(int64_t n) {
   const int64_t ntiles = (std::max<int64_t>(n, 1) + kRsTile - 1) / kRsTile;

@@ -17,14 +17,19 @@ the small global statistics and the query results:
   global_df_index  the same for a libsme shard, keyed by 128-bit device term
                    fingerprints, exchanged by owner rank (df_exchange: all_to_all
                    to the owner, dedup of 1/W of the terms, all_to_all back)
+  reference_partitions  the reference's R term-partitioned part files from the
+                   shards: all_to_all of per-owner term/postings blobs, per-term
+                   reducer merge on the owner (sme_merge_pieces)
   merge_topk_owner per-shard top-k -> global top-k of the queries a rank owns
                    (query-owner all_to_all of Q x k x (4 + 8) B, score desc,
                    docno asc); merge_topk also all_gathers the merged slices
 
 Exactness: with docids unique across shards (every synthetic corpus), the sharded
 result equals the single-index result bit for bit: a document's score only uses its
-own postings, and N / df are the global ones.  A docid duplicated ACROSS shards would
-be merged by the reference's single reducer but stays two postings here.
+own postings, and N / df are the global ones.  A docid duplicated ACROSS shards is
+merged by the reference's single reducer: reference_partitions merges it the same
+way (tf summed); the per-shard query path cannot (two partial postings), so
+shard_docno_duplicates detects it so callers can refuse to score such shards.
 """
 import importlib
 
@@ -242,6 +247,92 @@ def global_df_index(ix, group=None, timings=None):
     if timings is not None:
         timings.update(fingerprints_ms=(t1 - t0) * 1e3)
     return out
+
+
+def reference_partitions(ix, group=None, timings=None):
+    """The reference's R part files from doc shards (last row): this
+    shard's terms and reduce-order postings go, per term partition p
+    ((Arrays.hashCode & MAX) % R, TermDF.java:79-81), to rank p % W in one
+    all_to_all of self-describing blobs (sme_index_pack_pieces); every rank
+    merges what it received per term exactly as the single reducer would
+    (MyReducer.reduce, TermKGramDocIndexer.java:189-211: docno sort, equal
+    docnos -- a docid duplicated across shards -- summed, stable tf-desc sort;
+    sme_merge_pieces).  Returns (records-only Index, the partitions this rank
+    owns): read them with Index.partition_records(p)."""
+    import time
+    sme = importlib.import_module(__package__)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = _dev(group)
+    t0 = time.perf_counter()
+    sizes = ix.pack_pieces(world)
+    send = torch.empty(max(sum(sizes), 16), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    ix.pack_pieces(world, send.data_ptr())
+    t1 = time.perf_counter()
+    cnt = torch.tensor(sizes, dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    rsizes = rcnt.tolist()
+    recv = torch.empty(max(sum(rsizes), 16), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(recv[:sum(rsizes)], send[:sum(sizes)].to(dev), rsizes, sizes, group=group)
+    recv = recv.to("cuda")
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    merged = ix.ctx.merge_pieces(recv.data_ptr(), rsizes)
+    del send, recv
+    t3 = time.perf_counter()
+    R = ix.ctx.num_partitions
+    if timings is not None:
+        timings.update(pack_ms=(t1 - t0) * 1e3, exchange_ms=(t2 - t1) * 1e3, merge_ms=(t3 - t2) * 1e3,
+                       bytes_out=int(sum(sizes)), bytes_in=int(sum(rsizes)))
+    return merged, [p for p in range(R) if p % world == rank]
+
+
+def docno_duplicates(docnos, group=None):
+    """Number of distinct docnos that more than one shard holds (docnos: this
+    shard's record docnos, an int64 tensor on the collective's device).  Disjoint
+    [min, max] ranges answer 0 at once (all_gather of 16 B); otherwise each rank
+    sends its distinct docnos to owner docno mod W, and owners count the values
+    that arrive from more than one shard.  A docid duplicated across shards is
+    one posting with summed tf in the reference's single reducer
+    (TermKGramDocIndexer.java:202-210); per-shard scoring would keep two."""
+    world = dist.get_world_size(group)
+    dev = docnos.device
+    n = int(docnos.shape[0])
+    big = 1 << 62
+    mm = torch.tensor([int(docnos.min()) if n else big, int(docnos.max()) if n else -big], dtype=torch.int64, device=dev)
+    alls = [torch.empty_like(mm) for _ in range(world)]
+    dist.all_gather(alls, mm, group=group)
+    rng = sorted((int(a[0]), int(a[1])) for a in alls if int(a[0]) <= int(a[1]))
+    if all(rng[i][1] < rng[i + 1][0] for i in range(len(rng) - 1)):
+        return 0
+    u = torch.unique(docnos) if n else docnos
+    owner = torch.remainder(u, world)
+    order = torch.argsort(owner, stable=True)
+    u = u[order].contiguous()
+    cnt = torch.bincount(owner, minlength=world).to(torch.int64)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    recv = torch.empty(int(rcnt.sum()), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv, u, rcnt.tolist(), cnt.tolist(), group=group)
+    if recv.numel():
+        _, c = torch.unique(recv, return_counts=True)
+        dup = torch.tensor([int((c > 1).sum())], dtype=torch.int64, device=dev)
+    else:
+        dup = torch.zeros(1, dtype=torch.int64, device=dev)
+    dist.all_reduce(dup, group=group)
+    return int(dup.item())
+
+
+def shard_docno_duplicates(ix, group=None):
+    """docno_duplicates over a libsme shard index's record docnos."""
+    sme = importlib.import_module(__package__)
+    ptr, n = ix.record_docnos_ptr()
+    d = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    if n:
+        sme.memcpy(d.data_ptr(), ptr, 4 * n, None)
+    return docno_duplicates(d[:n].to(torch.int64).to(_dev(group)), group)
 
 
 def owner_bounds(nq, world):

@@ -10,7 +10,10 @@ and every rank scores the golden queries on its shard.  The query-owner merge
 (dist.merge_topk_owner) must give, for the queries this rank owns, exactly the
 docnos and fp64 score bits the single-index CPU oracle produced for the whole
 corpus (tests/golden/scale_c4multi.json, tools/gen_scale_golden.py) -- the
-reference's one global reduce (TermKGramDocIndexer.java:175-183,246).
+reference's one global reduce (TermKGramDocIndexer.java:175-183,246).  The
+shards' reference_partitions (term-partition all_to_all + per-term reducer merge)
+must reproduce the oracle's R = 10 part files for the same 4 map tasks
+(scale_c4multi.json split_parts, tools/gen_scale_golden.py c4multi-parts).
 usage: dist_c4_worker.py RANK WORLD PORT OUT_DIR"""
 import importlib
 import json
@@ -63,8 +66,9 @@ def main():
         mapping = synth.mapping_bytes(c["n"])
         timing = {"rank": rank}
         checked = []
+        sp = g["split_parts"]  # the oracle's R = 10 part files for these 4 map tasks
         for idf_mode in (0, 1):
-            ctx = sme.Context(1, 1, idf_mode)
+            ctx = sme.Context(1, sp["R"], idf_mode)
             cuts = D.split_points(corpus, world, ctx)
             ctx.load_docno_mapping(mapping)
             ix = ctx.build_device(corpus.ptr + cuts[rank], cuts[rank + 1] - cuts[rank])
@@ -77,6 +81,20 @@ def main():
             t["total_ms"] = (time.perf_counter() - t0) * 1e3
             assert t["global_terms"] == g["V"]  # the union of the shard vocabularies
             timing["df_exchange_mode%d" % idf_mode] = t
+            if idf_mode == 0:
+                # reference-layout output: the shards' postings merged per term on
+                # the partition owners equal the single reducer's R part files
+                assert cuts == sp["cuts"] and world == sp["world"]
+                assert D.shard_docno_duplicates(ix) == 0
+                tp = {}
+                t0 = time.perf_counter()
+                merged, owned = D.reference_partitions(ix, timings=tp)
+                tp["total_ms"] = (time.perf_counter() - t0) * 1e3
+                import common
+                for p in owned:
+                    assert common.canon_digest(merged.partition_records(p)) == sp["parts"][p], p
+                timing["reference_partitions"] = tp
+                merged.close()
             ix.reweight(N, gdf.data_ptr() if idf_mode == 1 else None)
             for group in g["queries"]:
                 if group["idf_mode"] == idf_mode:

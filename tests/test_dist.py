@@ -176,3 +176,32 @@ def test_df_exchange_owner_gloo(tmp_path, world, collide):
     dedup there, all_to_all back) equals the brute-force sum over shards."""
     mp.spawn(_dfx_worker, args=(world, _free_port(), str(tmp_path), collide), nprocs=world, join=True)
     assert all((tmp_path / ("ok%d" % r)).exists() for r in range(world))
+
+
+def _dup_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        D = importlib.import_module(PKG + ".dist")
+        # disjoint ranges: 0 without the exchange
+        d = torch.arange(100 * rank, 100 * rank + 100, dtype=torch.int64)
+        assert D.docno_duplicates(d) == 0
+        # overlapping ranges, no duplicates (interleaved), one shard empty
+        d = torch.arange(rank, 600, world, dtype=torch.int64) if rank != 1 else torch.zeros(0, dtype=torch.int64)
+        assert D.docno_duplicates(d) == 0
+        # duplicates: 7 and 42 in every shard, -3 (an unmapped docid) in shards 0 and 1,
+        # 99 twice inside shard 0 only (not a cross-shard duplicate)
+        extra = [7, 42] + ([-3] if rank < 2 else []) + ([99, 99] if rank == 0 else [])
+        d = torch.tensor(extra + list(range(1000 + 10 * rank, 1010 + 10 * rank)), dtype=torch.int64)
+        assert D.docno_duplicates(d) == (3 if world >= 2 else 0)
+        open(os.path.join(out_dir, "ok%d" % rank), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_docno_duplicates_gloo(tmp_path, world):
+    """Docnos held by more than one shard (a docid duplicated across doc shards):
+    counted exactly, duplicates inside one shard excluded."""
+    mp.spawn(_dup_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert all((tmp_path / ("ok%d" % r)).exists() for r in range(world))

@@ -58,3 +58,13 @@ def test_c4_four_shards(tmp_path):
     t = [json.load(open(tmp_path / ("timing%d.json" % r))) for r in range(4)]
     assert sum(x["queries_checked"] for x in t) == 1100
     print("df exchange (rank 0, gloo):", json.dumps(t[0]["df_exchange_mode1"]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_reference_partitions(tmp_path, world):
+    """Reference-layout output from doc shards: the term-partition all_to_all of
+    postings and the owners' per-term reducer merge give exactly the oracle's R
+    part files for the same map tasks (R = 10 and 3), with docids duplicated
+    across shards merged as the single reducer merges them
+    (tests/dist_parts_worker.py)."""
+    _run_ranks("dist_parts_worker.py", world, [], tmp_path, 240)
