@@ -10,8 +10,12 @@
  *   records     XMLRecordReader (XMLInputFormat.java:110-143,173-198), one split
  *   docno       TrecDocument.getDocid + Arrays.binarySearch over the mapping
  *               (TrecDocument.java:76-89, TrecDocnoMapping.java:67-69)
- *   tokens      GalagoTokenizer.processContent (GalagoTokenizer.java:139-183):
- *               the oracle's TagTokenizer, stopword hash set, per-thread stem cache
+ *   tokens      GalagoTokenizer.processContent (GalagoTokenizer.java:139-183): a
+ *               byte-level TagTokenizer for records of simple markup (the device's
+ *               fast path: raw tokens = runs of non-split bytes outside tag /
+ *               entity spans), each DISTINCT raw token normalized, stop-filtered
+ *               and stemmed once per thread (T13); other records through the
+ *               oracle's TagTokenizer
  *   postings    MyReducer.reduce (TermKGramDocIndexer.java:168-213): per term
  *               docno asc with duplicate docnos merged, then stable tf desc
  *   terms       TermDF.compareTo order (String.compareTo on UTF-16 units), K = 1
@@ -20,11 +24,15 @@
  *               docno asc
  */
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <omp.h>
 #include <stdint.h>
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -78,6 +86,146 @@ int jcmp(const u16s &a, const u16s &b) {
   return (int)a.size() - (int)b.size();
 }
 
+// TagTokenizer split bytes (TagTokenizer.java:73-95): 0..32 and ;"&/:!#?$%()@^*+-,=><[]{}|`~_
+struct SplitTab {
+  bool t[256];
+  SplitTab() {
+    for (int c = 0; c < 256; c++) t[c] = c <= 32 || (c < 128 && strchr(";\"&/:!#?$%()@^*+-,=><[]{}|`~_", c) != nullptr);
+  }
+};
+const SplitTab kSplit;
+inline bool split_byte(uint8_t c) { return kSplit.t[c]; }
+// span end (inclusive) of the markup at '<' p of a simple record (sme_build.hip lt_span_end)
+int64_t lt_end(const uint8_t *t, int64_t n, int64_t p) {
+  if (p + 1 >= n) return n;
+  const uint8_t c = t[p + 1];
+  if (c == '!' && p + 3 < n && t[p + 2] == '-' && t[p + 3] == '-') {
+    for (int64_t i = p + 1; i + 2 < n; i++)
+      if (t[i] == '-' && t[i + 1] == '-' && t[i + 2] == '>') return i + 2;
+    return n;
+  }
+  if (c == '?') {
+    for (int64_t i = p + 1; i + 1 < n; i++)
+      if (t[i] == '?' && t[i + 1] == '>') return i + 1;
+    return n;
+  }
+  for (int64_t i = p + (c == '/' ? 2 : 1); i < n; i++)
+    if (t[i] == '>') return i;
+  return n;
+}
+// entity span end: '&' [a-z0-9#]* ';' (TagTokenizer.onAmpersand 644-662); p if none
+int64_t amp_end(const uint8_t *t, int64_t n, int64_t p) {
+  for (int64_t i = p + 1; i < n; i++) {
+    const uint8_t d = t[i];
+    if ((d >= 'a' && d <= 'z') || (d >= '0' && d <= '9') || d == '#') continue;
+    return d == ';' ? i : p;
+  }
+  return p;
+}
+// every '<' of the record is markup the byte-level path reproduces exactly
+// (sme_build.hip lt_simple: terminated, no '<' inside, begin tags without space /
+// non-ASCII before '>', not script / style)
+bool simple_record(const uint8_t *t, int64_t n) {
+  for (const uint8_t *q = (const uint8_t *)memchr(t, '<', (size_t)n); q;
+       q = (const uint8_t *)memchr(q + 1, '<', (size_t)(t + n - q - 1))) {
+    const int64_t p = q - t;
+    if (p + 1 >= n) return false;
+    const uint8_t c = t[p + 1];
+    if (c == '/' || c == '!' || c == '?') {
+      int64_t e;
+      if (c == '/') {
+        e = n;
+        for (int64_t i = p + 2; i < n; i++)
+          if (t[i] == '>') {
+            e = i;
+            break;
+          }
+      } else if (c == '!' && !(p + 3 < n && t[p + 2] == '-' && t[p + 3] == '-')) {
+        e = n;
+        for (int64_t i = p + 1; i < n; i++)
+          if (t[i] == '>') {
+            e = i;
+            break;
+          }
+      } else {
+        e = lt_end(t, n, p);
+      }
+      if (e >= n) return false;
+      for (int64_t i = p + 1; i <= e; i++)
+        if (t[i] == '<') return false;
+      continue;
+    }
+    int64_t i = p + 1;
+    for (; i < n; i++) {
+      const uint8_t x = t[i];
+      if (x == '>') break;
+      if (x == ' ' || x >= 0x80 || x == '<') return false;
+    }
+    if (i >= n) return false;
+    const int64_t l = i - (p + 1);
+    auto lc = [&](int64_t k) { const uint8_t x = t[p + 1 + k]; return (x >= 'A' && x <= 'Z') ? x + 32 : x; };
+    if (l == 6 && lc(0) == 's' && lc(1) == 'c' && lc(2) == 'r' && lc(3) == 'i' && lc(4) == 'p' && lc(5) == 't')
+      return false;
+    if (l == 5 && lc(0) == 's' && lc(1) == 't' && lc(2) == 'y' && lc(3) == 'l' && lc(4) == 'e') return false;
+  }
+  return true;
+}
+
+// open-addressing table of distinct raw tokens (byte strings): lookup returns the
+// token's id (insertion order); lp / ll hold each id's bytes
+struct RawTab {
+  struct E {
+    uint64_t h;  // hash | 1; 0 = empty
+    const uint8_t *p;
+    int32_t len, id;
+  };
+  std::vector<E> e;
+  std::vector<const uint8_t *> lp;
+  std::vector<int32_t> ll;
+  uint64_t mask = 0;
+  RawTab() { rehash(1 << 14); }
+  static uint64_t hash(const uint8_t *s, int64_t l) {
+    uint64_t x = 0x9E3779B97F4A7C15ull ^ (uint64_t)l;
+    int64_t i = 0;
+    for (; i + 8 <= l; i += 8) {
+      uint64_t w;
+      memcpy(&w, s + i, 8);
+      x = (x ^ w) * 0xFF51AFD7ED558CCDull;
+      x ^= x >> 32;
+    }
+    uint64_t w = 0;
+    memcpy(&w, s + i, (size_t)(l - i));
+    x = (x ^ w) * 0xC4CEB9FE1A85EC53ull;
+    x ^= x >> 29;
+    return x | 1ull;
+  }
+  void rehash(uint64_t cap) {
+    std::vector<E> o(cap, E{0, nullptr, 0, 0});
+    for (const E &x : e) {
+      if (!x.h) continue;
+      uint64_t s = x.h & (cap - 1);
+      while (o[s].h) s = (s + 1) & (cap - 1);
+      o[s] = x;
+    }
+    e.swap(o);
+    mask = cap - 1;
+  }
+  int32_t lookup(const uint8_t *s, int64_t l) {
+    const uint64_t x = hash(s, l);
+    uint64_t i = x & mask;
+    while (e[i].h) {
+      if (e[i].h == x && e[i].len == l && memcmp(e[i].p, s, (size_t)l) == 0) return e[i].id;
+      i = (i + 1) & mask;
+    }
+    const int32_t id = (int32_t)lp.size();
+    lp.push_back(s);
+    ll.push_back((int32_t)l);
+    e[i] = E{x, s, (int32_t)l, id};
+    if (2 * lp.size() > mask + 1) rehash(2 * (mask + 1));
+    return id;
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -122,37 +270,49 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   }
   const auto recs = records(corpus, n);
   const int64_t nR = (int64_t)recs.size();
-  // per record: docno and its (term, tf) pairs (term as string, aggregated)
+  // Three phases, no locks; every DISTINCT raw token is normalized, stop-filtered
+  // and stemmed once (T13):
+  //  1. per record (threads): docno; raw tokens by the byte-level TagTokenizer
+  //     into the thread's table of distinct raw tokens (local ids per record);
+  //     records of complex markup through the oracle's TagTokenizer (terms)
+  //  2. the threads' distinct raw tokens merged into one table, each normalized
+  //     once (in parallel); the vocabulary = the sorted distinct outputs
+  //  3. per record (threads): local raw ids -> term ids -> tf
+  const int nthr = omp_get_max_threads();
   std::vector<int32_t> rdocno((size_t)nR);
-  std::vector<std::vector<std::pair<u16s, int32_t>>> rterms((size_t)nR);
+  std::vector<std::vector<int32_t>> rtok((size_t)nR);   // local raw ids (simple records)
+  std::vector<std::vector<u16s>> rterm((size_t)nR);     // terms (complex records)
+  std::vector<int16_t> rthr((size_t)nR);
+  std::vector<RawTab> tabs((size_t)nthr);
   int fail = 0;
 #pragma omp parallel reduction(| : fail)
   {
-    std::unordered_map<u16s, u16s, U16Hash> stem_cache;
+    const int me = omp_get_thread_num();
+    RawTab &raw = tabs[(size_t)me];
     jstr text, st;
     js_init(&text);
     js_init(&st);
     jstr_list toks;
     jl_init(&toks);
-    std::unordered_map<u16s, int32_t, U16Hash> tfm;
 #pragma omp for schedule(dynamic, 64)
     for (int64_t r = 0; r < nR; r++) {
-      utf8_to_utf16(corpus + recs[(size_t)r].first, recs[(size_t)r].second, &text);
-      // getDocid: trim(substring(indexOf("<DOCNO>") + 7, indexOf("</DOCNO>", start)))
-      static const char16_t O[] = u"<DOCNO>", Cl[] = u"</DOCNO>";
-      const u16s doc((const char16_t *)text.p, (size_t)text.n);
+      const uint8_t *b = corpus + recs[(size_t)r].first;
+      const int64_t len = (int64_t)recs[(size_t)r].second;
+      // getDocid: trim(substring(indexOf("<DOCNO>") + 7, indexOf("</DOCNO>", start)));
+      // the tags are ASCII, so byte offsets locate the same characters
       u16s docid;
-      const size_t a = doc.find(O);
-      if (a != u16s::npos) {
-        const size_t e = doc.find(Cl, a);
-        if (e == u16s::npos || e < a + 7) {
+      const uint8_t *a = (const uint8_t *)memmem(b, (size_t)len, "<DOCNO>", 7);
+      if (a) {
+        const uint8_t *e = (const uint8_t *)memmem(a + 7, (size_t)(b + len - (a + 7)), "</DOCNO>", 8);
+        if (!e) {
           fail |= 1;
           continue;
         }
-        size_t b0 = a + 7, e0 = e;
-        while (b0 < e0 && doc[b0] <= 0x20) b0++;
-        while (e0 > b0 && doc[e0 - 1] <= 0x20) e0--;
-        docid = doc.substr(b0, e0 - b0);
+        const uint8_t *b0 = a + 7, *e0 = e;
+        while (b0 < e0 && *b0 <= 0x20) b0++;
+        while (e0 > b0 && e0[-1] <= 0x20) e0--;
+        utf8_to_utf16(b0, (size_t)(e0 - b0), &text);
+        docid.assign((const char16_t *)text.p, (size_t)text.n);
       }
       int lo = 0, hi = (int)ids.size() - 1, dn = 0;  // Arrays.binarySearch
       bool found = false;
@@ -168,64 +328,174 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
         }
       }
       rdocno[(size_t)r] = found ? dn : -(lo + 1);
-      for (int i = 0; i < toks.n; i++) js_free(&toks.v[i]);
-      toks.n = 0;
-      or_tag_tokenize(text.p, text.n, &toks);
-      tfm.clear();
-      for (int i = 0; i < toks.n; i++) {
-        u16s w((const char16_t *)toks.v[i].p, (size_t)toks.v[i].n);
-        if (stop.count(w)) continue;
-        auto it = stem_cache.find(w);
-        if (it == stem_cache.end()) {
-          or_stem_js(toks.v[i].p, toks.v[i].n, &st);
-          it = stem_cache.emplace(w, u16s((const char16_t *)st.p, (size_t)st.n)).first;
+      rthr[(size_t)r] = (int16_t)me;
+      if (simple_record(b, len)) {
+        // byte-level TagTokenizer (the device's fast path, sme_build.hip k_tok_fast):
+        // raw tokens = maximal runs of non-split bytes starting outside every
+        // tag / comment / PI / entity span
+        auto &out = rtok[(size_t)r];
+        int64_t i = 0;
+        while (i < len) {
+          const uint8_t c = b[i];
+          if (c == '<') {
+            i = lt_end(b, len, i) + 1;
+            continue;
+          }
+          if (c == '&') {
+            i = amp_end(b, len, i) + 1;
+            continue;
+          }
+          if (split_byte(c)) {
+            i++;
+            continue;
+          }
+          int64_t j = i + 1;
+          while (j < len && !split_byte(b[j])) j++;
+          out.push_back(raw.lookup(b + i, j - i));
+          i = j;
         }
-        tfm[it->second]++;
+      } else {
+        // complex markup: the oracle's TagTokenizer over the decoded record
+        utf8_to_utf16(b, (size_t)len, &text);
+        for (int i = 0; i < toks.n; i++) js_free(&toks.v[i]);
+        toks.n = 0;
+        or_tag_tokenize(text.p, text.n, &toks);
+        for (int i = 0; i < toks.n; i++) {
+          u16s w((const char16_t *)toks.v[i].p, (size_t)toks.v[i].n);
+          if (stop.count(w)) continue;
+          or_stem_js(toks.v[i].p, toks.v[i].n, &st);
+          rterm[(size_t)r].emplace_back((const char16_t *)st.p, (size_t)st.n);
+        }
       }
-      auto &out = rterms[(size_t)r];
-      out.reserve(tfm.size());
-      for (auto &kv : tfm) out.emplace_back(kv.first, kv.second);
     }
     jl_free(&toks);
     js_free(&text);
     js_free(&st);
   }
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "tokens", omp_get_wtime() - t0);
   if (fail) return nullptr;
-  // vocabulary in String.compareTo order (UTF-16 unit order = u16string operator<)
-  std::vector<u16s> vocab;
-  {
-    const int nt = omp_get_max_threads();
-    std::vector<std::unordered_set<u16s, U16Hash>> loc((size_t)nt);
-#pragma omp parallel
-    {
-      auto &s = loc[(size_t)omp_get_thread_num()];
-#pragma omp for schedule(static)
-      for (int64_t r = 0; r < nR; r++)
-        for (auto &p : rterms[(size_t)r]) s.insert(p.first);
-    }
-    std::unordered_set<u16s, U16Hash> all;
-    for (auto &s : loc) all.insert(s.begin(), s.end());
-    vocab.assign(all.begin(), all.end());
-    std::sort(vocab.begin(), vocab.end());
+  // 2. one table of the distinct raw tokens (local id -> global id per thread)
+  RawTab glob;
+  std::vector<std::vector<int32_t>> lmap((size_t)nthr);
+  for (int t = 0; t < nthr; t++) {
+    const RawTab &tb = tabs[(size_t)t];
+    lmap[(size_t)t].resize(tb.lp.size());
+    for (size_t i = 0; i < tb.lp.size(); i++) lmap[(size_t)t][i] = glob.lookup(tb.lp[i], tb.ll[i]);
   }
+  const int64_t G = (int64_t)glob.lp.size();
+  // processContent of each distinct raw token, once (parallel)
+  std::vector<std::vector<u16s>> gout((size_t)G);
+#pragma omp parallel
+  {
+    jstr text, st;
+    js_init(&text);
+    js_init(&st);
+    jstr_list toks;
+    jl_init(&toks);
+#pragma omp for schedule(dynamic, 1024)
+    for (int64_t g = 0; g < G; g++) {
+      utf8_to_utf16(glob.lp[(size_t)g], (size_t)glob.ll[(size_t)g], &text);
+      for (int i = 0; i < toks.n; i++) js_free(&toks.v[i]);
+      toks.n = 0;
+      or_tag_tokenize(text.p, text.n, &toks);
+      for (int i = 0; i < toks.n; i++) {
+        u16s w((const char16_t *)toks.v[i].p, (size_t)toks.v[i].n);
+        if (stop.count(w)) continue;
+        or_stem_js(toks.v[i].p, toks.v[i].n, &st);
+        gout[(size_t)g].emplace_back((const char16_t *)st.p, (size_t)st.n);
+      }
+    }
+    jl_free(&toks);
+    js_free(&text);
+    js_free(&st);
+  }
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "normalize", omp_get_wtime() - t0);
+  // vocabulary in String.compareTo order (UTF-16 unit order = u16string operator<):
+  // the sorted distinct outputs.  Keys: units 0-3 and 4-7 (zero padded; no term
+  // unit is 0, a split character), so strings of <= 8 units compare by key alone
+  struct TK {
+    uint64_t k0, k1;
+    const u16s *s;
+  };
+  auto tkey = [](const u16s *w) {
+    TK t{0, 0, w};
+    for (size_t i = 0; i < 8; i++) {
+      const uint64_t u = i < w->size() ? (uint64_t)(uint16_t)(*w)[i] : 0ull;
+      if (i < 4) t.k0 = (t.k0 << 16) | u;
+      else t.k1 = (t.k1 << 16) | u;
+    }
+    return t;
+  };
+  auto tless = [](const TK &x, const TK &y) {
+    if (x.k0 != y.k0) return x.k0 < y.k0;
+    if (x.k1 != y.k1) return x.k1 < y.k1;
+    if (x.s->size() <= 8 && y.s->size() <= 8) return x.s->size() < y.s->size();
+    return *x.s < *y.s;
+  };
+  auto teq = [](const TK &x, const TK &y) {
+    return x.k0 == y.k0 && x.k1 == y.k1 && (x.s->size() <= 8 && y.s->size() <= 8 ? x.s->size() == y.s->size() : *x.s == *y.s);
+  };
+  std::vector<TK> keyed;
+  for (auto &v : gout)
+    for (auto &w : v) keyed.push_back(tkey(&w));
+  for (auto &v : rterm)
+    for (auto &w : v) keyed.push_back(tkey(&w));
+  std::sort(keyed.begin(), keyed.end(), tless);
+  std::vector<u16s> vocab;
+  std::vector<TK> vk;
+  for (size_t i = 0; i < keyed.size(); i++)
+    if (i == 0 || !teq(keyed[i], keyed[i - 1])) {
+      vocab.push_back(*keyed[i].s);
+      vk.push_back(keyed[i]);
+    }
+  keyed.clear();
+  keyed.shrink_to_fit();
   const int64_t V = (int64_t)vocab.size();
-  std::unordered_map<u16s, int32_t, U16Hash> tid;
-  tid.reserve((size_t)V * 2);
-  for (int64_t t = 0; t < V; t++) tid.emplace(vocab[(size_t)t], (int32_t)t);
-  // pairs by record, records in docno order (the reducer sorts postings by docno;
-  // stable, so equal docnos keep input order before they merge)
+  for (int64_t i = 0; i < V; i++) vk[(size_t)i].s = &vocab[(size_t)i];
+  auto term_of = [&](const u16s &w) {
+    const TK k = tkey(&w);
+    return (int32_t)(std::lower_bound(vk.begin(), vk.end(), k, tless) - vk.begin());
+  };
+  // term ids of every distinct raw token's outputs
+  std::vector<int32_t> go0((size_t)G + 1, 0);
+  for (int64_t g = 0; g < G; g++) go0[(size_t)g + 1] = go0[(size_t)g] + (int32_t)gout[(size_t)g].size();
+  std::vector<int32_t> gterm((size_t)go0[(size_t)G]);
+#pragma omp parallel for schedule(dynamic, 1024)
+  for (int64_t g = 0; g < G; g++)
+    for (size_t k = 0; k < gout[(size_t)g].size(); k++) gterm[(size_t)go0[(size_t)g] + k] = term_of(gout[(size_t)g][k]);
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "vocab_sort", omp_get_wtime() - t0);
+  // 3. per record: term ids -> tf
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> rid((size_t)nR);
+#pragma omp parallel
+  {
+    std::vector<int32_t> tfc((size_t)V, 0), touched;
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t r = 0; r < nR; r++) {
+      touched.clear();
+      auto count = [&](int32_t id) {
+        if (tfc[(size_t)id]++ == 0) touched.push_back(id);
+      };
+      const std::vector<int32_t> &lm = lmap[(size_t)rthr[(size_t)r]];
+      for (int32_t x : rtok[(size_t)r]) {
+        const int32_t g = lm[(size_t)x];
+        for (int32_t k = go0[(size_t)g]; k < go0[(size_t)g + 1]; k++) count(gterm[(size_t)k]);
+      }
+      for (const u16s &w : rterm[(size_t)r]) count(term_of(w));
+      auto &out = rid[(size_t)r];
+      out.reserve(touched.size());
+      for (int32_t id : touched) {
+        out.emplace_back(id, tfc[(size_t)id]);
+        tfc[(size_t)id] = 0;
+      }
+      std::vector<int32_t>().swap(rtok[(size_t)r]);
+    }
+  }
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "lmap", omp_get_wtime() - t0);
+  // records in docno order (the reducer sorts postings by docno; stable, so equal
+  // docnos keep input order before they merge)
   std::vector<int64_t> order((size_t)nR);
   for (int64_t r = 0; r < nR; r++) order[(size_t)r] = r;
   std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return rdocno[(size_t)a] < rdocno[(size_t)b]; });
-  std::vector<std::vector<std::pair<int32_t, int32_t>>> rid((size_t)nR);  // (term id, tf)
-#pragma omp parallel for schedule(dynamic, 256)
-  for (int64_t r = 0; r < nR; r++) {
-    auto &o = rid[(size_t)r];
-    o.reserve(rterms[(size_t)r].size());
-    for (auto &p : rterms[(size_t)r]) o.emplace_back(tid.at(p.first), p.second);
-    rterms[(size_t)r].clear();
-    rterms[(size_t)r].shrink_to_fit();
-  }
   // counting sort by term: counts, prefix, scatter in docno order
   std::vector<int64_t> cnt((size_t)V + 1, 0);
   for (int64_t r = 0; r < nR; r++)
@@ -245,6 +515,7 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
       }
     }
   }
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "scatter", omp_get_wtime() - t0);
   rid.clear();
   rid.shrink_to_fit();
   // per term: merge equal docnos (sum tf), then stable sort by tf desc
@@ -278,6 +549,7 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
       pd[(size_t)i] = tmp[(size_t)(i - b)].second;
     }
   }
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "reduce", omp_get_wtime() - t0);
   ix->off.assign((size_t)V + 1, 0);
   for (int64_t t = 0; t < V; t++) ix->off[(size_t)t + 1] = ix->off[(size_t)t] + merged[(size_t)t];
   ix->P = ix->off[(size_t)V];
@@ -291,6 +563,7 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
       ix->tf[(size_t)(ix->off[(size_t)t] + i)] = pf[(size_t)(s + i)];
     }
   }
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "finish", omp_get_wtime() - t0);
   ix->build_s = omp_get_wtime() - t0;
   return ix;
 }

@@ -714,20 +714,55 @@ __device__ __forceinline__ uint32_t raw_insert(const RawTable &tb, const TokSig 
 //   4. the raw slots stored coalesced per record.
 // Token i of record r goes to tokstream[(rs[r] >> 1) + i]; ntok[r] is written by
 // the lane holding r's last byte.
-constexpr int kTokNT = 256;
+// Streams read or written once (the text, the token stream, the pairs) bypass
+// the L2 with nontemporal loads / stores (SME_NT = 1), so the hot raw-vocabulary
+// slots and raw_term entries the probes and gathers reuse stay cached.
+#ifndef SME_NT
+#define SME_NT 1
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+#if SME_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#if SME_NT
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+#else
+  const u32x4 v = *reinterpret_cast<const u32x4 *>(p);
+#endif
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <typename T>
+__device__ __forceinline__ void st_stream(T *p, T v) {
+#if SME_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+#ifndef SME_TOKNT
+#define SME_TOKNT 256
+#endif
+constexpr int kTokNT = SME_TOKNT;  // lanes per workgroup (one 64-byte lane slice each)
 constexpr int kTokWords = 4;                      // 16-byte words per lane
 constexpr int kTokBytes = 16 * kTokWords;         // 64 bytes per lane
 constexpr int kChunk = kTokNT * kTokBytes;        // 16 KiB of text per block step
 constexpr int kStageV = kTokNT * kTokWords + 64;  // staged 16-byte words: chunk + 1 KiB lookahead
-constexpr int kRecWin = 384;  // records overlapping one chunk: fast-path records are >= kMinFastRec bytes
-constexpr int kTokCap = 2560;  // chunk tokens per round (a c2 chunk holds ~1950; more take further rounds)
+constexpr int kRecWin = 384 * (kTokNT / 256);  // records overlapping one chunk: fast-path records are >= kMinFastRec bytes
+constexpr int kTokCap = 2560 * (kTokNT / 256);  // chunk tokens per round (a c2 16 KiB chunk holds ~1950; more take further rounds)
+constexpr int kTokMiss = 256;  // deferred raw-vocabulary inserts per round (more: inserted in place)
 #ifndef SME_TOKOCC
-#define SME_TOKOCC 4
+#define SME_TOKOCC (1024 / SME_TOKNT)
 #endif
 #ifndef SME_TOKG
-#define SME_TOKG 8
+#define SME_TOKG 2
 #endif
-constexpr int kTokG = SME_TOKG;  // tokens per lane step in the probe pass (all their slot loads in flight)
+constexpr int kTokG = SME_TOKG;  // tokens per lane step in the probe pass
 #ifndef SME_FASTPROBES
 #define SME_FASTPROBES 4
 #endif
@@ -778,6 +813,8 @@ struct TokLds {
   int32_t sc32[kTokNT / 64 + 1];
   uint32_t cls[256];                  // byte class: bit 0 split byte, bit 16 span starter ('<' or '&')
   uint32_t tl[kTokCap];               // round's chunk tokens by rank: start position, then raw slot
+  int32_t miss[kTokMiss];             // round's tokens whose probe found no slot: inserted together
+  int32_t nmiss;
 };
 
 // byte at chunk-relative position p (stage, or global beyond the lookahead)
@@ -879,37 +916,6 @@ __device__ __forceinline__ void tok_sig_at(const TokLds &L, const uint8_t *t, in
   *len_o = len;
 }
 
-// Words and length of the token at chunk-relative x, without the hash: the probe
-// pass re-derives them from LDS after its slot loads return, so a token in
-// flight holds only its loaded slot words and slot index in registers.  len is
-// 99 for a token longer than 16 bytes (only the byte path knows its length).
-__device__ __forceinline__ void tok_words_at(const TokLds &L, int32_t x, uint64_t *w0, uint64_t *w1, int32_t *len_o) {
-  const int ln = x >> 6, bi = x & 63;
-  const uint64_t rest = L.emask[ln] >> bi >> 1;
-  int32_t len = 99;
-  if (rest) {
-    len = __ffsll((unsigned long long)rest);
-  } else if (ln + 1 < kTokNT) {
-    const uint64_t m = L.emask[ln + 1];
-    if (m) len = 64 - bi + __ffsll((unsigned long long)m) - 1;
-  }
-  if (len <= 16) {
-    const uint32_t *st32 = reinterpret_cast<const uint32_t *>(L.st4);
-    const int a = x >> 2, r = x & 3;
-    const uint32_t d0 = st32[a], d1 = st32[a + 1], d2 = st32[a + 2], d3 = st32[a + 3], d4 = st32[a + 4];
-    const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, r) |
-                        ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32);
-    const uint64_t hi = (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, r) |
-                        ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, r) << 32);
-    *w0 = len >= 8 ? lo : (lo & ((1ull << (8 * len)) - 1ull));
-    *w1 = len <= 8 ? 0ull : (len >= 16 ? hi : (hi & ((1ull << (8 * (len - 8))) - 1ull)));
-  } else {
-    *w0 = 0;
-    *w1 = 0;
-  }
-  *len_o = len;
-}
-
 __device__ __forceinline__ bool slot_hit(const SlotVal &v, const TokSig &g, int32_t len) {
   return len <= 16 && v.key == g.h && v.rep != 0 && (v.rep & 0xFFFFFFull) == (uint64_t)len && v.w0 == g.w0 &&
          v.w1 == g.w1;
@@ -924,6 +930,7 @@ __device__ __forceinline__ bool slot_hit16(const ulonglong2 &v, const TokSig &g,
   return len < 16 && v.x == g.w0 && v.y == g.w1;
 }
 
+// rs_g / re_g: record bounds of the fast records in frec order (rsF[f] = rs[frec[f]])
 __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n,
                                                      const uint64_t *__restrict__ rs_g,
                                                      const uint64_t *__restrict__ re_g,
@@ -940,21 +947,21 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
   const int64_t nq = n + mis;
   const uint8_t *stg = reinterpret_cast<const uint8_t *>(L.st4);
   const int tid = threadIdx.x;
-  L.cls[tid] = (is_split_byte((uint32_t)tid) ? 1u : 0u) | ((tid == '<' || tid == '&') ? 0x10000u : 0u);
-  const int64_t end_all = (int64_t)re_g[frec[f1 - 1]];
+  if (tid < 256) L.cls[tid] = (is_split_byte((uint32_t)tid) ? 1u : 0u) | ((tid == '<' || tid == '&') ? 0x10000u : 0u);
+  const int64_t end_all = (int64_t)re_g[f1 - 1];
   int64_t fcur = f0;        // first fast record not wholly before the current chunk
   int64_t mask_carry = -1;  // absolute end of the furthest span begun in earlier chunks
   int32_t tok_carry = 0;    // tokens of the record continuing from the previous chunk
-  int64_t Q = ((int64_t)rs_g[frec[f0]] + mis) & ~(int64_t)15;
+  int64_t Q = ((int64_t)rs_g[f0] + mis) & ~(int64_t)15;
   uint8_t prev_chunk_byte = Q - mis > 0 ? t[Q - mis - 1] : (uint8_t)' ';
   for (; Q < end_all + mis; Q += kChunk) {
     const int64_t c_lo = Q - mis;  // chunk = positions c_lo + [0, kChunk)
     for (int i = tid; i < kRecWin; i += kTokNT) {
       const int64_t f = fcur + i;
       const int32_t r = f < f1 ? frec[f] : -1;
-      const int64_t a = r >= 0 ? (int64_t)rs_g[r] : INT64_MAX;
+      const int64_t a = r >= 0 ? (int64_t)rs_g[f] : INT64_MAX;  // (independent loads: no frec -> rs chain)
       const bool ok = a < c_lo + kChunk;
-      const int64_t b = ok ? (int64_t)re_g[r] : INT64_MAX;
+      const int64_t b = ok ? (int64_t)re_g[f] : INT64_MAX;
       L.rs[i] = ok ? (int32_t)max<int64_t>(a - c_lo, -1) : kFar;
       L.re[i] = ok ? (int32_t)min<int64_t>(b - c_lo, kFar) : kFar;
       if (i == 0) L.tbase0 = ok ? (a >> 1) : 0;
@@ -963,7 +970,7 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
     }
     for (int i = tid; i < kStageV; i += kTokNT) {
       const int64_t q = Q + 16 * (int64_t)i;
-      L.st4[i] = q < nq ? a4[q >> 4] : make_uint4(0, 0, 0, 0);
+      L.st4[i] = q < nq ? ld_stream(a4 + (q >> 4)) : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
     const int32_t p0 = kTokBytes * tid;
@@ -1098,6 +1105,7 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
     for (int32_t rlo = 0; rlo < blk_cnt; rlo += kTokCap) {
       const int32_t nr = min(kTokCap, blk_cnt - rlo);
       // pass 2: start positions of the round's tokens by chunk rank
+      if (tid == 0) L.nmiss = 0;
       {
         uint64_t keep = keep_all;
         int32_t idx = base - rlo;
@@ -1111,69 +1119,67 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
         }
       }
       __syncthreads();
-      // pass 3: raw-vocabulary slot of every token.  A lane holds up to kTokG
-      // tokens (a c2 chunk's ~1950 tokens are one step of 256 lanes) and all
-      // their home-slot loads are in flight together; the loaded words and the
-      // slot index are all a token keeps in registers (its words and length are
-      // re-read from LDS to compare).  Tokens whose home slot holds another
-      // token advance together, one slot per round, with plain loads (a slot,
-      // once filled, never changes); an empty-looking slot, a token of >= 16
-      // bytes or a long probe run take raw_insert.
+      // pass 3: signature + raw-vocabulary slot, kTokG tokens per lane step (their
+      // home-slot loads in flight together)
       for (int32_t r0 = (texp & 1) ? nr : tid; r0 < nr; r0 += kTokG * kTokNT) {
+        TokSig g[kTokG];
+        int32_t len[kTokG], x[kTokG];
         ulonglong2 v[kTokG];
-        uint32_t sl[kTokG];
-        uint32_t live = 0, ins = 0;  // bit u: token u still probing / to raw_insert
+#pragma unroll
+        for (int u = 0; u < kTokG; u++) {
+          const int32_t r = r0 + u * kTokNT;
+          x[u] = (int32_t)L.tl[r < nr ? r : r0];
+          tok_sig_at(L, t, c_lo, x[u], &g[u], &len[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kTokG; u++)
+          v[u] = *reinterpret_cast<const ulonglong2 *>(&tb.slots[g[u].h & tb.mask].w0);
 #pragma unroll
         for (int u = 0; u < kTokG; u++) {
           const int32_t r = r0 + u * kTokNT;
           if (r < nr) {
-            uint64_t w0, w1;
-            int32_t len;
-            tok_words_at(L, (int32_t)L.tl[r], &w0, &w1, &len);  // no calls while loads are in flight
-            if (len < 16) {
-              sl[u] = (uint32_t)(sig_head(w0, w1) & tb.mask);
-              v[u] = *reinterpret_cast<const ulonglong2 *>(&tb.slots[sl[u]].w0);
-              live |= 1u << u;
+            // linear probing over occupied slots of other tokens with plain
+            // loads (a slot, once filled, never changes); an empty-looking slot,
+            // a token of >= 16 bytes or a long probe run take raw_insert
+            uint64_t sl = g[u].h & tb.mask;
+            bool hit = slot_hit16(v[u], g[u], len[u]);
+            if (!hit && len[u] < 16 && v[u].x != 0 && !(texp & 8)) {
+              for (int pr = 1; pr < kFastProbes; pr++) {
+                const uint64_t s2 = (sl + pr) & tb.mask;
+                const ulonglong2 w = *reinterpret_cast<const ulonglong2 *>(&tb.slots[s2].w0);
+                if (slot_hit16(w, g[u], len[u])) {
+                  hit = true;
+                  sl = s2;
+                  break;
+                }
+                if (w.x == 0) break;
+              }
+            }
+            if (hit || (texp & 12)) {  // (timing experiments 4 / 8: no insert / no probe walk)
+              L.tl[r] = (uint32_t)sl;
             } else {
-              ins |= 1u << u;
+              // a new raw token (or a long / contended probe): inserted after the
+              // probe pass, with the round's other inserts, so a wave waits on one
+              // insert chain rather than on one per lane step
+              const int k = atomicAdd(&L.nmiss, 1);
+              if (k < kTokMiss)
+                L.miss[k] = r;
+              else
+                L.tl[r] = raw_insert(tb, g[u], (uint64_t)(c_lo + x[u]), (uint64_t)len[u], SlotVal{0, 0, 0, 0});
             }
           }
         }
-        for (int pr = 0; pr < kFastProbes && live; pr++) {
-          if (pr > 0) {
-#pragma unroll
-            for (int u = 0; u < kTokG; u++)
-              if (live >> u & 1u) {
-                sl[u] = (uint32_t)((sl[u] + 1) & tb.mask);
-                v[u] = *reinterpret_cast<const ulonglong2 *>(&tb.slots[sl[u]].w0);
-              }
-          }
-#pragma unroll
-          for (int u = 0; u < kTokG; u++)
-            if (live >> u & 1u) {
-              const int32_t r = r0 + u * kTokNT;
-              uint64_t w0, w1;
-              int32_t len;
-              tok_words_at(L, (int32_t)L.tl[r], &w0, &w1, &len);
-              if (v[u].x == w0 && v[u].y == w1) {
-                L.tl[r] = sl[u];
-                live &= ~(1u << u);
-              } else if (v[u].x == 0) {
-                live &= ~(1u << u);
-                ins |= 1u << u;
-              }
-            }
-        }
-        ins |= live;
-        for (int u = 0; u < kTokG; u++)
-          if (ins >> u & 1u) {
-            const int32_t r = r0 + u * kTokNT;
-            const int32_t x = (int32_t)L.tl[r];
-            TokSig g;
-            int32_t len;
-            tok_sig_at(L, t, c_lo, x, &g, &len);
-            L.tl[r] = raw_insert(tb, g, (uint64_t)(c_lo + x), (uint64_t)len, SlotVal{0, 0, 0, 0});
-          }
+      }
+      __syncthreads();
+      // pass 3b: the deferred inserts (the noinline raw_insert re-reads the home
+      // slot coherently; concurrent inserts of one token resolve there)
+      for (int i = tid; i < min(L.nmiss, kTokMiss); i += kTokNT) {
+        const int32_t r = L.miss[i];
+        const int32_t x = (int32_t)L.tl[r];
+        TokSig g;
+        int32_t len;
+        tok_sig_at(L, t, c_lo, x, &g, &len);
+        L.tl[r] = raw_insert(tb, g, (uint64_t)(c_lo + x), (uint64_t)len, SlotVal{0, 0, 0, 0});
       }
       __syncthreads();
       // pass 4: coalesced stores: chunk token i belongs to the last window record
@@ -1195,7 +1201,7 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
           while (k + 1 < nk && fr(k + 1) <= i) k++;
           const int32_t r0k = k == 0 ? L.c0[0] - carry0 : L.c0[k];
           const int64_t tbse = k == 0 ? L.tbase0 : ((c_lo + L.rs[k]) >> 1);
-          tokstream[tbse + (i - r0k)] = L.tl[i - rlo];
+          st_stream(tokstream + tbse + (i - r0k), L.tl[i - rlo]);
         }
       }
       if (rlo + kTokCap < blk_cnt) __syncthreads();  // the next round rewrites tl
@@ -1204,6 +1210,15 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
                       // the next chunk's staging barrier)
     fcur += s_adv;
     tok_carry = L.sc32[0];
+  }
+}
+
+__global__ void k_gather_bounds(const int32_t *frec, int64_t nF, const uint64_t *rs, const uint64_t *re, uint64_t *rsF,
+                                uint64_t *reF) {
+  for (int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; f < nF; f += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t r = frec[f];
+    rsF[f] = rs[r];
+    reF[f] = re[r];
   }
 }
 
@@ -1820,7 +1835,7 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
       uint32_t slot[kAggU];
       int32_t rt[kAggU];
 #pragma unroll
-      for (int u = 0; u < kAggU; u++) slot[u] = t0 + u * 64 < nt ? ts[t0 + u * 64] : 0u;
+      for (int u = 0; u < kAggU; u++) slot[u] = t0 + u * 64 < nt ? ld_stream(ts + t0 + u * 64) : 0u;
 #pragma unroll
       for (int u = 0; u < kAggU; u++) rt[u] = t0 + u * 64 < nt ? in.raw_term[slot[u]] : -1;
 #pragma unroll
@@ -1859,9 +1874,9 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
       if (key >= 0) {
         const int64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
         const int32_t c = cnt[k + lane];
-        p_term[o] = (uint32_t)key;
+        st_stream(p_term + o, (uint32_t)key);
         if (in.v32)
-          in.v32[o] = (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c);
+          st_stream(in.v32 + o, (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c));
         else
           p_val[o] = dn | (uint32_t)c;
         if (fused) wmax = max(wmax, (uint32_t)c);
@@ -2884,6 +2899,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
     if (nR > 0) {
       if (nF > 0) {
+        uint64_t *rsF = W[W_LT].as<uint64_t>(2 * (size_t)nF), *reF = rsF + nF;  // '<' list no longer needed
+        hipLaunchKernelGGL(k_gather_bounds, dim3(grid_for(nF)), dim3(256), 0, st, frec, nF, rs, re, rsF, reF);
         // events bracket exactly this launch: "tok_kernel" is the dominant kernel's
         // duration that bench.py reports against the HBM roofline
         prof.mark("tok_setup");
@@ -2892,11 +2909,12 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
         int tokexp = 0;
 #ifdef SME_EXPERIMENTS
         // SME_TOKEXP (timing experiments, experiment builds only; wrong results):
-        // 1 no signatures / probes, 2 no token stores
+        // 1 no signatures / probes, 2 no token stores, 4 no raw_insert (a miss
+        // takes its home slot), 8 home slot only (no probe walk, no insert)
         if (const char *tx = getenv("SME_TOKEXP")) tokexp = atoi(tx);
 #endif
-        hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)((nF + rpb - 1) / rpb)), dim3(kTokNT), 0, st, t, (int64_t)n, rs,
-                           re, frec, nF, rpb, tok, ntok, tb, tokexp);
+        hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)((nF + rpb - 1) / rpb)), dim3(kTokNT), 0, st, t, (int64_t)n, rsF,
+                           reF, frec, nF, rpb, tok, ntok, tb, tokexp);
         SME_CHECK_LAUNCH();
         prof.mark("tok_kernel");
       }

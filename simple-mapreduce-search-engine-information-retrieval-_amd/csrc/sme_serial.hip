@@ -84,6 +84,61 @@ __global__ void k_ser_offsets(const uint32_t *grp_term, const int64_t *scan, int
   }
 }
 
+constexpr int64_t kSerBigDf = 8192;             // larger terms: posting stream in tiles (k_ser_big)
+constexpr int64_t kSerTileBytes = 64 * 1024;    // stream bytes per tile
+
+// Stream bytes [b0, b1) of a posting list's big-endian (docno, tf) words, at
+// post + b0, written as aligned dwords: output dword at stream byte b = 4 f + s
+// is v_alignbyte of the stream words f + 1 and f (each byte-swapped, so a
+// little-endian store lays its bytes out big-endian); the unaligned head and
+// tail bytes singly (byte stores of every posting cost 22 ms on c2).  Tiles of
+// one stream meet on byte boundaries, so no byte is written twice.
+__device__ __forceinline__ void ser_posts(uint8_t *post, const int32_t *dn, const int32_t *tf, int64_t b0, int64_t b1,
+                                          int lane) {
+  auto word = [&](int64_t f) -> uint32_t {
+    const uint32_t v = (f & 1) ? (uint32_t)tf[f >> 1] : (uint32_t)dn[f >> 1];
+    return __builtin_bswap32(v);
+  };
+  const int a = (int)((uintptr_t)(post + b0) & 3);
+  const int64_t h = min((int64_t)((4 - a) & 3), b1 - b0);  // head bytes before the first aligned address
+  if (lane < h) {
+    const int64_t b = b0 + lane;
+    post[b] = (uint8_t)(word(b >> 2) >> (8 * (b & 3)));
+  }
+  const int64_t s = b0 + h, nd = (b1 - s) >> 2;  // whole aligned dwords
+  uint32_t *dst = reinterpret_cast<uint32_t *>(post + s);
+  for (int64_t k = lane; k < nd; k += 64) {
+    const int64_t b = s + 4 * k, f = b >> 2;
+    const int sft = (int)(b & 3);
+    dst[k] = sft == 0 ? word(f) : __builtin_amdgcn_alignbyte(word(f + 1), word(f), sft);
+  }
+  const int64_t t0 = s + 4 * nd;  // tail bytes
+  if (lane < b1 - t0) {
+    const int64_t b = t0 + lane;
+    post[b] = (uint8_t)(word(b >> 2) >> (8 * (b & 3)));
+  }
+}
+
+// big terms (df > kSerBigDf): tile counts and the byte offset of the posting
+// stream inside the record
+__global__ void k_ser_bigflags(const int64_t *off, int64_t V, uint8_t *f) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x)
+    f[t] = off[t + 1] - off[t] > kSerBigDf;
+}
+__global__ void k_ser_bigtiles(const int32_t *big, int64_t nbig, const int64_t *off, const int64_t *toff,
+                               const uint16_t *tch, const int32_t *gram, int K, int64_t *ntile, int64_t *post_rel) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < nbig; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = big[j], df = off[t + 1] - off[t];
+    ntile[j] = (8 * df + kSerTileBytes - 1) / kSerTileBytes;
+    int64_t ul = 0;
+    for (int c = 0; c < K; c++) {
+      const int64_t e = comp_of(gram, K, t, c);
+      for (int64_t i = toff[e]; i < toff[e + 1]; i++) ul += mutf8_unit_len(tch[i]);
+    }
+    post_rel[j] = 8 + (4 + 2 * (int64_t)K + ul + 4) + 4 + 2 + kClassLen;
+  }
+}
+
 // one wave per index term
 __global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int32_t *gram, int K, const int64_t *off,
                             const int32_t *docno_o, const int32_t *tf_o, int64_t V, const int64_t *rec_off,
@@ -169,33 +224,31 @@ __global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int3
         for (int i = 0; i < kClassLen; i++) q[10 + i] = (uint8_t)"sa.edu.kaust.io.PostingWritable"[i];
       }
     }
-    // postings: the stream of big-endian (docno, tf) words written as aligned
-    // dwords -- output dword at stream byte b = 4 f + s is v_alignbyte of the
-    // stream words f + 1 and f (each word byte-swapped so that a little-endian
-    // store lays its bytes out big-endian); the unaligned head and tail bytes
-    // singly.  (Byte stores of every posting cost 22 ms on c2.)
-    if (df > 0) {
-      const int64_t nb = 8 * df;
-      const int a = (int)((uintptr_t)post & 3);
-      const int h = (4 - a) & 3;  // head bytes before the first aligned address
-      auto word = [&](int64_t f) -> uint32_t {
-        const uint32_t v = (f & 1) ? (uint32_t)tf_o[p0 + (f >> 1)] : (uint32_t)docno_o[p0 + (f >> 1)];
-        return __builtin_bswap32(v);
-      };
-      if (lane < h && lane < nb) post[lane] = (uint8_t)(word(0) >> (8 * lane));
-      const int64_t nd = (nb - h) >> 2;  // whole aligned dwords
-      uint32_t *dst = reinterpret_cast<uint32_t *>(post + h);
-      for (int64_t k = lane; k < nd; k += 64) {
-        const int64_t b = h + 4 * k, f = b >> 2;
-        const int sft = (int)(b & 3);
-        dst[k] = sft == 0 ? word(f) : __builtin_amdgcn_alignbyte(word(f + 1), word(f), sft);
-      }
-      const int64_t t0 = h + 4 * nd;  // tail bytes
-      if (lane < nb - t0) {
-        const int64_t b = t0 + lane;
-        post[b] = (uint8_t)(word(b >> 2) >> (8 * (b & 3)));
-      }
+    // postings: this wave writes those of small terms; a large term's stream is
+    // cut into tiles written by many waves (k_ser_big), so one wave does not
+    // write a 1 M-posting list alone (that tail cost c2 most of the pass)
+    if (df > 0 && df <= kSerBigDf) ser_posts(post, docno_o + p0, tf_o + p0, 0, 8 * df, lane);
+  }
+}
+
+// tiles of the large terms' posting streams: tile i of big term j covers stream
+// bytes [i, i + 1) x kSerTileBytes (clamped); tile_off = exclusive scan of the
+// terms' tile counts
+__global__ void k_ser_big(const int32_t *big, int64_t nbig, const int64_t *tile_off, const int64_t *off,
+                          const int32_t *docno_o, const int32_t *tf_o, const int64_t *rec_off,
+                          const int64_t *post_rel, uint8_t *out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wpb = blockDim.x / 64, ntiles = tile_off[nbig];
+  for (int64_t x = blockIdx.x * wpb + (threadIdx.x >> 6); x < ntiles; x += (int64_t)gridDim.x * wpb) {
+    int64_t lo = 0, hi = nbig;  // last j with tile_off[j] <= x
+    while (hi - lo > 1) {
+      const int64_t m = (lo + hi) >> 1;
+      if (tile_off[m] <= x) lo = m;
+      else hi = m;
     }
+    const int64_t t = big[lo], p0 = off[t], nb = 8 * (off[t + 1] - p0);
+    const int64_t b0 = (x - tile_off[lo]) * kSerTileBytes, b1 = min(nb, b0 + kSerTileBytes);
+    ser_posts(out + rec_off[t] + post_rel[lo], docno_o + p0, tf_o + p0, b0, b1, lane);
   }
 }
 
@@ -285,6 +338,27 @@ void serialize_index(sme_index *ix, hipStream_t st) {
                        (const int64_t *)ix->d_off.p, (const int32_t *)ix->d_docno_o.p, (const int32_t *)ix->d_tf_o.p,
                        V, rec_off, out);
     SME_CHECK_LAUNCH();
+    // the large terms' posting streams, in tiles
+    uint8_t *bflag = W[24].as<uint8_t>(V + 1);
+    int32_t *big = W[25].as<int32_t>(V + 1), *d_nbig = W[30].as<int32_t>(4);
+    hipLaunchKernelGGL(k_ser_bigflags, dim3(G), dim3(256), 0, st, (const int64_t *)ix->d_off.p, V, bflag);
+    select_flagged(bflag, V, big, d_nbig, W[29], W[23], st);
+    int32_t nbig = 0;
+    SME_HIP(hipMemcpyAsync(&nbig, d_nbig, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    if (nbig > 0) {
+      int64_t *ntile = W[26].as<int64_t>(nbig + 1), *tile_off = W[27].as<int64_t>(nbig + 1);
+      int64_t *post_rel = W[28].as<int64_t>(nbig + 1);
+      hipLaunchKernelGGL(k_ser_bigtiles, dim3((unsigned)std::min<int64_t>((nbig + 255) / 256, 4096)), dim3(256), 0, st,
+                         big, (int64_t)nbig, (const int64_t *)ix->d_off.p, (const int64_t *)ix->d_term_off.p,
+                         (const uint16_t *)ix->d_term_chars.p, gram, ix->K, ntile, post_rel);
+      SME_HIP(hipMemsetAsync(ntile + nbig, 0, sizeof(int64_t), st));
+      excl_scan<int64_t>(ntile, tile_off, nbig + 1, W[23], st);
+      hipLaunchKernelGGL(k_ser_big, dim3(8192), dim3(256), 0, st, big, (int64_t)nbig, tile_off,
+                         (const int64_t *)ix->d_off.p, (const int32_t *)ix->d_docno_o.p, (const int32_t *)ix->d_tf_o.p,
+                         rec_off, post_rel, out);
+      SME_CHECK_LAUNCH();
+    }
   }
   if (N > 0) {
     hipLaunchKernelGGL(k_ser_space, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 8192)), dim3(256), 0, st,

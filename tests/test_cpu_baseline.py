@@ -38,11 +38,23 @@ def test_cpuopt_synthetic(threads):
     _check(synth.gen_corpus(n, V=3000, seed=11, len_lo=20, len_hi=120), synth.docids(n), threads)
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_cpuopt_fuzz(seed):
+@pytest.mark.parametrize("seed,hard", [(1, True), (2, True), (3, True), (4, False), (5, False), (6, False)])
+def test_cpuopt_fuzz(seed, hard):
+    """Markup, entities, non-ASCII and quirk records: the byte-level fast path on
+    the records of simple markup, the oracle's TagTokenizer on the rest."""
     import common
-    corpus, ids = common.fuzz_corpus(seed, 120)
+    corpus, ids = common.fuzz_corpus(seed, 150, hard=hard)
     _check(corpus, ids, 4)
+
+
+def test_cpuopt_kat_and_invalid_utf8():
+    import json
+    import os
+    kat = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kat_appendix_b.json")))
+    _check(kat["index_corpus"].encode(), kat["index_mapping"], 2)
+    bad = b"".join(b"<DOC><DOCNO>D%d</DOCNO> caf\xc3 \xe9t\xc3\xa9 \xff\xfe ok&amp;go x\xe2\x82 y <b>z</b> AT&T"
+                   b" U.S.A. don't</DOC>\n" % i for i in range(40))
+    _check(bad, sorted("D%d" % i for i in range(40)), 2)
 
 
 def test_cpuopt_from_csr_matches_built_index():
