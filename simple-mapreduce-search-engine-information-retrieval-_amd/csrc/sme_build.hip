@@ -1604,6 +1604,67 @@ __global__ void k_final_fixup(uint32_t *order, int64_t V, const uint32_t *vslot,
   }
 }
 
+// ASCII vocabularies: the code units in use (128-bit presence map), so a sort
+// key packs ceil(log2(units + 1)) bits per unit (6 for letters and digits: 10
+// units per 64-bit word instead of 9 x 7 bits)
+__global__ void k_unit_presence(int64_t V, const uint64_t *vcs, const uint16_t *pool, unsigned int *pres) {
+  __shared__ unsigned int sp[4];
+  if (threadIdx.x < 4) sp[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned int m[4] = {0, 0, 0, 0};
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t cs = vcs[i];
+    const uint16_t *u = pool + (cs >> 16);
+    const int l = (int)(cs & 0xFFFF);
+    for (int j = 0; j < l; j++) m[(u[j] >> 5) & 3] |= 1u << (u[j] & 31);
+  }
+  for (int k = 0; k < 4; k++)
+    if (m[k]) atomicOr(&sp[k], m[k]);
+  __syncthreads();
+  if (threadIdx.x < 4 && sp[threadIdx.x]) atomicOr(&pres[threadIdx.x], sp[threadIdx.x]);
+}
+// key of term order[i]: its first cpw units as codes (code[u] = rank of u among
+// the units in use + 1; 0 pads), most significant first -- String.compareTo
+// order of the first cpw units
+__global__ void k_term_code(const uint32_t *order, int64_t V, const uint64_t *vcs, const uint16_t *pool,
+                            const uint8_t *code, int cpw, int ub, uint64_t *key) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t cs = vcs[order[i]];
+    const uint16_t *u = pool + (cs >> 16);
+    const int l = (int)(cs & 0xFFFF);
+    uint64_t k = 0;
+    for (int j = 0; j < cpw; j++) k = (k << ub) | (j < l ? code[u[j] & 127] : 0u);
+    key[i] = k;
+  }
+}
+// runs of equal keys (terms sharing their first cpw units): longest run
+__global__ void k_key_runs(const uint64_t *key, int64_t V, unsigned int *maxrun) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i > 0 && key[i] == key[i - 1]) continue;
+    int64_t j = i + 1;
+    while (j < V && key[j] == key[i] && j - i < 4096) j++;
+    if (j - i > 1) atomicMax(maxrun, (unsigned int)(j - i));
+  }
+}
+// order each run of equal keys by the whole string (insertion sort: runs are short)
+__global__ void k_key_fixup(const uint64_t *key, int64_t V, uint32_t *order, const uint64_t *vcs,
+                            const uint16_t *pool) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
+    if ((i > 0 && key[i] == key[i - 1]) || i + 1 >= V || key[i + 1] != key[i]) continue;
+    int64_t j = i + 1;
+    while (j < V && key[j] == key[i]) j++;
+    for (int64_t a = i + 1; a < j; a++) {
+      const uint32_t v = order[a];
+      int64_t b = a - 1;
+      while (b >= i && cmp_pool(pool, vcs[order[b]], vcs[v]) > 0) {
+        order[b + 1] = order[b];
+        b--;
+      }
+      order[b + 1] = v;
+    }
+  }
+}
+
 // rank of every final slot; term lengths in rank order
 __global__ void k_final_rank(const uint32_t *order, int64_t V, const uint32_t *vslot, const uint64_t *vcs,
                              int32_t *rank_of_slot, int64_t *term_len) {
@@ -2117,6 +2178,15 @@ __global__ void k_docno_keys(const int32_t *docno, int64_t nR, uint32_t *k, uint
 __global__ void k_widen_u32(const uint32_t *a, int64_t n, int64_t *b) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     b[i] = (int64_t)a[i];
+}
+__global__ void k_not_ascending(const int32_t *d, int64_t n, unsigned long long *cnt) {
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bad |= d[i] <= d[i - 1];
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(cnt, 1ull);
+}
+__global__ void k_iota_i64(int64_t *a, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) a[i] = i;
 }
 __global__ void k_adjacent_equal(const uint32_t *k, int64_t n, unsigned long long *cnt) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -2825,6 +2895,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   auto cub_tmp = [&](size_t bytes) { return cx->cub_tmp.get(bytes); };
   unsigned long long *cnt = W[W_CNT].as<unsigned long long>(32);  // [20] max tf, [22..23] docno range
 
+  uint8_t early_code[128];  // vocabulary sort: unit -> code (host copy outlives its async upload)
   const RecordSpans rsp = find_records(cx, t, n, st, &prof);
   uint64_t *rs = rsp.rs, *re = rsp.re, *C = rsp.C;
   const int64_t nR = rsp.nR, nC = rsp.nC;
@@ -2855,7 +2926,17 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   // records in docno order (stable) -> perm; duplicate docnos?
   int64_t *perm = W[W_PERM].as<int64_t>(nR + 1);
   bool dup_docno = false;
+  // records already in strictly ascending docno order (a corpus in docid order,
+  // as TREC collections and every synthetic corpus are): perm = identity, no
+  // duplicates, no sort
+  bool ascending = false;
   if (nR > 0) {
+    SME_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_not_ascending, dim3(grid_for(nR)), dim3(256), 0, st, docno, nR, cnt);
+    ascending = d2h(cnt, st) == 0;
+    if (ascending) hipLaunchKernelGGL(k_iota_i64, dim3(grid_for(nR)), dim3(256), 0, st, perm, nR);
+  }
+  if (nR > 0 && !ascending) {
     uint32_t *k0 = W[W_T0].as<uint32_t>(nR), *k1 = W[W_T1].as<uint32_t>(nR);
     uint32_t *v0 = W[W_T2].as<uint32_t>(nR), *v1 = W[W_T3].as<uint32_t>(nR);
     hipLaunchKernelGGL(k_docno_keys, dim3(grid_for(nR)), dim3(256), 0, st, docno, nR, k0, v0);
@@ -3068,12 +3149,50 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     uint64_t *kw = W[W_KHI].as<uint64_t>(V), *kw2 = W[W_KLO].as<uint64_t>(V);
     uint32_t *ord_a = vidx, *ord_b = order;
     uint32_t *rscr = W[W_RADIX].as<uint32_t>(kv_sort_scratch(V) / sizeof(uint32_t) + 1);
-    size_t tbb = 0;
-    for (int w = nwords - 1; w >= 0; w--) {
+    bool done = false;
+    if (!term_wide && nwords > 1) {
+      // ONE key word of the first cpw2 units, in ceil(log2(alphabet + 1)) bits each,
+      // then the short runs of terms sharing those units ordered by the whole
+      // string (c2: 6 radix passes instead of 12); runs over 64 terms: the full
+      // word-by-word sort below
+      unsigned int *pres = reinterpret_cast<unsigned int *>(cnt + 28);
+      SME_HIP(hipMemsetAsync(pres, 0, 4 * sizeof(unsigned int), st));
+      hipLaunchKernelGGL(k_unit_presence, dim3(grid_for(V, 256, 2048)), dim3(256), 0, st, V, vcs, co.pool, pres);
+      unsigned int hp[4];
+      SME_HIP(hipMemcpyAsync(hp, pres, sizeof hp, hipMemcpyDeviceToHost, st));
+      SME_HIP(hipStreamSynchronize(st));
+      uint8_t *code_h = early_code;
+      int nsym = 0;
+      for (int u = 0; u < 128; u++) code_h[u] = (hp[u >> 5] >> (u & 31)) & 1u ? (uint8_t)++nsym : (uint8_t)0;
+      const int ub2 = bits_for((uint64_t)nsym), cpw2 = 64 / ub2;
+      if (cpw2 > cpw) {
+        uint8_t *code = reinterpret_cast<uint8_t *>(W[W_SEGB].as<uint64_t>(16));
+        SME_HIP(hipMemcpyAsync(code, code_h, 128, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_term_code, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V, vcs, co.pool, code, cpw2, ub2,
+                           kw);
+        uint32_t *so = kv_sort<uint64_t>(kw, ord_a, kw2, ord_b, V, cpw2 * ub2, rscr, st, true);
+        const uint64_t *sk = so == ord_a ? kw : kw2;
+        unsigned int mr = 0;
+        if (term_maxlen > cpw2) {
+          unsigned int *d_mr = pres;
+          SME_HIP(hipMemsetAsync(d_mr, 0, sizeof(unsigned int), st));
+          hipLaunchKernelGGL(k_key_runs, dim3(grid_for(V)), dim3(256), 0, st, sk, V, d_mr);
+          mr = d2h(d_mr, st);
+        }
+        if (mr <= 64) {
+          if (mr > 1) hipLaunchKernelGGL(k_key_fixup, dim3(grid_for(V)), dim3(256), 0, st, sk, V, so, vcs, co.pool);
+          if (so != order) SME_HIP(hipMemcpyAsync(order, so, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+          done = true;
+        } else {
+          hipLaunchKernelGGL(k_iota_u32, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V);  // start over
+        }
+      }
+    }
+    for (int w = nwords - 1; w >= 0 && !done; w--) {
       hipLaunchKernelGGL(k_term_word, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V, vcs, co.pool, w, cpw, ub, kw);
       if (kv_sort<uint64_t>(kw, ord_a, kw2, ord_b, V, kbits, rscr, st) != ord_a) std::swap(ord_a, ord_b);
     }
-    if (ord_a != order)
+    if (!done && ord_a != order)
       SME_HIP(hipMemcpyAsync(order, ord_a, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     if (term_maxlen > 32)
       hipLaunchKernelGGL(k_final_fixup, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, freps, co.cand_str,
@@ -3396,6 +3515,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   }
   int32_t *docno_d = nullptr, *tf_d = nullptr;
   int64_t *off = nullptr;
+  std::vector<double> early_lut;  // the fused weight pass's LUT (outlives its async upload)
+  bool weights_fused = false;
   if (packed) {
     uint32_t *v32 = ai.v32;
     if (v32 == nullptr) {
@@ -3408,8 +3529,19 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     // hand-written stable LSD radix sort by term id (sme_sort.hip); the last
     // pass unpacks (docno, tf) into the CSR arrays
     uint32_t *rscr = W[W_RADIX].as<uint32_t>(term_sort_scratch(P) / sizeof(uint32_t) + 1);
+    // reference idf mode: one idf for every term (stored df 1, T1/T2), so the last
+    // pass writes the TF-IDF weights too (no separate weight pass over tf)
+    double *wf = nullptr;
+    if (ix->idf_mode == SME_IDF_REFERENCE && P > 0) {
+      early_lut.assign((size_t)max_tf + 1, 0.0);
+      for (int i = 1; i <= max_tf; i++) early_lut[(size_t)i] = 1.0 + log((double)i);
+      SME_HIP(hipMemcpyAsync(ix->d_lut.as<double>(max_tf + 1), early_lut.data(), early_lut.size() * sizeof(double),
+                             hipMemcpyHostToDevice, st));
+      wf = ix->d_w.as<double>(P + 1);
+      weights_fused = true;
+    }
     key_s = term_sort(p_term, v32, key_s, v32s, sort_nrec, sort_reg, sort_xoff, P, tbits, dmin, F, docno_d, tf_d, rscr,
-                      st);
+                      st, wf ? (const double *)ix->d_lut.p : nullptr, log10((double)(std::max<int64_t>(nR, 0) / 1)), wf);
     off = ix->d_off.as<int64_t>(Vi + 1);
     SME_HIP(hipMemsetAsync(off, 0, (Vi + 1) * sizeof(int64_t), st));
     hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, Vi);
@@ -3478,7 +3610,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       hipLaunchKernelGGL(k_term_idf, dim3(grid_for(Vi)), dim3(256), 0, st, off, Vi, idf_ref, Nn, nullptr, d_bydf, sdf,
                          d_byq, ix->idf_mode, idf);
     double *w = ix->d_w.as<double>(PP + 1);
-    if (PP > 0)
+    if (PP > 0 && !weights_fused)
       hipLaunchKernelGGL(k_weights, dim3(grid_for(PP)), dim3(256), 0, st, key_s, tf_d, PP, d_lut, idf_ref, off, Nn,
                          d_bydf, sdf, d_byq, ix->idf_mode, w);
     SME_CHECK_LAUNCH();

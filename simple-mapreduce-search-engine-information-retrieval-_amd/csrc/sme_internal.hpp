@@ -180,7 +180,8 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
 // holding it -- the single-pass aggregation's layout)
 uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t nrec, const int64_t *reg,
                     const int64_t *xoff, int64_t P, int bits, int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf,
-                    uint32_t *counts, hipStream_t st);
+                    uint32_t *counts, hipStream_t st, const double *lut = nullptr, double idf = 0.0,
+                    double *w = nullptr);
 size_t term_sort_scratch(int64_t P);
 // stable LSD radix sort of (key, u32 value) pairs by the key's low `bits` bits
 // (sme_sort.hip; K = uint32_t or uint64_t); ping-pongs between (k0, v0) and

@@ -244,7 +244,8 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
                                                       const uint32_t *__restrict__ offs, uint32_t *__restrict__ okey,
                                                       uint32_t *__restrict__ oval, int32_t *__restrict__ odocno,
                                                       int32_t *__restrict__ otf, int64_t dmin, uint32_t F,
-                                                      Gather g) {
+                                                      Gather g, const double *__restrict__ lut, double idf,
+                                                      double *__restrict__ ow) {
   // wc: per-wave running digit counts, then each (wave, digit)'s first slot in
   // the tile sorted by digit; gd: global offset - tile slot of each digit
   __shared__ uint16_t wc[kRsWaves * kRsMaxBins];
@@ -385,6 +386,9 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
       if (LAST) {
         odocno[dst[j]] = (int32_t)((int64_t)(vv / F) + dmin);
         otf[dst[j]] = (int32_t)(vv % F);
+        // the TF-IDF weight pass fused in for one idf for every term (reference
+        // mode, T1/T2): w = (1 + ln tf) * log10(N / 1), fp64, no contraction
+        if (ow) ow[dst[j]] = __dmul_rn(lut[vv % F], idf);
       } else {
         oval[dst[j]] = vv;
       }
@@ -655,7 +659,7 @@ __global__ void k_select_scatter(const uint8_t *__restrict__ f, const int64_t *_
 // tf.  counts: ceil(P / 16384) * 2048 + 2048 * 256 u32 of scratch.
 uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t nrec, const int64_t *reg,
                     const int64_t *xoff, int64_t P, int bits, int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf,
-                    uint32_t *counts, hipStream_t st) {
+                    uint32_t *counts, hipStream_t st, const double *lut, double idf, double *w) {
   if (P <= 0) return k0;
   if (P > 0xFFFFFFFFll) throw Error(SME_ELIMIT, "term sort of more than 2^32 pairs");
   bits = std::max(bits, 1);
@@ -686,10 +690,10 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
     const unsigned sgrid = (unsigned)(8 * ((ntiles + 7) / 8));  // see the XCD tile order in k_rs_scatter
     if (last)
       hipLaunchKernelGGL(k_rs_scatter<true>, dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, P, shift, nb, counts,
-                         k1, nullptr, docno, tf, dmin, F, g);
+                         k1, nullptr, docno, tf, dmin, F, g, lut, idf, w);
     else
       hipLaunchKernelGGL(k_rs_scatter<false>, dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, P, shift, nb,
-                         counts, k1, v1, nullptr, nullptr, dmin, F, g);
+                         counts, k1, v1, nullptr, nullptr, dmin, F, g, nullptr, 0.0, nullptr);
     SME_CHECK_LAUNCH();
     std::swap(k0, k1);
     std::swap(v0, v1);
