@@ -991,6 +991,7 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
     uint64_t S = 0, SPN = 0;  // split bytes; '<' / '&' bytes (span starters)
 #pragma unroll
     for (int w = 0; w < kTokWords; w++) {
+      if (texp & 32) break;  // (timing experiment: no byte classes)
       const uint4 q = L.st4[kTokWords * tid + w];
       uint32_t acc = 0;  // bits 0-15 split, 16-31 span starter
 #pragma unroll
@@ -1102,7 +1103,7 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
       nk = lo;
     }
     auto fr = [&](int k) { return (k == 0 && L.rs[0] < 0) ? 0 : L.c0[k]; };
-    for (int32_t rlo = 0; rlo < blk_cnt; rlo += kTokCap) {
+    for (int32_t rlo = 0; rlo < ((texp & 16) ? 0 : blk_cnt); rlo += kTokCap) {  // (16: no token passes)
       const int32_t nr = min(kTokCap, blk_cnt - rlo);
       // pass 2: start positions of the round's tokens by chunk rank
       if (tid == 0) L.nmiss = 0;
@@ -2991,7 +2992,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
 #ifdef SME_EXPERIMENTS
         // SME_TOKEXP (timing experiments, experiment builds only; wrong results):
         // 1 no signatures / probes, 2 no token stores, 4 no raw_insert (a miss
-        // takes its home slot), 8 home slot only (no probe walk, no insert)
+        // takes its home slot), 8 home slot only (no probe walk, no insert),
+        // 16 no token passes (positions, probes, stores), 32 no byte classes
         if (const char *tx = getenv("SME_TOKEXP")) tokexp = atoi(tx);
 #endif
         hipLaunchKernelGGL(k_tok_fast, dim3((unsigned)((nF + rpb - 1) / rpb)), dim3(kTokNT), 0, st, t, (int64_t)n, rsF,

@@ -424,6 +424,13 @@ __global__ void k_term_rows(const int32_t *mark, const int32_t *row_of, int64_t 
       rdf[row_of[t]] = off[t + 1] - off[t];
     }
 }
+// df of the rows the window skip table needs (sparse terms); heavy rows 0, and
+// the last entry 0 (the exclusive scan's total)
+__global__ void k_sparse_rdf(const int32_t *term_of_row, const int64_t *rdf, const int32_t *hrow_of, int64_t nrows,
+                             int64_t *rdfw) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r <= nrows; r += (int64_t)gridDim.x * blockDim.x)
+    rdfw[r] = r == nrows ? 0 : (hrow_of[term_of_row[r]] >= 0 ? 0 : rdf[r]);
+}
 __global__ void k_max_qlen(const int64_t *qoff, int nq, int *mx) {
   int m = 0;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x)
@@ -538,7 +545,7 @@ __global__ void k_row_qlut(const int32_t *term_of_row, int64_t nrows, const doub
 // df, then smaller id) and second heaviest, so concurrent waves on one XCD read
 // the same rows / posting ranges.
 __global__ void k_query_keys(const int32_t *terms, const int64_t *qoff, int nq, const int64_t *off, int64_t V,
-                             uint64_t *keys, int32_t *idx) {
+                             int tb, uint64_t *keys, int32_t *idx) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
     int64_t d1 = -1, d2 = -1;
     uint32_t t1 = 0xFFFFFFFFu, t2 = 0xFFFFFFFFu;
@@ -556,7 +563,8 @@ __global__ void k_query_keys(const int32_t *terms, const int64_t *qoff, int nq, 
         t2 = (uint32_t)t;
       }
     }
-    keys[q] = ((uint64_t)t1 << 32) | t2;
+    // (heaviest, second heaviest) term ids in tb bits each (no term: V, last)
+    keys[q] = ((uint64_t)min<uint64_t>(t1, (uint64_t)V) << tb) | min<uint64_t>(t2, (uint64_t)V);
     idx[q] = q;
   }
 }
@@ -2000,10 +2008,21 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
             const int64_t nwin = T >> 2, ne = nrows * (nwin + 1);
             skt = W[31].as<int32_t>(ne);
             SME_HIP(hipMemsetAsync(skt, 0x7F, (size_t)ne * sizeof(int32_t), st));
-            hipLaunchKernelGGL(k_skipw_fill, dim3(16384), dim3(256), 0, st, rpre, nrows, tor, off, dn, ix->dmin, nwin,
+            // only the sparse rows: k_query_win reads heavy terms from their impact
+            // rows, never their skip entries (and heavy terms hold most postings)
+            const int32_t *hro = ix->q_H > 0 ? (const int32_t *)ix->d_hrow_of.p : nullptr;
+            int64_t *rdfw = rdf, *rprew = rpre;
+            if (hro) {
+              rdfw = W[12].as<int64_t>(nrows + 1);
+              rprew = W[13].as<int64_t>(nrows + 1);
+              hipLaunchKernelGGL(k_sparse_rdf, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 16384)), dim3(256),
+                                 0, st, tor, rdf, hro, nrows, rdfw);
+              excl_scan(rdfw, rprew, nrows + 1, cx->ws[23], st);
+            }
+            hipLaunchKernelGGL(k_skipw_fill, dim3(16384), dim3(256), 0, st, rprew, nrows, tor, off, dn, ix->dmin, nwin,
                                skt);
             hipLaunchKernelGGL(k_skipw_suffix, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 16384)),
-                               dim3(256), 0, st, rdf, nrows, nwin, skt);
+                               dim3(256), 0, st, rdfw, nrows, nwin, skt);
           } else {
             build_sk();
           }
@@ -2027,11 +2046,14 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     // heaviest-term query order
     uint64_t *qk = W[46].as<uint64_t>(2 * (size_t)nq);
     int32_t *qi = W[45].as<int32_t>(2 * (size_t)nq);
+    int tb = 1;
+    while (tb < 32 && (1ll << tb) <= V) tb++;  // ids 0 .. V (V = no term)
     hipLaunchKernelGGL(k_query_keys, dim3(std::min((nq + 255) / 256, 4096)), dim3(256), 0, st, d_terms, d_qoff, nq, off,
-                       V, qk, qi);
+                       V, tb, qk, qi);
     uint32_t *rscr = W[35].as<uint32_t>(kv_sort_scratch(nq) / sizeof(uint32_t) + 1);
     qord = reinterpret_cast<const int32_t *>(kv_sort<uint64_t>(qk, reinterpret_cast<uint32_t *>(qi), qk + nq,
-                                                               reinterpret_cast<uint32_t *>(qi + nq), nq, 64, rscr, st));
+                                                               reinterpret_cast<uint32_t *>(qi + nq), nq, 2 * tb, rscr,
+                                                               st));
   }
   // events on the launch stream bracket the scoring kernel (bench.py roofline)
   hipEvent_t e0, e1, e2, e3;
