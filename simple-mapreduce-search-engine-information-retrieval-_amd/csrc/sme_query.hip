@@ -1494,11 +1494,36 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
               const int r = (int)clist[c0 + lane];
               const int32_t d = (int32_t)(wbase + r);
               uint32_t tie = 0xFFFFFFFFu;
+              // the first 8 heavy terms' tf bytes first, their loads in flight
+              // together (the ordered sum below would wait on each in turn)
+              uint64_t hb = 0;
+              {
+                uint64_t mh = hm;
+                uint32_t fb[8];
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                  fb[c] = 0;
+                  if (mh) {
+                    const int j = (int)__builtin_ctzll(mh);
+                    mh &= mh - 1;
+                    fb[c] = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
+                  }
+                }
+#pragma unroll
+                for (int c = 0; c < 8; c++) hb |= (uint64_t)fb[c] << (8 * c);
+              }
+              int hseen = 0;
               for (uint64_t m = amask; m; m &= m - 1) {
                 const int j = (int)__builtin_ctzll(m);
                 int f = 0;
                 if ((hm >> j) & 1) {
-                  f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
+                  if (hseen < 8) {
+                    f = (int)(hb & 0xFFu);
+                    hb >>= 8;
+                  } else {
+                    f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
+                  }
+                  hseen++;
                 } else if (listed) {
                   const int lo0 = __builtin_amdgcn_readlane(prej, j), hi0 = lo0 + __builtin_amdgcn_readlane(cj, j);
                   int lo = lo0, hi = hi0;
