@@ -6,11 +6,13 @@
 //
 // LSD radix sort over the term id, <= 11-bit digits (2 passes for the 21-bit
 // ids of c2).  Each pass is reduce-then-scan, no inter-block waiting:
-//   k_rs_count   one 16384-item tile per 1024-thread block: LDS digit
+//   k_rs_count   one 8192-item tile per 512-thread block: LDS digit
 //                histogram, written tile-major (coalesced)
-//   k_rs_colsum  per (digit, tile group) sums; k_rs_scan one-block exclusive
-//                scan over them in digit-major order; k_rs_colscan turns the
-//                tile counts into each (tile, digit)'s global output offset
+//   k_rs_colsum  per (digit, tile group) sums, up to 1024 groups (c2's 45 k
+//                tiles x 2048 digits are 372 MB, which 256 groups of 178 tiles
+//                read at 1.3 TB/s); an exclusive scan over them in digit-major
+//                order (one block, or device-wide when long); k_rs_colscan turns
+//                the tile counts into each (tile, digit)'s global output offset
 //   k_rs_scatter each wave ranks its 1024 contiguous items with ballot peer
 //                masks and running per-wave digit counters in LDS (stable);
 //                the block scans those counters (digits, then waves) into the
@@ -37,7 +39,8 @@ constexpr int kRsWaveItems = 64 * kRsIPL;   // 1024 contiguous items per wave
 constexpr int kRsMaxBits = 11;
 constexpr int kRsMaxBins = 1 << kRsMaxBits;
 constexpr int kRsBPT = kRsMaxBins / kRsNT;  // digits per thread in the scatter's tile scan
-constexpr int kRsGroups = 256;              // most tile groups of the column scan
+constexpr int kRsGroups = 1024;             // most tile groups of the column scan
+constexpr int kRsScanSums = 1024;           // device scan of the (digit, group) sums: its tile sums
 
 // Tile groups of the column scan: at least 4 tiles a group, so the one-block
 // scan over (digit, group) sums stays short for small sorts; a multiple of 16
@@ -651,6 +654,19 @@ __global__ void k_select_scatter(const uint8_t *__restrict__ f, const int64_t *_
   }
 }
 
+// exclusive scan of the n (digit, group) sums in place: one block when short,
+// else the device-wide reduce-then-scan (sums: kRsScanSums u32 of scratch)
+void rs_scan(uint32_t *gsum, int64_t n, uint32_t *sums, hipStream_t st) {
+  if (n <= 16 * 4 * kRsNT) {
+    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, (int)n);
+    return;
+  }
+  const int64_t nt = (n + kScTile - 1) / kScTile;
+  hipLaunchKernelGGL(k_sc_sums<uint32_t>, dim3((unsigned)nt), dim3(kScNT), 0, st, gsum, n, sums);
+  hipLaunchKernelGGL(k_sc_carry<uint32_t>, dim3(1), dim3(kScNT), 0, st, sums, nt);
+  hipLaunchKernelGGL(k_sc_apply<uint32_t>, dim3((unsigned)nt), dim3(kScNT), 0, st, gsum, gsum, n, sums);
+}
+
 }  // namespace
 
 // Stable sort of P (key, packed value) pairs by the low `bits` bits of key.
@@ -671,7 +687,7 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
   uint32_t *gsum = counts + ntiles * kRsMaxBins;
   Gather g0{nullptr, nullptr, nullptr, 0};
   if (reg != nullptr) {
-    int64_t *crec = reinterpret_cast<int64_t *>(gsum + kRsMaxBins * kRsGroups);
+    int64_t *crec = reinterpret_cast<int64_t *>(gsum + kRsMaxBins * kRsGroups + kRsScanSums);
     const int64_t nch = (P + 1023) >> 10;
     hipLaunchKernelGGL(k_rs_chunk_rec, dim3((unsigned)std::min<int64_t>((nch + 255) / 256, 4096)), dim3(256), 0, st,
                        xoff, nrec, P, crec);
@@ -685,7 +701,7 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
     const bool last = p == npass - 1;
     hipLaunchKernelGGL(k_rs_count, dim3((unsigned)ntiles), dim3(kRsNT), 0, st, k0, P, shift, nbins, counts, g);
     hipLaunchKernelGGL(k_rs_colsum, dim3(G), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, G, gsum);
-    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, nbins * G);
+    rs_scan(gsum, (int64_t)nbins * G, gsum + kRsMaxBins * kRsGroups, st);
     hipLaunchKernelGGL(k_rs_colscan, dim3(G), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, G, gsum);
     const unsigned sgrid = (unsigned)(8 * ((ntiles + 7) / 8));  // see the XCD tile order in k_rs_scatter
     if (last)
@@ -704,7 +720,7 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
 
 size_t term_sort_scratch(int64_t P) {
   const int64_t ntiles = (std::max<int64_t>(P, 1) + kRsTile - 1) / kRsTile;
-  return (size_t)(ntiles * kRsMaxBins + (int64_t)kRsMaxBins * kRsGroups) * sizeof(uint32_t) +
+  return (size_t)(ntiles * kRsMaxBins + (int64_t)kRsMaxBins * kRsGroups + kRsScanSums) * sizeof(uint32_t) +
          (size_t)(((std::max<int64_t>(P, 1) + 1023) >> 10) + 1) * sizeof(int64_t);
 }
 // Stable sort of n (key, u32 value) pairs by the low `bits` bits of the key
@@ -730,7 +746,7 @@ uint32_t *kv_sort(K *k0, uint32_t *v0, K *k1, uint32_t *v1, int64_t n, int bits,
     const int nbins = 1 << nb;
     hipLaunchKernelGGL(k_kv_count<K>, dim3((unsigned)ntiles), dim3(kRsNT), 0, st, k0, n, shift, nbins, counts);
     hipLaunchKernelGGL(k_rs_colsum, dim3(G), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, G, gsum);
-    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kRsNT), 0, st, gsum, nbins * G);
+    rs_scan(gsum, (int64_t)nbins * G, gsum + kRsMaxBins * kRsGroups, st);
     hipLaunchKernelGGL(k_rs_colscan, dim3(G), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, G, gsum);
     const unsigned sgrid = (unsigned)(8 * ((ntiles + 7) / 8));
     if (p == npass - 1 && !keys_out)
@@ -781,6 +797,6 @@ void select_flagged(const uint8_t *flag, int64_t n, int32_t *out, int32_t *d_cou
 
 size_t kv_sort_scratch(int64_t n) {
   const int64_t ntiles = (std::max<int64_t>(n, 1) + kRsTile - 1) / kRsTile;
-  return (size_t)(ntiles * kRsMaxBins + (int64_t)kRsMaxBins * kRsGroups) * sizeof(uint32_t);
+  return (size_t)(ntiles * kRsMaxBins + (int64_t)kRsMaxBins * kRsGroups + kRsScanSums) * sizeof(uint32_t);
 }
 }  // namespace sme
