@@ -5,12 +5,13 @@ the c4 distribution (V_w = 2^22, 200-360 tokens, Zipf s = 1, seed 44) with about
 6.8 M local terms (the words it holds + its 6.25 M docid terms).  This builds
 such a shard in HBM, runs the real global_df_index on a world-1 RCCL group
 (fingerprints + offsets, gather, unique, reduce), and then times the part that
-grows with the world on the device: torch.unique + index_add + gather over the
-8-shard gathered fingerprint set, emulated from this shard's own fingerprints
-(rows with df > 1 -- the words -- shared by all 8 shards, the df = 1 rows --
-docid terms and rare words -- made shard-private by xoring the shard number
-into the fingerprint).  The all-gather itself needs 8 GPUs; its volume is
-reported.  Writes profiles/r03_dfx_c4.json.
+grows with the world on the device: the owner's unique + index_add + gather over the
+8-shard set, emulated from this shard's own fingerprints (rows with df > 1 --
+the words -- shared by all 8 shards, the df = 1 rows -- docid terms and rare
+words -- made shard-private by xoring the shard number into the fingerprint):
+dist.df_exchange sends each row to the owner rank of its fingerprint, so one
+owner deduplicates and sums 1/8 of all shards' rows.  The all_to_alls need 8
+GPUs; their volume is reported.  Writes gpurun_out/dfx_c4.json (kept as profiles/r04_dfx_c4.json).
     python tools/dfx_c4.py [--docs 6250000] [--world 8]
 """
 import argparse
@@ -55,7 +56,9 @@ def main():
         t["total_ms"] = (time.perf_counter() - ts) * 1e3
         runs.append(t)
     out["world1_global_df_index"] = runs[-1]
-    # emulated world-W gather: the device-side dedup that grows with the world
+    # emulated world-W owner exchange (dist.df_exchange): rank r receives, from
+    # each of the W shards, the rows whose fingerprint's first word is r mod W;
+    # it deduplicates and sums only those, then returns each sender its rows
     V = int(ix.V)
     fp = torch.empty((V, 2), dtype=torch.int64, device="cuda")
     ix.term_fingerprints(fp.data_ptr(), torch.cuda.current_stream().cuda_stream)
@@ -65,33 +68,51 @@ def main():
     torch.cuda.synchronize()
     df = offs[1:] - offs[:-1]
     private = df == 1
-    parts = []
+    parts, dfs = [], []
     for s in range(a.world):
         f = fp.clone()
         f[private, 1] ^= (s + 1) << 40
+        f[private, 0] ^= (s + 1) << 40  # shard-private terms: owners spread like any term's
         parts.append(f)
+        dfs.append(df)
     allfp = torch.cat(parts, 0)
-    del parts
-    times = []
+    alldf = torch.cat(dfs, 0)
+    del parts, dfs
+    mine = torch.remainder(allfp[:, 0], a.world) == 0
+    recv_fp = allfp[mine].contiguous()
+    recv_df = alldf[mine].contiguous()
+    del allfp, alldf
+    send_t, owner_t = [], []
     for _ in range(3):
         torch.cuda.synchronize()
         ts = time.perf_counter()
-        uniq, inv = torch.unique(allfp, dim=0, return_inverse=True)
-        mine = inv[:V]
-        g = torch.zeros(uniq.shape[0], dtype=torch.int64, device="cuda")
-        g.index_add_(0, mine, df)
-        res = g[mine].contiguous()
+        owner = torch.remainder(fp[:, 0], a.world)
+        order = torch.argsort(owner, stable=True)
+        send_fp = fp[order].contiguous()
+        send_df = df[order].contiguous()
         torch.cuda.synchronize()
-        times.append((time.perf_counter() - ts) * 1e3)
+        t1 = time.perf_counter()
+        uniq, inv = D._unique_rows(recv_fp)
+        g = torch.zeros(uniq.shape[0], dtype=torch.int64, device="cuda")
+        g.index_add_(0, inv, recv_df)
+        back = g[inv].contiguous()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        send_t.append((t1 - ts) * 1e3)
+        owner_t.append((t2 - t1) * 1e3)
     out["emulated_world"] = a.world
-    out["emulated_gathered_terms"] = int(allfp.shape[0])
-    out["emulated_global_terms"] = int(uniq.shape[0])
-    out["emulated_unique_reduce_ms"] = round(min(times), 3)
-    out["all_gather_bytes_per_rank"] = int(a.world * V * 16)
+    out["emulated_rows_received_by_owner"] = int(recv_fp.shape[0])
+    out["emulated_terms_owned"] = int(uniq.shape[0])
+    out["emulated_send_prep_ms"] = round(min(send_t), 3)
+    out["emulated_owner_dedup_reduce_ms"] = round(min(owner_t), 3)
+    out["all_to_all_bytes_out_per_rank"] = int(24 * V)
+    out["all_to_all_bytes_back_per_rank"] = int(8 * V)
     out["private_terms"] = int(private.sum().item())
-    out["what"] = ("world-1 global_df_index at c4 shard size (real path), then torch.unique + index_add + gather "
-                   "over an emulated %d-shard fingerprint set (df>1 rows shared, df=1 rows shard-private); the "
-                   "all-gather needs %d GPUs and is reported as bytes" % (a.world, a.world))
+    out["what"] = ("world-1 global_df_index at c4 shard size (real path), then the owner side of dist.df_exchange "
+                   "for an emulated %d-shard set (df>1 rows shared, df=1 rows shard-private): one owner's received "
+                   "rows (1/%d of every shard's) deduplicated + summed, and the sender's owner sort; the two "
+                   "all_to_alls need %d GPUs and are reported as bytes" % (a.world, a.world, a.world))
+    res = back
     del res, gdf
     print(json.dumps(out), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
