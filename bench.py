@@ -302,11 +302,8 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     barrier()
     gc.collect()
     gc.disable()  # no cyclic-GC pause inside the timed batches (re-enabled after)
-    # a one-off host stall of ~50 ms right after the timed region opens was seen
-    # on the GPU box (cause not found: not GC, not the profile read); >= 5
-    # batches amortise it like any other steady-state overhead (10 at least)
-    # batches: at least 10 and enough for ~1.5 s of query work (a one-off stall
-    # then moves the mean by < 4 %), at most 50; every rank runs the same count
+    # batches: at least 10 and enough for ~1.5 s of query work, at most 50;
+    # every rank runs the same count
     ts1 = time.perf_counter()
     qstep()
     torch.cuda.synchronize()
@@ -318,17 +315,34 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     barrier()
     steps = max(a.steps, min(50, max(10, int(1.5 / max(t_one, 1e-6)))))
     kms, pms, kname = [], [], "k_query"
+
+    def _cg():
+        try:
+            return {l.split()[0]: int(l.split()[1]) for l in open("/sys/fs/cgroup/cpu.stat")}
+        except (OSError, ValueError, IndexError):
+            return {}
+    cg0 = _cg() if os.environ.get("SME_BENCH_VERBOSE") else None
+    # the per-batch records are allocated before the clock starts (a ~50 ms
+    # host stall was measured at the first allocation after it on the GPU box)
+    walls = [0.0] * steps
+    starts = [0.0] * steps
     t0 = time.perf_counter()
-    walls = []
-    for _ in range(steps):
+    for i in range(steps):
         tq = time.perf_counter()
+        starts[i] = tq
         qstep()
-        walls.append((time.perf_counter() - tq) * 1e3)
+        walls[i] = (time.perf_counter() - tq) * 1e3
+    tb = time.perf_counter()
     barrier()
     dt = (time.perf_counter() - t0) / steps
     gc.enable()
     if os.environ.get("SME_BENCH_VERBOSE"):
-        print("query step walls %s ms" % ["%.3f" % w for w in walls], file=sys.stderr)
+        cg1 = _cg()
+        print("query step walls %s ms, loop %.3f ms, closing barrier %.3f ms, cgroup cpu.stat delta %s" % (
+              ["%.3f" % w for w in walls], (tb - t0) * 1e3, (time.perf_counter() - tb) * 1e3,
+              {k: cg1[k] - cg0.get(k, 0) for k in cg1}), file=sys.stderr)
+        print("query step gaps (start - previous end) %s ms" % ["%.3f" % ((starts[i] - (starts[i - 1] if i else t0)) * 1e3 -
+              (walls[i - 1] if i else 0.0)) for i in range(len(starts))], file=sys.stderr)
     # device-event timings of the last batch (read after the timed region: the
     # profile call is measurement overhead, not query work; every batch is identical)
     qp = ix.ctx.last_build_profile()
