@@ -248,8 +248,10 @@ def main():
         ix = None
         gc.collect()
         result["end_to_end_ms"] = end_to_end_stage(sme, ctx, d_corpus.value, nbytes, torch)
-    if rank == 0 and a.cpu_docs > 0 and a.config == "c2":
+    if rank == 0 and a.cpu_docs > 0:
         result["cpu_baseline"] = cpu_baseline(synth, a)
+        if a.config == "c2":
+            result["c1_sample"] = c1_sample(sme, a)
         if cpu_full is not None:
             result["cpu_baseline"]["cpu_opt"].update(cpu_full)
     if rank == 0:
@@ -614,9 +616,10 @@ def cpu_baseline(synth, a):
            "cpu_model": _cpu_model(),
            "cores_what": "threads used = OMP_NUM_THREADS (the GPU box's CPU share for one GPU's job; nproc "
                          "shows the whole host) or the affinity set"}
-    # ref-faithful build + rank() (indexOf scan) on a small sample
+    # ref-faithful build + rank() (indexOf scan) on a small sample of this config's distribution
+    cfg = a.cfg
     n_ref = a.cpu_docs
-    corpus = synth.gen_corpus(n_ref, V=a.vocab, seed=42, len_lo=400, len_hi=600)
+    corpus = synth.gen_corpus(n_ref, V=a.vocab, seed=cfg["seed"], len_lo=cfg["lo"], len_hi=cfg["hi"])
     mapping = synth.mapping_bytes(n_ref)
     t0 = time.perf_counter()
     ref = O.OracleIndex(corpus, mapping, 1, 1)
@@ -625,38 +628,82 @@ def cpu_baseline(synth, a):
     cpu_small = O.CpuOptIndex(corpus, mapping, threads)
     off, _, _, terms = cpu_small.csr()
     df = np.diff(off).astype(np.int32)
-    tq, qo = synth.queries_by_df(df, a.cpu_ref_queries, seed=7)
+    tq, qo = synth.queries_by_df(df, a.cpu_ref_queries, seed=cfg["qseed"])
     O.lib().or_set_ref_scan(1)
     t0 = time.perf_counter()
     for q in range(len(qo) - 1):
-        ref.query([terms[t] for t in tq[qo[q]:qo[q + 1]]], 10, 0, 0)
+        ref.query([terms[t] for t in tq[qo[q]:qo[q + 1]]], cfg["k"], 0, 0)
     dt_rq = time.perf_counter() - t0
     O.lib().or_set_ref_scan(0)
     del ref, cpu_small
     out["ref_faithful"] = {
         "build_GBps": round(len(corpus) / dt_ref / 1e9, 6), "cores": 1,
-        "build_sample": "%d docs (%d bytes) of c2, %.1f s" % (n_ref, len(corpus), dt_ref),
+        "build_sample": "%d docs (%d bytes) of %s, %.1f s" % (n_ref, len(corpus), a.config, dt_ref),
         "query_qps": round(a.cpu_ref_queries / dt_rq, 2),
-        "query_sample": "%d c3-style top-10 queries over that %d-doc index (indexOf accumulator), %.1f s"
-                        % (a.cpu_ref_queries, n_ref, dt_rq)}
+        "query_sample": "%d c3-style top-%d queries over that %d-doc index (indexOf accumulator), %.1f s"
+                        % (a.cpu_ref_queries, cfg["k"], n_ref, dt_rq)}
     n_opt = a.cpu_opt_docs
-    corpus = synth.gen_corpus(n_opt, V=a.vocab, seed=42, len_lo=400, len_hi=600)
+    corpus = synth.gen_corpus(n_opt, V=a.vocab, seed=cfg["seed"], len_lo=cfg["lo"], len_hi=cfg["hi"])
     mapping = synth.mapping_bytes(n_opt)
     t0 = time.perf_counter()
     cpu = O.CpuOptIndex(corpus, mapping, threads)
     dt_opt = time.perf_counter() - t0
     off, _, _, _ = cpu.csr()
     df = np.diff(off).astype(np.int32)
-    tq, qo = synth.queries_by_df(df, a.cpu_opt_queries, seed=7)
-    _, _, dt_q = cpu.query(tq, qo, 10, 0, threads)
+    tq, qo = synth.queries_by_df(df, a.cpu_opt_queries, seed=cfg["qseed"])
+    _, _, dt_q = cpu.query(tq, qo, cfg["k"], 0, threads)
     out["value"] = round(len(corpus) / dt_opt / 1e9, 6)
-    out["sample"] = ("cpu-opt (%d threads): build of %d docs (%d bytes) of c2 in %.1f s; %d c3-style top-10 queries "
-                     "over that index in %.2f s" % (threads, n_opt, len(corpus), dt_opt, a.cpu_opt_queries, dt_q))
+    out["sample"] = ("cpu-opt (%d threads): build of %d docs (%d bytes) of %s in %.1f s; %d c3-style top-%d queries "
+                     "over that index in %.2f s" % (threads, n_opt, len(corpus), a.config, dt_opt, a.cpu_opt_queries,
+                                                    cfg["k"], dt_q))
     out["cpu_opt"] = {"build_GBps": out["value"], "build_GBps_per_thread": round(out["value"] / threads, 6),
                       "query_qps": round(a.cpu_opt_queries / dt_q, 1), "query_index_docs": n_opt,
                       "query_what": "query_qps: over the %d-doc sample index; query_qps_full_index: over the "
                                     "GPU's full-size index" % n_opt}
     return out
+
+
+def c1_sample(sme, a):
+    """c1: the committed 1,000-document seed-1 sample
+    (tests/golden/c1_sample_trec.xml + its mapping), built by libsme from device
+    memory (best of 5 after a warm-up) and by both CPU legs."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    g = os.path.join(ROOT, "tests", "golden")
+    corpus = open(os.path.join(g, "c1_sample_trec.xml"), "rb").read()
+    mapping = open(os.path.join(g, "c1_sample_mapping.bin"), "rb").read()
+    threads, _ = cpu_threads()
+    ctx = sme.Context(1, 1)
+    ctx.load_docno_mapping(mapping)
+    d = torch.frombuffer(bytearray(corpus), dtype=torch.uint8).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    ms = []
+    for i in range(6):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ix = ctx.build_device(d.data_ptr(), len(corpus), stream)
+        torch.cuda.synchronize()
+        if i:
+            ms.append((time.perf_counter() - t0) * 1e3)
+        N, V, P = ix.N, ix.V, ix.P
+        ix.close()
+    ctx.close()
+    t0 = time.perf_counter()
+    ref = O.OracleIndex(corpus, mapping, 1, 1)
+    dt_ref = time.perf_counter() - t0
+    del ref
+    t0 = time.perf_counter()
+    cpu = O.CpuOptIndex(corpus, mapping, threads)
+    dt_opt = time.perf_counter() - t0
+    del cpu
+    return {"docs": N, "terms": V, "postings": P, "bytes": len(corpus), "gpu_build_ms": round(min(ms), 3),
+            "gpu_build_GBps": round(len(corpus) / min(ms) / 1e6, 3),
+            "cpu_ref_faithful_ms": round(dt_ref * 1e3, 1), "cpu_opt_ms": round(dt_opt * 1e3, 1),
+            "cpu_opt_threads": threads,
+            "what": "tests/golden/c1_sample_trec.xml (1,000 docs, seed 1): libsme build from device memory (best of "
+                    "5, wall clock incl. launch latency), oracle ref-faithful (1 thread), cpu-opt; parity of this "
+                    "sample is tests/test_gpu_parity.py::test_c1_sample_on_device"}
 
 
 if __name__ == "__main__":
