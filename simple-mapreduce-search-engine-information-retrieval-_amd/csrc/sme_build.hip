@@ -25,7 +25,6 @@
 //   K7 weights          w = LUT[tf] * idf(term)  (fp64, no contraction)
 //   K8 sort by (term, tf desc)  stable -> MyReducer.reduce's output order
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <limits.h>
 #include <math.h>
 #include <stdio.h>
@@ -3332,8 +3331,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       const int64_t nbig = (int64_t)d2h(cnt + 26, st);
       if (nbig > 0) {
         int64_t *bl2 = W[W_BIGL2].as<int64_t>(nbig);
-        SME_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tbb, ai.big_out, bl2, (int)nbig, 0, 64, st));
-        SME_HIP(hipcub::DeviceRadixSort::SortKeys(cub_tmp(tbb), tbb, ai.big_out, bl2, (int)nbig, 0, 64, st));
+        sort_pairs_v64<uint64_t>(reinterpret_cast<uint64_t *>(ai.big_out), reinterpret_cast<uint64_t *>(bl2), nullptr,
+                                 nullptr, nbig, 64, cx->ws[120], cx->ws[121], cx->ws[122], st);
         int64_t *bcap = W[W_BIGCAP].as<int64_t>(nbig + 1), *boff = W[W_RLIST].as<int64_t>(nbig + 1);
         hipLaunchKernelGGL(k_big_caps, dim3(grid_for(nbig)), dim3(256), 0, st, bl2, nbig, perm, ntok, max_nout, bcap);
         SME_HIP(hipMemsetAsync(bcap + nbig, 0, sizeof(int64_t), st));
@@ -3376,8 +3375,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     // deterministic order of big records (atomic compaction above is unordered)
     size_t tbb = 0;
     int64_t *bl2 = W[W_SCROFF].as<int64_t>(nbig);
-    SME_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tbb, big_list, bl2, (int)nbig, 0, 64, st));
-    SME_HIP(hipcub::DeviceRadixSort::SortKeys(cub_tmp(tbb), tbb, big_list, bl2, (int)nbig, 0, 64, st));
+    sort_pairs_v64<uint64_t>(reinterpret_cast<uint64_t *>(big_list), reinterpret_cast<uint64_t *>(bl2), nullptr,
+                             nullptr, nbig, 64, cx->ws[120], cx->ws[121], cx->ws[122], st);
     big_list = bl2;
     bcap = W[W_T0].as<int64_t>(nbig + 1);
     boff = W[W_T1].as<int64_t>(nbig + 1);
@@ -3460,17 +3459,17 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     uint64_t *pkey_s = W[W_CKEY].as<uint64_t>(Pg + 1);
     p_val = W[W_PVAL].as<uint64_t>(Pg + 1);
     if (Pg > 0) {
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, pkey, pkey_s, pval0, p_val, (int)Pg, 0, K * tb, st));
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, pkey, pkey_s, pval0, p_val, (int)Pg, 0, K * tb,
-                                                 st));
+      sort_pairs_v64<uint64_t>(pkey, pkey_s, pval0, p_val, Pg, K * tb, cx->ws[120], cx->ws[121], cx->ws[122], st);
     }
-    uint32_t *gflag = W[W_VSLOT].as<uint32_t>(Pg + 1), *gincl = W[W_VIDX].as<uint32_t>(Pg + 1);
+    uint32_t *gflag = W[W_VSLOT].as<uint32_t>(Pg + 1), *gincl = W[W_VIDX].as<uint32_t>(Pg + 2);
     p_term = W[W_PTERM].as<uint32_t>(Pg + 1);
     int64_t Vg = 0;
     if (Pg > 0) {
       hipLaunchKernelGGL(k_gram_flags, dim3(grid_for(Pg)), dim3(256), 0, st, pkey_s, Pg, gflag);
-      SME_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tbb, gflag, gincl, (int)Pg, st));
-      SME_HIP(hipcub::DeviceScan::InclusiveSum(cub_tmp(tbb), tbb, gflag, gincl, (int)Pg, st));
+      // inclusive sum = the exclusive scan of (flags, 0) shifted by one
+      SME_HIP(hipMemsetAsync(gflag + Pg, 0, sizeof(uint32_t), st));
+      excl_scan(gflag, gincl, Pg + 1, cx->ws[23], st);
+      gincl += 1;
       Vg = (int64_t)d2h(gincl + Pg - 1, st);
       int32_t *gcomp = ix->d_gram.as<int32_t>(Vg * K + 1);
       hipLaunchKernelGGL(k_gram_ids, dim3(grid_for(Pg)), dim3(256), 0, st, pkey_s, gincl, Pg, K, tb, p_term, gcomp);
@@ -3550,22 +3549,15 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     SME_CHECK_LAUNCH();
   } else {
     uint64_t *val_s = W[W_T1].as<uint64_t>(P + 1);
-    if (P > 0) {
-      size_t tbb = 0;
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, p_term, key_s, p_val, val_s, (int)P, 0, tbits, st));
-      SME_HIP(
-          hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, p_term, key_s, p_val, val_s, (int)P, 0, tbits, st));
-    }
+    if (P > 0)
+      sort_pairs_v64<uint32_t>(p_term, key_s, p_val, val_s, P, tbits, cx->ws[120], cx->ws[121], cx->ws[122], st);
     if (dup_docno && P > 0) {
       // MyReducer.reduce: equal docnos (duplicate docids) are merged by summing tf
       uint64_t *ck = W[W_PVAL].as<uint64_t>(P), *ck2 = W[W_T2].as<uint64_t>(P);
       int32_t *tfv = reinterpret_cast<int32_t *>(W[W_PTERM].as<uint32_t>(P)), *tf2 = W[W_T3].as<int32_t>(P);
       hipLaunchKernelGGL(k_dup_keys, dim3(grid_for(P)), dim3(256), 0, st, key_s, val_s, P, ck, tfv);
       int64_t *nout = reinterpret_cast<int64_t *>(cnt + 10);
-      size_t tbb = 0;
-      SME_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tbb, ck, ck2, tfv, tf2, nout, hipcub::Sum(), (int)P, st));
-      SME_HIP(
-          hipcub::DeviceReduce::ReduceByKey(cub_tmp(tbb), tbb, ck, ck2, tfv, tf2, nout, hipcub::Sum(), (int)P, st));
+      reduce_by_key_sum(ck, tfv, P, ck2, tf2, nout, cx->ws[120], cx->ws[121], cx->ws[23], st);
       Pm = d2h(nout, st);
       hipLaunchKernelGGL(k_dup_unpack, dim3(grid_for(Pm)), dim3(256), 0, st, ck2, tf2, Pm, key_s, val_s);
     }
@@ -3578,9 +3570,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     SME_CHECK_LAUNCH();
     if (Pm > 0) {
       int32_t *mx = reinterpret_cast<int32_t *>(cnt + 11);
-      size_t tbb = 0;
-      SME_HIP(hipcub::DeviceReduce::Max(nullptr, tbb, tf_d, mx, (int)Pm, st));
-      SME_HIP(hipcub::DeviceReduce::Max(cub_tmp(tbb), tbb, tf_d, mx, (int)Pm, st));
+      reduce_max<int32_t>(tf_d, Pm, mx, st);
       max_tf = std::max(1, d2h(mx, st));
     }
   }
@@ -3664,21 +3654,18 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       const uint32_t tfmask = (uint32_t)((1ull << tfb) - 1);
       uint32_t *ck = reinterpret_cast<uint32_t *>(W[W_PVAL].as<uint64_t>(PP)), *ck2 = W[W_T2].as<uint32_t>(PP);
       hipLaunchKernelGGL(k_composite32, dim3(grid_for(PP)), dim3(256), 0, st, key_s, tf_d, PP, tfb, tfmask, ck);
-      size_t tbb = 0;
-      SME_HIP(
-          hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, ck, ck2, docno_d, docno_o, (int)PP, 0, tbits + tfb, st));
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, ck, ck2, docno_d, docno_o, (int)PP, 0,
-                                                 tbits + tfb, st));
+      // (docno_d stays intact: the sort's values start from a copy)
+      uint32_t *dv = W[W_T3].as<uint32_t>(PP);
+      SME_HIP(hipMemcpyAsync(dv, docno_d, (size_t)PP * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+      sort_pairs<uint32_t>(ck, ck2, dv, reinterpret_cast<uint32_t *>(docno_o), PP, tbits + tfb, cx->ws[122], st);
       hipLaunchKernelGGL(k_composite32_tf, dim3(grid_for(PP)), dim3(256), 0, st, ck2, PP, tfmask, tf_o);
     } else {
       const uint64_t tfmask = (1ull << tfb) - 1;
       uint64_t *ck = W[W_PVAL].as<uint64_t>(PP), *ck2 = W[W_T2].as<uint64_t>(PP);
       hipLaunchKernelGGL(k_composite, dim3(grid_for(PP)), dim3(256), 0, st, key_s, tf_d, PP, tfb, tfmask, ck);
-      size_t tbb = 0;
-      SME_HIP(
-          hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, ck, ck2, docno_d, docno_o, (int)PP, 0, tbits + tfb, st));
-      SME_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp(tbb), tbb, ck, ck2, docno_d, docno_o, (int)PP, 0,
-                                                 tbits + tfb, st));
+      uint32_t *dv = W[W_T3].as<uint32_t>(PP);
+      SME_HIP(hipMemcpyAsync(dv, docno_d, (size_t)PP * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+      sort_pairs<uint64_t>(ck, ck2, dv, reinterpret_cast<uint32_t *>(docno_o), PP, tbits + tfb, cx->ws[122], st);
       hipLaunchKernelGGL(k_composite_tf, dim3(grid_for(PP)), dim3(256), 0, st, ck2, PP, tfmask, tf_o);
     }
     SME_CHECK_LAUNCH();

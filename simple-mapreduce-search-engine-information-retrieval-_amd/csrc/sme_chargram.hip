@@ -23,7 +23,6 @@
 // (gram, first occurrence), dedup -> per-element HashSet rank key -> sort -> one pass
 // that writes every line at its scanned offset.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
@@ -281,8 +280,6 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   if (K < 1 || K > kCgMaxK) throw Error(SME_ENOTIMPL, "CharKGramTermIndexer with k > 5 is not built");
   ix->job = 1;
   auto &W = cx->ws;  // slots 48..63 (query / serializer region) are free during a build
-  auto tmp = [&](size_t b) { return cx->cub_tmp.get(b); };
-  size_t tbb = 0;
   ix->part_start.assign((size_t)R + 1, 0);
   ix->h_parts.clear();
   ix->h_parts.resize((size_t)R);
@@ -300,8 +297,10 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   uint32_t *ti = W[49].as<uint32_t>(V), *order = W[50].as<uint32_t>(V), *rank = W[51].as<uint32_t>(V);
   unsigned long long *first_s = W[52].as<unsigned long long>(V);
   hipLaunchKernelGGL(k_iota32, dim3(cg_grid(V)), dim3(256), 0, st, ti, V);
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, first, first_s, ti, order, (int)V, 0, 64, st));
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(tmp(tbb), tbb, first, first_s, ti, order, (int)V, 0, 64, st));
+  // (the hand-written LSD sorts clobber their inputs; none is read afterwards unless copied)
+  DevBuf &rs = cx->ws[122];
+  sort_pairs<uint64_t>(reinterpret_cast<uint64_t *>(first), reinterpret_cast<uint64_t *>(first_s), ti, order, V, 64,
+                       rs, st);
   hipLaunchKernelGGL(k_rank_of, dim3(cg_grid(V)), dim3(256), 0, st, order, V, rank);
   int32_t *jh = W[53].as<int32_t>(V), *u8len = W[54].as<int32_t>(V);
   int64_t *ng = W[55].as<int64_t>(V + 1), *goff = W[56].as<int64_t>(V + 1);
@@ -321,31 +320,32 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   uint32_t *kord = W[59].as<uint32_t>(NP), *kterm = W[60].as<uint32_t>(NP);
   hipLaunchKernelGGL(k_gram_pairs, dim3(cg_grid(V)), dim3(256), 0, st, term_off, tch, V, K, goff, rank, khi, klo, kord,
                      kterm);
-  uint32_t *ia = W[61].as<uint32_t>(NP), *ib = W[62].as<uint32_t>(NP);
+  uint32_t *ia = W[61].as<uint32_t>(NP), *ib = W[62].as<uint32_t>(NP + 1);
   uint64_t *k64 = W[52].as<uint64_t>(NP), *k64s = W[48].as<uint64_t>(NP);
   uint32_t *k32s = W[49].as<uint32_t>(NP);
   hipLaunchKernelGGL(k_iota32, dim3(cg_grid(NP)), dim3(256), 0, st, ia, NP);
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, kord, k32s, ia, ib, (int)NP, 0, 32, st));
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(tmp(tbb), tbb, kord, k32s, ia, ib, (int)NP, 0, 32, st));
+  sort_pairs<uint32_t>(kord, k32s, ia, ib, NP, 32, rs, st);
   hipLaunchKernelGGL(k_gather<uint64_t>, dim3(cg_grid(NP)), dim3(256), 0, st, klo, ib, NP, k64);
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, k64, k64s, ib, ia, (int)NP, 0, 64, st));
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(tmp(tbb), tbb, k64, k64s, ib, ia, (int)NP, 0, 64, st));
+  sort_pairs<uint64_t>(k64, k64s, ib, ia, NP, 64, rs, st);
   hipLaunchKernelGGL(k_gather<uint64_t>, dim3(cg_grid(NP)), dim3(256), 0, st, khi, ia, NP, k64);
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, k64, k64s, ia, ib, (int)NP, 0, 64, st));
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(tmp(tbb), tbb, k64, k64s, ia, ib, (int)NP, 0, 64, st));
+  sort_pairs<uint64_t>(k64, k64s, ia, ib, NP, 64, rs, st);
   // dedup equal (gram, term) -> u: pair indices in (gram, insertion) order
   uint8_t *keep = W[63].as<uint8_t>(NP);
   hipLaunchKernelGGL(k_cg_flags, dim3(cg_grid(NP)), dim3(256), 0, st, khi, klo, kterm, ib, NP, keep);
   uint32_t *u = ia;
   int32_t *d_nu = reinterpret_cast<int32_t *>(W[55].as<int64_t>(V + 1));
-  SME_HIP(hipcub::DeviceSelect::Flagged(nullptr, tbb, ib, keep, u, d_nu, (int)NP, st));
-  SME_HIP(hipcub::DeviceSelect::Flagged(tmp(tbb), tbb, ib, keep, u, d_nu, (int)NP, st));
+  int32_t *sel = cx->ws[120].as<int32_t>(NP + 1);
+  select_flagged(keep, NP, sel, d_nu, cx->ws[25], cx->ws[23], st);
   const int64_t n = cg_d2h(d_nu, st);
+  hipLaunchKernelGGL(k_gather<uint32_t>, dim3(cg_grid(n)), dim3(256), 0, st, ib, reinterpret_cast<const uint32_t *>(sel),
+                     n, u);
   // gram segments
-  uint32_t *gflag = ib, *gincl = W[50].as<uint32_t>(std::max<int64_t>(NP, V));
+  uint32_t *gflag = ib, *gincl = W[50].as<uint32_t>(std::max<int64_t>(NP, V) + 1);
   hipLaunchKernelGGL(k_cg_gstart, dim3(cg_grid(n)), dim3(256), 0, st, khi, klo, u, n, gflag);
-  SME_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tbb, gflag, gincl, (int)n, st));
-  SME_HIP(hipcub::DeviceScan::InclusiveSum(tmp(tbb), tbb, gflag, gincl, (int)n, st));
+  // inclusive sum = the exclusive scan of (flags, 0) shifted by one
+  SME_HIP(hipMemsetAsync(gflag + n, 0, sizeof(uint32_t), st));
+  excl_scan(gflag, gincl, n + 1, cx->ws[23], st);
+  gincl += 1;
   const int64_t ngr = cg_d2h(gincl + n - 1, st);
   int64_t *gstart = W[56].as<int64_t>(std::max<int64_t>(ngr + 1, V + 1));
   hipLaunchKernelGGL(k_cg_segs, dim3(cg_grid(n)), dim3(256), 0, st, gincl, n, gstart);
@@ -354,8 +354,11 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   uint64_t *skey = W[52].as<uint64_t>(n), *skey_s = W[48].as<uint64_t>(n);
   hipLaunchKernelGGL(k_cg_setkey, dim3(cg_grid(n)), dim3(256), 0, st, u, kterm, gincl, gstart, ngr, n, jh, skey);
   uint32_t *u2 = ib;
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, skey, skey_s, u, u2, (int)n, 0, 64, st));
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(tmp(tbb), tbb, skey, skey_s, u, u2, (int)n, 0, 64, st));
+  {  // u is read again below: sort a copy of it
+    uint32_t *uc = cx->ws[121].as<uint32_t>(n + 1);
+    SME_HIP(hipMemcpyAsync(uc, u, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    sort_pairs<uint64_t>(skey, skey_s, uc, u2, n, 64, rs, st);
+  }
   uint32_t *g_of = W[59].as<uint32_t>(n), *g_of_s = W[49].as<uint32_t>(n);
   // gram of each element of u2: gincl is by position in u -> scatter by pair index, gather by u2
   {
@@ -364,8 +367,7 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
     hipLaunchKernelGGL(k_gather<uint32_t>, dim3(cg_grid(n)), dim3(256), 0, st, gid_by_pair, u2, n, g_of);
   }
   uint32_t *u3 = W[61].as<uint32_t>(n);
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, g_of, g_of_s, u2, u3, (int)n, 0, 32, st));
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(tmp(tbb), tbb, g_of, g_of_s, u2, u3, (int)n, 0, 32, st));
+  sort_pairs<uint32_t>(g_of, g_of_s, u2, u3, n, 32, rs, st);
   // u3: elements in (gram key, HashSet order); gincl / gstart still describe the segments
   if (prof) prof->mark("cg_sets");
   // line lengths, partitions, offsets
@@ -380,8 +382,7 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
                      part);
   uint32_t *gseq = W[51].as<uint32_t>(ngr + 1), *gorder = W[63].as<uint32_t>(ngr + 1);
   hipLaunchKernelGGL(k_iota32, dim3(cg_grid(ngr)), dim3(256), 0, st, gseq, ngr);
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbb, part, part_s, gseq, gorder, (int)ngr, 0, 32, st));
-  SME_HIP(hipcub::DeviceRadixSort::SortPairs(tmp(tbb), tbb, part, part_s, gseq, gorder, (int)ngr, 0, 32, st));
+  sort_pairs<uint32_t>(part, part_s, gseq, gorder, ngr, 32, rs, st);
   int64_t *llen_s = W[52].as<int64_t>(ngr + 1);
   hipLaunchKernelGGL(k_gather<int64_t>, dim3(cg_grid(ngr)), dim3(256), 0, st, llen, gorder, ngr, llen_s);
   SME_HIP(hipMemsetAsync(llen_s + ngr, 0, sizeof(int64_t), st));

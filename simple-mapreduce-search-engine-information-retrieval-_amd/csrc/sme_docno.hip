@@ -18,7 +18,6 @@
 // reference's text round trip (split("\\t")[0] per line); this path keeps the
 // docid whole.  Such docids are "parity unpinned".
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
@@ -160,8 +159,7 @@ void number_documents(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st,
   int64_t maxlen = 0;
   if (nR > 0) {
     int64_t *mx = W[54].as<int64_t>(1);
-    SME_HIP(hipcub::DeviceReduce::Max(nullptr, tb, len, mx, (int)nR, st));
-    SME_HIP(hipcub::DeviceReduce::Max(cub_tmp(tb), tb, len, mx, (int)nR, st));
+    reduce_max<int64_t>(len, nR, mx, st);
     SME_HIP(hipMemcpyAsync(&maxlen, mx, sizeof maxlen, hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
   }

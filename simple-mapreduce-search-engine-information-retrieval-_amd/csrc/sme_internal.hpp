@@ -197,6 +197,20 @@ template <typename T>
 void excl_scan(const T *in, T *out, int64_t n, DevBuf &scratch, hipStream_t st);
 void select_flagged(const uint8_t *flag, int64_t n, int32_t *out, int32_t *d_count, DevBuf &s1, DevBuf &s2,
                     hipStream_t st);
+// SortPairs-shaped wrappers of kv_sort (separate in / out arrays; the inputs are
+// clobbered): u32 values, or 64-bit values through a sorted index + gather
+template <typename K>
+void sort_pairs(K *keys_in, K *keys_out, uint32_t *vals_in, uint32_t *vals_out, int64_t n, int bits, DevBuf &radix,
+                hipStream_t st);
+template <typename K>
+void sort_pairs_v64(K *keys_in, K *keys_out, const uint64_t *vals_in, uint64_t *vals_out, int64_t n, int bits,
+                    DevBuf &ia, DevBuf &ib, DevBuf &radix, hipStream_t st);
+// *d_max = the largest of n >= 1 values (non-negative integers)
+template <typename T>
+void reduce_max(const T *in, int64_t n, T *d_max, hipStream_t st);
+// runs of equal keys (sorted input) -> (key, sum of vals) per run, *d_runs = count
+void reduce_by_key_sum(const uint64_t *keys, const int32_t *vals, int64_t n, uint64_t *ukeys, int32_t *sums,
+                       int64_t *d_runs, DevBuf &flags, DevBuf &pos, DevBuf &scan, hipStream_t st);
 void serialize_index(sme_index *ix, hipStream_t st);
 // reference-layout output from doc shards (sme_merge.hip): per-owner blobs of a
 // shard's terms and postings, and the owner's merge of the received blobs

@@ -18,7 +18,6 @@
 // per query with fp64 LDS accumulators over 4096-document tiles, k <= 32),
 // which takes batches holding a longer query.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>

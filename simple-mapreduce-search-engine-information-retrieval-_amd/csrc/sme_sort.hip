@@ -767,6 +767,104 @@ template uint32_t *kv_sort<uint64_t>(uint64_t *, uint32_t *, uint64_t *, uint32_
 template uint32_t *kv_sort<uint32_t>(uint32_t *, uint32_t *, uint32_t *, uint32_t *, int64_t, int, uint32_t *,
                                      hipStream_t, bool);
 
+namespace {
+__global__ void k_sp_iota(uint32_t *a, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    a[i] = (uint32_t)i;
+}
+__global__ void k_sp_gather64(const uint64_t *__restrict__ v, const uint32_t *__restrict__ idx, int64_t n,
+                              uint64_t *__restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = v[idx[i]];
+}
+template <typename T>
+__global__ void k_max_zero(T *m) {
+  *m = 0;
+}
+__device__ __forceinline__ void atomic_max_t(int32_t *p, int32_t v) { atomicMax(p, v); }
+__device__ __forceinline__ void atomic_max_t(int64_t *p, int64_t v) {
+  atomicMax(reinterpret_cast<unsigned long long *>(p), (unsigned long long)v);  // values are >= 0
+}
+template <typename T>
+__global__ void k_max_reduce(const T *__restrict__ in, int64_t n, T *m) {
+  T x = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x = in[i] > x ? in[i] : x;
+  for (int o = 32; o > 0; o >>= 1) {
+    const T y = __shfl_xor(x, o, 64);
+    x = y > x ? y : x;
+  }
+  if ((threadIdx.x & 63) == 0 && x > 0) atomic_max_t(m, x);
+}
+__global__ void k_run_heads(const uint64_t *__restrict__ k, int64_t n, int64_t *__restrict__ f) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x)
+    f[i] = (i < n && (i == 0 || k[i] != k[i - 1])) ? 1 : 0;
+}
+// run r = pos[i + 1] - 1 of item i (pos: exclusive scan of the head flags); sums
+// by integer atomics (order-free)
+__global__ void k_run_sums(const uint64_t *__restrict__ k, const int32_t *__restrict__ v, int64_t n,
+                           const int64_t *__restrict__ f, const int64_t *__restrict__ pos, uint64_t *__restrict__ uk,
+                           int32_t *__restrict__ sums, int64_t *d_runs) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = pos[i] + f[i] - 1;
+    if (f[i]) uk[r] = k[i];
+    atomicAdd(&sums[r], v[i]);
+    if (i == n - 1) *d_runs = r + 1;
+  }
+}
+unsigned sp_grid(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384)); }
+}  // namespace
+
+template <typename K>
+void sort_pairs(K *keys_in, K *keys_out, uint32_t *vals_in, uint32_t *vals_out, int64_t n, int bits, DevBuf &radix,
+                hipStream_t st) {
+  if (n <= 0) return;
+  uint32_t *scr = radix.as<uint32_t>(kv_sort_scratch(n) / sizeof(uint32_t) + 1);
+  if (kv_sort<K>(keys_in, vals_in, keys_out, vals_out, n, bits, scr, st, true) == vals_in) {
+    SME_HIP(hipMemcpyAsync(keys_out, keys_in, (size_t)n * sizeof(K), hipMemcpyDeviceToDevice, st));
+    SME_HIP(hipMemcpyAsync(vals_out, vals_in, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  }
+}
+template void sort_pairs<uint64_t>(uint64_t *, uint64_t *, uint32_t *, uint32_t *, int64_t, int, DevBuf &,
+                                   hipStream_t);
+template void sort_pairs<uint32_t>(uint32_t *, uint32_t *, uint32_t *, uint32_t *, int64_t, int, DevBuf &,
+                                   hipStream_t);
+template <typename K>
+void sort_pairs_v64(K *keys_in, K *keys_out, const uint64_t *vals_in, uint64_t *vals_out, int64_t n, int bits,
+                    DevBuf &ia, DevBuf &ib, DevBuf &radix, hipStream_t st) {
+  if (n <= 0) return;
+  uint32_t *a = ia.as<uint32_t>((size_t)n + 1), *b = ib.as<uint32_t>((size_t)n + 1);
+  hipLaunchKernelGGL(k_sp_iota, dim3(sp_grid(n)), dim3(256), 0, st, a, n);
+  sort_pairs<K>(keys_in, keys_out, a, b, n, bits, radix, st);
+  if (vals_in) hipLaunchKernelGGL(k_sp_gather64, dim3(sp_grid(n)), dim3(256), 0, st, vals_in, b, n, vals_out);
+  SME_CHECK_LAUNCH();
+}
+template void sort_pairs_v64<uint64_t>(uint64_t *, uint64_t *, const uint64_t *, uint64_t *, int64_t, int, DevBuf &,
+                                       DevBuf &, DevBuf &, hipStream_t);
+template void sort_pairs_v64<uint32_t>(uint32_t *, uint32_t *, const uint64_t *, uint64_t *, int64_t, int, DevBuf &,
+                                       DevBuf &, DevBuf &, hipStream_t);
+template <typename T>
+void reduce_max(const T *in, int64_t n, T *d_max, hipStream_t st) {
+  hipLaunchKernelGGL(k_max_zero<T>, dim3(1), dim3(1), 0, st, d_max);
+  if (n > 0) hipLaunchKernelGGL(k_max_reduce<T>, dim3(std::min(sp_grid(n), 2048u)), dim3(256), 0, st, in, n, d_max);
+  SME_CHECK_LAUNCH();
+}
+template void reduce_max<int32_t>(const int32_t *, int64_t, int32_t *, hipStream_t);
+template void reduce_max<int64_t>(const int64_t *, int64_t, int64_t *, hipStream_t);
+void reduce_by_key_sum(const uint64_t *keys, const int32_t *vals, int64_t n, uint64_t *ukeys, int32_t *sums,
+                       int64_t *d_runs, DevBuf &flags, DevBuf &pos, DevBuf &scan, hipStream_t st) {
+  if (n <= 0) {
+    SME_HIP(hipMemsetAsync(d_runs, 0, sizeof(int64_t), st));
+    return;
+  }
+  int64_t *f = flags.as<int64_t>((size_t)n + 1), *p = pos.as<int64_t>((size_t)n + 1);
+  hipLaunchKernelGGL(k_run_heads, dim3(sp_grid(n + 1)), dim3(256), 0, st, keys, n, f);
+  excl_scan(f, p, n + 1, scan, st);
+  SME_HIP(hipMemsetAsync(sums, 0, (size_t)n * sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_run_sums, dim3(sp_grid(n)), dim3(256), 0, st, keys, vals, n, f, p, ukeys, sums, d_runs);
+  SME_CHECK_LAUNCH();
+}
+
 template <typename T>
 void excl_scan(const T *in, T *out, int64_t n, DevBuf &scratch, hipStream_t st) {
   if (n <= 0) return;

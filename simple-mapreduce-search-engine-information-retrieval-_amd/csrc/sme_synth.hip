@@ -2,7 +2,6 @@
 // (same bytes as synth.py's host generator).  Used by bench.py
 // to put the c2 corpus (~3.3 GB) straight into HBM.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "sme_internal.hpp"
 
@@ -133,11 +132,8 @@ extern "C" int sme_synth_corpus(int device, const uint8_t *vocab, const int64_t 
     const unsigned g = (unsigned)std::min<int64_t>((n_docs + 3) / 4, 65536);
     hipLaunchKernelGGL(sme::k_syn_sizes, dim3(g), dim3(256), 0, st, s, n_docs, size);
     SME_HIP(hipMemsetAsync(size + n_docs, 0, sizeof(int64_t), st));
-    size_t tb = 0;
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, size, off, (int)n_docs + 1, st));
-    void *tmp;
-    SME_HIP(hipMalloc(&tmp, tb + 16));
-    SME_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, size, off, (int)n_docs + 1, st));
+    sme::DevBuf scan_tmp;
+    sme::excl_scan(size, off, n_docs + 1, scan_tmp, st);
     int64_t total = 0;
     SME_HIP(hipMemcpyAsync(&total, off + n_docs, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
@@ -151,7 +147,6 @@ extern "C" int sme_synth_corpus(int device, const uint8_t *vocab, const int64_t 
     (void)hipFree(dc);
     (void)hipFree(size);
     (void)hipFree(off);
-    (void)hipFree(tmp);
     (void)hipStreamDestroy(st);
     *d_corpus = out;
     *nbytes = (size_t)total;

@@ -118,6 +118,25 @@ def test_build_big_records_interleaved(sme, synth):
     _check_build(sme, b"".join(docs), ids, R=3)
 
 
+@pytest.mark.parametrize("dup", [False, True])
+def test_build_high_tf(sme, dup):
+    """A term repeated > 1023 times in a record (largest tf past the segmented
+    counting sort's LDS counters): the reduce order comes from the composite
+    (term, tf desc) radix sort; with a docid repeated across records the
+    aggregation's pairs are unpacked and equal docnos merged (the reducer's sum)."""
+    rng = random.Random(3)
+    docs, ids = [], []
+    for i in range(30):
+        did = "H%02d" % (i if not (dup and i % 10 == 9) else i - 1)
+        ids.append(did)
+        words = ["w%02d" % rng.randrange(40) for _ in range(rng.randint(5, 60))]
+        if i in (4, 21):
+            words += ["flood"] * (1500 + 700 * (i == 21)) + ["w07"] * 1100
+        docs.append(b"<DOC>\n<DOCNO>" + did.encode() + b"</DOCNO>\n" + " ".join(words).encode() + b"\n</DOC>\n")
+    ix, _ = _check_build(sme, b"".join(docs), sorted(set(ids)), R=3)
+    assert int(ix.csr()[2].max()) > 1023
+
+
 def test_build_many_tiny_records(sme):
     """Thousands of records with 0-3 words (a few pairs each, some only the
     docid): a wave's 1024 pairs of the term sort's gather pass span hundreds of
