@@ -1850,13 +1850,15 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// insert into the record's table of cap slots (a power of two <= kWCap)
-__device__ __forceinline__ bool aggw_insert(int32_t *keys, int32_t *cnt, int32_t term, uint32_t cap) {
+// insert into the record's table of cap slots (a power of two <= kWCap); the
+// counts are u16 pairs (slot h in the low / high half of word h / 2: a record
+// of < 2^16 tokens cannot carry one into the other), 6 KB of LDS per wave
+__device__ __forceinline__ bool aggw_insert(int32_t *keys, uint32_t *cnt2, int32_t term, uint32_t cap) {
   uint32_t h = hash32((uint32_t)term) & (cap - 1);
   for (uint32_t probe = 0; probe < cap; probe++) {
     const int32_t old = atomicCAS(&keys[h], -1, term);
     if (old == -1 || old == term) {
-      atomicAdd(&cnt[h], 1);
+      atomicAdd(&cnt2[h >> 1], 1u << ((h & 1u) << 4));
       return true;
     }
     h = (h + 1) & (cap - 1);
@@ -1868,9 +1870,11 @@ template <bool EMIT>
 __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t *prec, const int64_t *pair_off,
                                                   uint32_t *p_term, uint64_t *p_val) {
   __shared__ int32_t keys_all[kAggNT / 64][kWCap];
-  __shared__ int32_t cnt_all[kAggNT / 64][kWCap];
+  __shared__ uint32_t cnt_all[kAggNT / 64][kWCap / 2];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int32_t *keys = keys_all[wv], *cnt = cnt_all[wv];
+  int32_t *keys = keys_all[wv];
+  uint32_t *cnt2 = cnt_all[wv];
+  auto cnt_at = [&](uint32_t k) { return (int32_t)((cnt2[k >> 1] >> ((k & 1u) << 4)) & 0xFFFFu); };
   const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
   uint32_t wmax = 0;  // count pass / single pass: largest tf over this wave's records
   const bool fused = EMIT && in.reg_off != nullptr;
@@ -1886,10 +1890,10 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
     while (cap < kWCap && (int64_t)cap < 2 * (int64_t)nt) cap <<= 1;
     for (uint32_t k = lane; k < cap; k += 64) {
       keys[k] = -1;
-      cnt[k] = 0;
+      if (k < cap / 2) cnt2[k] = 0;
     }
     wave_sync_lds();
-    bool ok = true;
+    bool ok = nt < 65536;  // (more tokens: the big-record path, u16 counts could carry)
     // kAggU tokens per lane step: their stream loads, then their raw_term
     // gathers, are in flight together (one step was two dependent latencies)
     for (int32_t t0 = lane; t0 < nt; t0 += kAggU * 64) {
@@ -1902,10 +1906,10 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
 #pragma unroll
       for (int u = 0; u < kAggU; u++) {
         if (rt[u] >= 0) {
-          ok &= aggw_insert(keys, cnt, rt[u], cap);
+          ok &= aggw_insert(keys, cnt2, rt[u], cap);
         } else if (rt[u] <= -2) {
           const int32_t m0 = -rt[u] - 2, mn = in.raw_nout[slot[u]];
-          for (int32_t m = 0; m < mn; m++) ok &= aggw_insert(keys, cnt, in.multi_term[m0 + m], cap);
+          for (int32_t m = 0; m < mn; m++) ok &= aggw_insert(keys, cnt2, in.multi_term[m0 + m], cap);
         }
       }
     }
@@ -1917,7 +1921,7 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
       if (lane == 0) prec[i] = big ? -1 : d;
       if (!big && in.max_tf) {
 #pragma unroll 4
-        for (uint32_t k = 0; k < cap; k += 64) wmax = max(wmax, (uint32_t)cnt[k + lane]);
+        for (uint32_t k = 0; k < cap; k += 64) wmax = max(wmax, (uint32_t)cnt_at(k + lane));
       }
       wave_sync_lds();
       continue;
@@ -1934,7 +1938,7 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
       const uint64_t m = __ballot(key >= 0);
       if (key >= 0) {
         const int64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
-        const int32_t c = cnt[k + lane];
+        const int32_t c = cnt_at(k + lane);
         st_stream(p_term + o, (uint32_t)key);
         if (in.v32)
           st_stream(in.v32 + o, (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c));
