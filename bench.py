@@ -89,11 +89,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    # SME_BENCH_REHEARSE=1: the N > 1 code path rehearsed on fewer GPUs than
+    # ranks (ranks share devices round-robin, collectives over gloo) -- a check
+    # of the multi-rank bench logic, never a scaling measurement
+    rehearse = os.environ.get("SME_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     sme = importlib.import_module(PKG)
     synth = importlib.import_module(PKG + ".synth")
     L = sme.lib()
@@ -238,7 +247,8 @@ def main():
     if query is not None:
         qinternal = (query.pop("_terms"), query.pop("_qoff"), query.pop("_out"))
     if not a.no_checks:
-        result["checks"] = post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank)
+        result["checks"] = post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank,
+                                       n_global=D.global_count(ix.N) if D is not None else None)
         result["stage_ms"]["serialize_records_untimed"] = serialize_stage(ix, torch)
     cpu_full = None
     if rank == 0 and a.cpu_docs > 0 and a.config == "c2" and qinternal is not None:
@@ -418,7 +428,7 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
             "postings_touched_what": "8 B x postings of every query term (re-reads across queries included)"}
 
 
-def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank):
+def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank, n_global=None):
     """Untimed, size-independent checks of the full-size build and query batch."""
     out = {}
     off, dn, tf, df = ix.csr()
@@ -466,12 +476,14 @@ def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank):
         out["query_sample_kernels_agree"] = bool(ok)
         out["query_sample"] = nq
         # the batch's first queries against a numpy restatement of rank() over the
-        # index's own postings (tests/common.np_rank; docnos + fp64 score bits)
+        # index's own postings (tests/common.np_rank; docnos + fp64 score bits),
+        # with the N the index is weighted by (all-reduced over the ranks if N > 1)
         import common
         nr = min(100, nq)
         good = True
+        n_idf = ix.N if n_global is None else int(n_global)
         for q in range(nr):
-            rd, rs = common.np_rank(off, dn, tf, terms[qoff[q]:qoff[q + 1]].tolist(), ix.N, k)
+            rd, rs = common.np_rank(off, dn, tf, terms[qoff[q]:qoff[q + 1]].tolist(), n_idf, k)
             good = good and d1[q, :len(rd)].tolist() == rd and s1[q, :len(rd)].tolist() == rs
         out["query_sample_vs_np_rank"] = bool(good)
         out["query_sample_np_rank"] = nr
