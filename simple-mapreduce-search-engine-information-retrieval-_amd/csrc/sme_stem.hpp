@@ -75,10 +75,17 @@ __device__ __forceinline__ bool g_valid_li(uint32_t c) {  // c d e g h k m n r t
   return c >= 99 && c <= 116 && ((0x28D37u >> (c - 99)) & 1u);
 }
 
+// b points at the word: the stemmer's own array (private, i.e. scratch
+// memory, as the buffer is indexed at run time), or a caller's LDS slice
 template <int CAP>
 struct StemmerT {
-  uint16_t b[CAP];
+  uint16_t own[CAP];
+  uint16_t *b;
   int len;
+  __device__ StemmerT() : b(own) {}
+  __device__ explicit StemmerT(uint16_t *ext) : b(ext) {}
+  StemmerT(const StemmerT &) = delete;
+  StemmerT &operator=(const StemmerT &) = delete;
   int c, lim, lb, bra, ket;
   int p1, p2;
   bool y_found;
