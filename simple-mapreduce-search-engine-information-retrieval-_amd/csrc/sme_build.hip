@@ -1283,7 +1283,26 @@ struct CandOut {
   int32_t *raw_nout;
   int32_t *max_nout;
   unsigned int *err;  // bit 1: an output overran its token's pool region (cannot happen; checked)
+  unsigned int *pres; // 128-bit presence of the code units (& 127) of every output (the one-word term sort)
 };
+// a stem's code units into the lane's 128-bit presence mask
+__device__ __forceinline__ void unit_bits(const uint16_t *b, int l, uint64_t &lo, uint64_t &hi) {
+  for (int k = 0; k < l; k++) {
+    const uint32_t c = b[k] & 127u;
+    if (c < 64) lo |= 1ull << c;
+    else hi |= 1ull << (c - 64);
+  }
+}
+// one atomic per wave and mask word
+__device__ __forceinline__ void flush_unit_bits(unsigned int *pres, uint64_t lo, uint64_t hi) {
+  const unsigned int m[4] = {(unsigned int)lo, (unsigned int)(lo >> 32), (unsigned int)hi, (unsigned int)(hi >> 32)};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    unsigned int v = m[k];
+    for (int o = 32; o > 0; o >>= 1) v |= (unsigned int)__shfl_xor((int)v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicOr(&pres[k], v);
+  }
+}
 
 __device__ __forceinline__ void ovf_push(const CandOut &co, uint32_t slot, uint32_t ord, uint64_t cs) {
   unsigned long long j = atomicAdd(co.novf, 1ull);
@@ -1304,7 +1323,7 @@ __device__ __forceinline__ void vocab_finish(const CandOut &co, int64_t i, uint3
 
 // normalize + stop + stem one decoded raw token (units) of list index i
 __device__ void vocab_one(const CandOut &co, int64_t i, uint32_t slot, const uint16_t *units, int nu,
-                          uint16_t *work, int work_cap) {
+                          uint16_t *work, int work_cap, uint64_t &plo, uint64_t &phi) {
   uint32_t ord = 0;
   uint64_t used = 0;
   Stemmer st;
@@ -1313,6 +1332,7 @@ __device__ void vocab_one(const CandOut &co, int64_t i, uint32_t slot, const uin
     for (int k = 0; k < l; k++) st.b[k] = p[k];
     st.len = l;
     st.run();
+    unit_bits(st.b, st.len, plo, phi);
     const uint64_t po = (uint64_t)co.poff[i] + used;
     if (po + (uint64_t)st.len > (uint64_t)co.poff[i + 1]) {
       atomicOr(co.err, 1u);
@@ -1333,7 +1353,7 @@ __device__ void vocab_one(const CandOut &co, int64_t i, uint32_t slot, const uin
 // Fast path for the common raw token: only [a-z0-9] (checkTokenStatus == Clean), so
 // normalization is the identity and the token goes straight to stop list + stemmer.
 __device__ bool vocab_clean(const CandOut &co, int64_t i, uint32_t slot, const uint8_t *p, uint64_t len,
-                            uint16_t *lds_buf) {
+                            uint16_t *lds_buf, uint64_t &plo, uint64_t &phi) {
   if (len > 48) return false;
   StemmerT<64> st(lds_buf);  // the word in the lane's LDS slice (a scratch array was the kernel's bottleneck)
   for (uint64_t k = 0; k < len; k++) {
@@ -1345,6 +1365,7 @@ __device__ bool vocab_clean(const CandOut &co, int64_t i, uint32_t slot, const u
   if (!is_stopword(st.b, (int)len)) {  // <= 48 ASCII bytes: addToken's >= 100-byte rule cannot apply
     st.len = (int)len;
     st.run();
+    unit_bits(st.b, st.len, plo, phi);
     const uint64_t po = (uint64_t)co.poff[i];
     for (int k = 0; k < st.len; k++) co.pool[po + k] = st.b[k];
     co.cand_str[i] = (po << 16) | (uint64_t)st.len;
@@ -1373,11 +1394,12 @@ constexpr int kVocabNT = 256;
 __global__ __launch_bounds__(kVocabNT, 4) void k_vocab(const RawTable tb, const int32_t *rlist, int64_t nraw, CandOut co,
                                                    int64_t *long_list, unsigned long long *nlong, uint64_t long_cap) {
   __shared__ uint16_t sbuf[kVocabNT][66];  // 64 units + 2 of padding: lanes' slices start on different banks
+  uint64_t plo = 0, phi = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nraw; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t slot = (uint32_t)rlist[i];
     uint64_t r = tb.rep[slot];
     uint64_t off = r >> 24, len = r & 0xFFFFFFull;
-    if (vocab_clean(co, i, slot, tb.text + off, len, sbuf[threadIdx.x])) continue;
+    if (vocab_clean(co, i, slot, tb.text + off, len, sbuf[threadIdx.x], plo, phi)) continue;
     if (len > kShortRaw) {
       unsigned long long j = atomicAdd(nlong, 1ull);
       if (j < long_cap) long_list[j] = i;
@@ -1393,12 +1415,14 @@ __global__ __launch_bounds__(kVocabNT, 4) void k_vocab(const RawTable tb, const 
       for (int x = 0; x < k; x++) units[nu++] = tmp[x];
       p += used;
     }
-    vocab_one(co, i, slot, units, nu, work, 4 * kShortRaw + 16);
+    vocab_one(co, i, slot, units, nu, work, 4 * kShortRaw + 16, plo, phi);
   }
+  flush_unit_bits(co.pres, plo, phi);
 }
 
 __global__ void k_vocab_long(const RawTable tb, const int32_t *rlist, CandOut co, const int64_t *long_list,
                              int64_t nlong, const int64_t *scr_off, uint16_t *scr) {
+  uint64_t plo = 0, phi = 0;
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < nlong; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = long_list[j];
     const uint32_t slot = (uint32_t)rlist[i];
@@ -1414,8 +1438,9 @@ __global__ void k_vocab_long(const RawTable tb, const int32_t *rlist, CandOut co
       p += used;
     }
     uint16_t *work = units + len + 8;
-    vocab_one(co, i, slot, units, nu, work, (int)(4 * len + 16));
+    vocab_one(co, i, slot, units, nu, work, (int)(4 * len + 16), plo, phi);
   }
+  flush_unit_bits(co.pres, plo, phi);
 }
 
 // final-term dedup table over pool strings
@@ -1611,30 +1636,6 @@ __global__ void k_final_fixup(uint32_t *order, int64_t V, const uint32_t *vslot,
 // ASCII vocabularies: the code units in use (128-bit presence map), so a sort
 // key packs ceil(log2(units + 1)) bits per unit (6 for letters and digits: 10
 // units per 64-bit word instead of 9 x 7 bits)
-__global__ void k_unit_presence(int64_t V, const uint64_t *vcs, const uint16_t *pool, unsigned int *pres) {
-  __shared__ unsigned int sp[4];
-  if (threadIdx.x < 4) sp[threadIdx.x] = 0;
-  __syncthreads();
-  // (two 64-bit masks, not a 4-word array indexed by the unit: a register
-  // array indexed at run time lives in scratch memory)
-  uint64_t lo = 0, hi = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t cs = vcs[i];
-    const uint16_t *u = pool + (cs >> 16);
-    const int l = (int)(cs & 0xFFFF);
-    for (int j = 0; j < l; j++) {
-      const uint32_t c = u[j] & 127u;
-      if (c < 64) lo |= 1ull << c;
-      else hi |= 1ull << (c - 64);
-    }
-  }
-  const unsigned int m[4] = {(unsigned int)lo, (unsigned int)(lo >> 32), (unsigned int)hi, (unsigned int)(hi >> 32)};
-#pragma unroll
-  for (int k = 0; k < 4; k++)
-    if (m[k]) atomicOr(&sp[k], m[k]);
-  __syncthreads();
-  if (threadIdx.x < 4 && sp[threadIdx.x]) atomicOr(&pres[threadIdx.x], sp[threadIdx.x]);
-}
 // key of term order[i]: its first cpw units as codes (code[u] = rank of u among
 // the units in use + 1; 0 pads), most significant first -- String.compareTo
 // order of the first cpw units
@@ -3075,6 +3076,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   int32_t *max_nout = W[W_MAXNOUT].as<int32_t>(4);  // must survive the counter resets below
   co.max_nout = max_nout;
   co.err = ovf;
+  co.pres = reinterpret_cast<unsigned int *>(cnt + 28);  // read by the one-word term sort below
+  SME_HIP(hipMemsetAsync(co.pres, 0, 4 * sizeof(unsigned int), st));
   int64_t *long_list = nullptr;
   uint64_t long_cap = std::max<uint64_t>(cx->vocab_long_cap, 4096);
   uint64_t ovf_cap = std::max<uint64_t>(cx->vocab_ovf_cap, 4096);
@@ -3177,9 +3180,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       // then the short runs of terms sharing those units ordered by the whole
       // string (c2: 6 radix passes instead of 12); runs over 64 terms: the full
       // word-by-word sort below
-      unsigned int *pres = reinterpret_cast<unsigned int *>(cnt + 28);
-      SME_HIP(hipMemsetAsync(pres, 0, 4 * sizeof(unsigned int), st));
-      hipLaunchKernelGGL(k_unit_presence, dim3(grid_for(V, 256, 2048)), dim3(256), 0, st, V, vcs, co.pool, pres);
+      // the units in use: collected by the vocabulary kernels from every stem
+      unsigned int *pres = co.pres;
       unsigned int hp[4];
       SME_HIP(hipMemcpyAsync(hp, pres, sizeof hp, hipMemcpyDeviceToHost, st));
       SME_HIP(hipStreamSynchronize(st));
