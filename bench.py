@@ -411,7 +411,7 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
             "terms_per_query": "U{2..8} drawn by df (seed %d)" % a.cfg["qseed"], "ms_per_batch": round(dt * 1e3, 3),
             "prep_ms": qp_ms, "query_index_build_ms": round(qidx_ms, 3),
             "query_index_what": "once per index, not per batch: tf byte rows + 16/1024-doc block maxima of the "
-                                "terms with df >= span/64 (sme_index_prepare_queries)",
+                                "terms with df >= span/128 (sme_index_prepare_queries)",
             "_terms": terms, "_qoff": qoff, "_out": (out_d, out_s),
             "prep_what": "per batch, inside ms_per_batch: skip table (distinct batch terms x 1024-doc tiles), "
                          "impact tables of the batch terms, heaviest-term query order",
@@ -470,7 +470,7 @@ def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank, n_global=None):
                     ix.ctx.set_option(n, v)
                 d2, s2 = ix.query_topk(t_s, q_s, k)
             finally:
-                ix.ctx.set_option("heavy_div", 64)
+                ix.ctx.set_option("heavy_div", 128)
                 ix.ctx.set_option("query_kernel", 0)
             ok = ok and np.array_equal(d1, d2) and np.array_equal(s1, s2)
         out["query_sample_kernels_agree"] = bool(ok)

@@ -89,7 +89,7 @@ void sme_destroy(sme_ctx *ctx);
  * tests can hold each device path to the others and benches can sweep them.
  *   "query_kernel"  0 window-major scoring with seeded thresholds (default), 1 streaming
  *                   k_query (k <= 32), 2 per-query block-max sweep k_query_bm
- *   "heavy_div"     heavy tf / impact rows for terms with df >= docno span / div (default 64; 0 none)
+ *   "heavy_div"     heavy tf / impact rows for terms with df >= docno span / div (default 128; 0 none)
  *   "seed_m"        seed postings per term for the window path's threshold, 0..4096 (default 64)
  *   "cand_cap"      candidate list per query of the window path, 1..2048 (default 1024; >= 1024:
  *                   at least 16 k)

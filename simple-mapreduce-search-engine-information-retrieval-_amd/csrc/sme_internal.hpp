@@ -41,7 +41,7 @@ struct sme_ctx {
   // Path options (sme_set_option).  Every setting gives identical results; they
   // exist so tests can hold each path to the others and benches can sweep them.
   int64_t opt_query_kernel = 0;   // "query_kernel": 0 window-major (auto), 1 streaming k_query, 2 block-max sweep
-  int64_t opt_heavy_div = 64;     // "heavy_div": heavy rows for terms with df >= span / div (0: none)
+  int64_t opt_heavy_div = 128;    // "heavy_div": heavy rows for terms with df >= span / div (0: none)
   int64_t opt_seed_tiles = 4;     // "seed_tiles": best-bound tiles scored before the sweep (0..8)
   int64_t opt_query_order = 1;    // "query_order": 1 heaviest-term query order, 0 batch order
   int64_t opt_agg_two_pass = 0;   // "agg_two_pass": 1 = count + emit aggregation passes

@@ -199,7 +199,7 @@ def test_queries_vs_oracle(sme, synth, idf_mode):
 
 def _query_opts(ix, terms, qoff, k, **opts):
     """Query with context path options set (sme_set_option), then restore the defaults."""
-    defaults = {"query_kernel": 0, "heavy_div": 64, "seed_tiles": 4, "query_order": 1, "cand_cap": 1024,
+    defaults = {"query_kernel": 0, "heavy_div": 128, "seed_tiles": 4, "query_order": 1, "cand_cap": 1024,
                 "seed_m": 64, "win_sample": 1}
     try:
         for n, v in opts.items():

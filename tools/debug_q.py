@@ -33,4 +33,4 @@ for opts in ({}, {"heavy_div": 0}, {"heavy_div": 1 << 30}, {"seed_m": 0}, {"quer
         print("  q", q, "terms", terms[qoff[q]:qoff[q + 1]].tolist(), "df", [int(df[t]) for t in terms[qoff[q]:qoff[q + 1]] if t >= 0])
         print("  got", dn[q].tolist(), "\n  exp", exp[q])
     for kk in opts:
-        ctx.set_option(kk, {"heavy_div": 64, "seed_m": 64, "query_kernel": 0, "cand_cap": 1024}[kk])
+        ctx.set_option(kk, {"heavy_div": 128, "seed_m": 64, "query_kernel": 0, "cand_cap": 1024}[kk])

@@ -85,7 +85,7 @@ def main():
                           "split": {x: prof.get(x) for x in ("query_seed", "query_final", "query_overflow",
                                                              "query_total") if x in prof}}), flush=True)
         for n in opts:  # restore defaults
-            ctx.set_option(n.strip(), {"heavy_div": 64, "seed_tiles": 4, "query_order": 1, "query_kernel": 0,
+            ctx.set_option(n.strip(), {"heavy_div": 128, "seed_tiles": 4, "query_order": 1, "query_kernel": 0,
                                        "cand_cap": 1024, "seed_m": 64, "win_slice": 256, "win_sample": 1}[n.strip()])
     ix.close()
     ctx.close()
