@@ -1217,13 +1217,47 @@ __global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
       v[u] = hk[i] != INT32_MIN ? __longlong_as_double((long long)hs[i]) : -1.0;
     }
     __syncthreads();
+    double th = -1.0;
+    int nused = 0;
+#pragma unroll
+    for (int u = 0; u < kSeedSlots / 64; u++) nused += __popcll((uint64_t)__ballot(v[u] >= 0.0));
+    if (a.k <= 32 && nused >= a.k) {
+      // small k: the k-th largest by k rounds of wave max + removal of one
+      // instance (duplicates count, as in the sorted list), all in registers
+      for (int r = 0; r < a.k; r++) {
+        double m = v[0];
+#pragma unroll
+        for (int u = 1; u < kSeedSlots / 64; u++) m = v[u] > m ? v[u] : m;
+        double M = m;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const double y = __shfl_xor(M, o, 64);
+          M = y > M ? y : M;
+        }
+        const uint64_t has = (uint64_t)__ballot(m == M);
+        if (lane == (int)__builtin_ctzll(has)) {
+          bool done = false;
+#pragma unroll
+          for (int u = 0; u < kSeedSlots / 64; u++)
+            if (!done && v[u] == M) {
+              v[u] = -2.0;
+              done = true;
+            }
+        }
+        th = M;
+      }
+      if (lane == 0) {
+        a.th0[q] = th;
+        a.thk[q] = kNoKey;
+      }
+      continue;  // (no LDS use after the last barrier: the next query's clear follows a barrier)
+    }
     double *ss = reinterpret_cast<double *>(hs);
 #pragma unroll
     for (int u = 0; u < kSeedSlots / 64; u++)
       if (v[u] >= 0.0) ss[atomicAdd(&s_n, 1)] = v[u];
     __syncthreads();
     const int n = s_n;
-    double th = -1.0;
     if (n >= a.k) {
       int n2 = 2;
       while (n2 < n) n2 <<= 1;
