@@ -1034,28 +1034,20 @@ static_assert(sizeof(QDesc) == 32 && sizeof(QPos) == 16, "record sizes");
 // Window-granular skip table of the k_query_win path, built directly (no tile
 // table, no transpose): skt[w * nrows + row] = first posting (term-relative) of
 // the row's term in window w or later; skt[nwin * nrows + row] = df.  Change
-// points as in k_skip_fill, then a suffix minimum per row over the windows.
-__global__ __launch_bounds__(256) void k_skipw_fill(const int64_t *rpre, int64_t nrows, const int32_t *term_of_row,
-                                                    const int64_t *off, const int32_t *docno, int64_t dmin,
-                                                    int64_t nwin, int32_t *skt) {
-  const int64_t total = rpre[nrows];
-  for (int64_t x0 = (int64_t)blockIdx.x * kSkipChunk; x0 < total; x0 += (int64_t)gridDim.x * kSkipChunk) {
-    const int64_t x1 = x0 + kSkipChunk < total ? x0 + kSkipChunk : total;
-    int64_t lo = 0, hi = nrows;  // row of x0: rpre[lo] <= x0 < rpre[hi]
-    while (hi - lo > 1) {
-      const int64_t m = (lo + hi) >> 1;
-      if (rpre[m] <= x0) lo = m;
-      else hi = m;
-    }
-    int64_t row = lo, rb = rpre[row], re = rpre[row + 1], b = off[term_of_row[row]];
-    for (int64_t x = x0 + threadIdx.x; x < x1; x += blockDim.x) {
-      while (x >= re) {
-        row++;
-        rb = re;
-        re = rpre[row + 1];
-        b = off[term_of_row[row]];
-      }
-      const int64_t i = x - rb, n = re - rb;
+// points (k_skipw_fill_rows), then a suffix minimum per row over the windows.
+// The same change points with one wave per row (lanes stride over the row's
+// postings): a chunk walk over a batch's many short sparse rows made every
+// thread advance row by row through dependent offset loads (0.84 ms per c2 batch)
+__global__ __launch_bounds__(256) void k_skipw_fill_rows(const int64_t *rdf, int64_t nrows, const int32_t *term_of_row,
+                                                         const int64_t *off, const int32_t *docno, int64_t dmin,
+                                                         int64_t nwin, int32_t *skt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < nrows; row += nw) {
+    const int64_t n = rdf[row];
+    if (n == 0) continue;  // (wave-uniform) heavy rows and absent terms
+    const int64_t b = off[term_of_row[row]];
+    for (int64_t i = lane; i < n; i += 64) {
       const int64_t j = ((int64_t)docno[b + i] - dmin) >> kWinB;
       const int64_t jp = i == 0 ? -1 : (((int64_t)docno[b + i - 1] - dmin) >> kWinB);
       if (jp < j) skt[j * nrows + row] = (int32_t)i;
@@ -2077,8 +2069,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
                                  0, st, tor, rdf, hro, nrows, rdfw);
               excl_scan(rdfw, rprew, nrows + 1, cx->ws[23], st);
             }
-            hipLaunchKernelGGL(k_skipw_fill, dim3(16384), dim3(256), 0, st, rprew, nrows, tor, off, dn, ix->dmin, nwin,
-                               skt);
+            hipLaunchKernelGGL(k_skipw_fill_rows, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 65536)),
+                               dim3(256), 0, st, rdfw, nrows, tor, off, dn, ix->dmin, nwin, skt);
             hipLaunchKernelGGL(k_skipw_suffix, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 16384)),
                                dim3(256), 0, st, rdfw, nrows, nwin, skt);
           } else {
