@@ -2061,13 +2061,11 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
             // only the sparse rows: k_query_win reads heavy terms from their impact
             // rows, never their skip entries (and heavy terms hold most postings)
             const int32_t *hro = ix->q_H > 0 ? (const int32_t *)ix->d_hrow_of.p : nullptr;
-            int64_t *rdfw = rdf, *rprew = rpre;
+            int64_t *rdfw = rdf;
             if (hro) {
               rdfw = W[12].as<int64_t>(nrows + 1);
-              rprew = W[13].as<int64_t>(nrows + 1);
               hipLaunchKernelGGL(k_sparse_rdf, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 16384)), dim3(256),
                                  0, st, tor, rdf, hro, nrows, rdfw);
-              excl_scan(rdfw, rprew, nrows + 1, cx->ws[23], st);
             }
             hipLaunchKernelGGL(k_skipw_fill_rows, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 65536)),
                                dim3(256), 0, st, rdfw, nrows, tor, off, dn, ix->dmin, nwin, skt);
