@@ -2867,10 +2867,13 @@ RecordSpans find_records(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t 
   if (nS > 0) {
     hipLaunchKernelGGL(k_chain, dim3(grid_for(nS)), dim3(256), 0, st, S, nS, E, nE, e_of, next_s, cnt);
     SME_CHECK_LAUNCH();
-    unsigned long long bad = d2h(cnt, st);
+    unsigned long long hc[3];  // bad, (walk count), records with an end tag: one read
+    SME_HIP(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    const unsigned long long bad = hc[0];
     if (bad == 0) {
       // records are the prefix of S with an end tag (e_of is monotone)
-      nR = (int64_t)d2h(cnt + 2, st);
+      nR = (int64_t)hc[2];
       if (nR > 0)
         hipLaunchKernelGGL(k_records_direct, dim3(grid_for(nR)), dim3(256), 0, st, S, E, e_of, nR, rs, re);
     } else {
@@ -2929,15 +2932,24 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     hipLaunchKernelGGL(k_iota_docno, dim3(grid_for(nR)), dim3(256), 0, st, docno, nR);
   }
   uint8_t *slow = W[W_SLOW].as<uint8_t>(nR + 1);
+  // fast-path records (ascending), for the stream tokenizer
+  int32_t *frec = W[W_FREC].as<int32_t>(nR + 1);
   if (nR > 0) {
     hipLaunchKernelGGL(k_mark_slow, dim3(grid_for(nR)), dim3(256), 0, st, rs, re, nR, C, nC, slow, cnt + 1);
+    // (queued before the one host read below: the docno order test and the
+    // fast-record list need nothing from the host)
+    hipLaunchKernelGGL(k_not_ascending, dim3(grid_for(nR)), dim3(256), 0, st, docno, nR, cnt + 3);
+    uint8_t *fflag = W[W_RFLAG].as<uint8_t>(nR);
+    hipLaunchKernelGGL(k_not_flags, dim3(grid_for(nR)), dim3(256), 0, st, slow, nR, fflag);
+    select_flagged(fflag, nR, frec, reinterpret_cast<int32_t *>(cnt + 14), cx->ws[25], cx->ws[23], st);
     SME_CHECK_LAUNCH();
   }
-  unsigned long long h2[2];
+  unsigned long long h2[16];  // [0] docid errors, [1] slow records, [3] docno descents, [14] fast records
   SME_HIP(hipMemcpyAsync(h2, cnt, sizeof h2, hipMemcpyDeviceToHost, st));
   SME_HIP(hipStreamSynchronize(st));
   if (h2[0]) throw Error(SME_EPARSE, "a record has <DOCNO> but no </DOCNO> (TrecDocument.getDocid throws)");
   const int64_t nslow = (int64_t)h2[1];
+  const int64_t nF = nR > 0 ? (int64_t)(int32_t)(uint32_t)h2[14] : 0;
   prof.mark("docno");
 
   // records in docno order (stable) -> perm; duplicate docnos?
@@ -2948,9 +2960,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   // duplicates, no sort
   bool ascending = false;
   if (nR > 0) {
-    SME_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_not_ascending, dim3(grid_for(nR)), dim3(256), 0, st, docno, nR, cnt);
-    ascending = d2h(cnt, st) == 0;
+    ascending = h2[3] == 0;
     if (ascending) hipLaunchKernelGGL(k_iota_i64, dim3(grid_for(nR)), dim3(256), 0, st, perm, nR);
   }
   if (nR > 0 && !ascending) {
@@ -2978,16 +2988,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   int32_t *ntok = W[W_NTOK].as<int32_t>(nR + 1);
   RawTable tb;
   unsigned int *ovf = reinterpret_cast<unsigned int *>(cnt + 8);
-  // fast-path records (ascending), for the stream tokenizer
-  int32_t *frec = W[W_FREC].as<int32_t>(nR + 1);
-  int64_t nF = 0;
-  if (nR > 0) {
-    uint8_t *fflag = W[W_RFLAG].as<uint8_t>(nR);
-    hipLaunchKernelGGL(k_not_flags, dim3(grid_for(nR)), dim3(256), 0, st, slow, nR, fflag);
-    int32_t *d_nf = reinterpret_cast<int32_t *>(cnt + 14);
-    select_flagged(fflag, nR, frec, d_nf, cx->ws[25], cx->ws[23], st);
-    nF = d2h(d_nf, st);
-  }
+  int64_t h_nsel = 0;  // distinct raw tokens (read with the overflow flags)
+
   for (int attempt = 0;; attempt++) {
     {
       uint8_t *rb = W[W_RKEYS].as<uint8_t>(rcap * kRawSlotBytes);
@@ -3038,7 +3040,17 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
                          u16s, boffs, tok, ntok, tb);
       SME_CHECK_LAUNCH();
     }
-    unsigned int of = d2h(ovf, st);
+    // the distinct raw tokens' list is queued before the one host read of the
+    // overflow flags and its length (an overflowing attempt discards it)
+    hipLaunchKernelGGL(k_raw_flags, dim3(grid_for((int64_t)rcap)), dim3(256), 0, st, tb.key, rcap,
+                       W[W_RFLAG].as<uint8_t>(rcap));
+    select_flagged(W[W_RFLAG].as<uint8_t>(rcap), (int64_t)rcap, W[W_RLIST].as<int32_t>(rcap),
+                   reinterpret_cast<int32_t *>(cnt + 13), cx->ws[25], cx->ws[23], st);
+    unsigned long long hov[6];  // cnt[8..13]: overflow flags (low word of [8]), ..., distinct count ([13])
+    SME_HIP(hipMemcpyAsync(hov, cnt + 8, sizeof hov, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    const unsigned int of = (unsigned int)hov[0];
+    h_nsel = (int64_t)(int32_t)(uint32_t)hov[5];
     if (of == 0) break;
     if (of & 2u) throw Error(SME_ELIMIT, "a raw token is longer than 16 MiB");
     if (attempt > 3 || rcap >= (1ull << 32)) throw Error(SME_ELIMIT, "raw vocabulary table overflow");
@@ -3048,12 +3060,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
 
   // ---------------- K4 vocabulary ----------------
   // distinct raw tokens -> rlist (ascending slot order)
-  uint8_t *rflag = W[W_RFLAG].as<uint8_t>(rcap);
   int32_t *rlist = W[W_RLIST].as<int32_t>(rcap);
-  int32_t *d_nsel = reinterpret_cast<int32_t *>(cnt + 13);
-  hipLaunchKernelGGL(k_raw_flags, dim3(grid_for((int64_t)rcap)), dim3(256), 0, st, tb.key, rcap, rflag);
-  select_flagged(rflag, (int64_t)rcap, rlist, d_nsel, cx->ws[25], cx->ws[23], st);
-  const int64_t nraw = d2h(d_nsel, st);
+  const int64_t nraw = h_nsel;
   // next build's raw table: load <= 40 % (fewer probe collisions: c2 tokenizes in 9.2 ms at 8 M
   // slots vs 10.0 ms at 4 M; option raw_load_pct)
   {
