@@ -314,22 +314,53 @@ __device__ __forceinline__ int64_t lower_bound_u64(const uint64_t *a, int64_t n,
 }
 
 // next pointers of the start/end alternation (XMLRecordReader.next)
-__global__ void k_chain(const uint64_t *S, int64_t nS, const uint64_t *E, int64_t nE, int64_t *e_of,
-                        int64_t *next_s, unsigned long long *bad) {
+__global__ __launch_bounds__(256) void k_chain(const uint64_t *S, int64_t nS, const uint64_t *E, int64_t nE,
+                                               int64_t *e_of, int64_t *next_s, unsigned long long *bad) {
+  // the two counts: per thread over its records, then one atomic per block (even
+  // one atomic per wave on one address serialised: 137 k of them took 1.7 ms on c5)
+  unsigned long long n_end = 0, n_broken = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nS; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t e = lower_bound_u64(E, nE, S[i] + 5);
-    if (e >= nE) {
+    // well-formed input alternates start and end tags: end tag i and start tag
+    // i + 1 are the answers whenever the neighbours confirm them (two binary
+    // searches of 23 dependent steps each per record otherwise: 1.7 ms on c5)
+    const uint64_t si = S[i];
+    int64_t e;
+    if (i < nE && E[i] >= si + 5 && (i == 0 || E[i - 1] < si + 5)) e = i;
+    else e = lower_bound_u64(E, nE, si + 5);
+    const bool has_end = e < nE;
+    bool broken = false;
+    if (!has_end) {
       e_of[i] = -1;
       next_s[i] = nS;
-      continue;
+    } else {
+      e_of[i] = e;
+      const uint64_t ve = E[e] + 6;
+      int64_t ns;
+      if (i + 1 >= nS || S[i + 1] >= ve) ns = i + 1;  // S[i] < ve always (E[e] >= S[i] + 5)
+      else ns = lower_bound_u64(S, nS, ve);
+      next_s[i] = ns;
+      // a start tag inside record i (nested <DOC>) or past the last end tag breaks
+      // "records = the start tags that have an end tag": walk the chain instead
+      broken = ns != i + 1 && i + 1 < nS;
     }
-    e_of[i] = e;
-    atomicAdd(bad + 2, 1ull);
-    int64_t ns = lower_bound_u64(S, nS, E[e] + 6);
-    next_s[i] = ns;
-    // a start tag inside record i (nested <DOC>) or past the last end tag breaks
-    // "records = the start tags that have an end tag": walk the chain instead
-    if (ns != i + 1 && i + 1 < nS) atomicAdd(bad, 1ull);
+    n_end += has_end ? 1ull : 0ull;
+    n_broken += broken ? 1ull : 0ull;
+  }
+  __shared__ unsigned long long s_c[2];
+  if (threadIdx.x < 2) s_c[threadIdx.x] = 0;
+  __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) {
+    n_end += __shfl_xor(n_end, o, 64);
+    n_broken += __shfl_xor(n_broken, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (n_end) atomicAdd(&s_c[0], n_end);
+    if (n_broken) atomicAdd(&s_c[1], n_broken);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_c[0]) atomicAdd(bad + 2, s_c[0]);
+    if (s_c[1]) atomicAdd(bad, s_c[1]);
   }
 }
 
