@@ -1670,14 +1670,29 @@ __global__ void k_final_fixup(uint32_t *order, int64_t V, const uint32_t *vslot,
 // key of term order[i]: its first cpw units as codes (code[u] = rank of u among
 // the units in use + 1; 0 pads), most significant first -- String.compareTo
 // order of the first cpw units
-__global__ void k_term_code(const uint32_t *order, int64_t V, const uint64_t *vcs, const uint16_t *pool,
-                            const uint8_t *code, int cpw, int ub, uint64_t *key) {
+// (the units are loaded eight at a time, all in flight together, and coded from an
+// LDS copy of the table: a unit-by-unit loop waited on each load in turn)
+__global__ __launch_bounds__(256) void k_term_code(const uint32_t *__restrict__ order, int64_t V,
+                                                   const uint64_t *__restrict__ vcs,
+                                                   const uint16_t *__restrict__ pool,
+                                                   const uint8_t *__restrict__ code, int cpw, int ub,
+                                                   uint64_t *__restrict__ key) {
+  __shared__ uint8_t s_code[128];
+  if (threadIdx.x < 128) s_code[threadIdx.x] = code[threadIdx.x];
+  __syncthreads();
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t cs = vcs[order[i]];
     const uint16_t *u = pool + (cs >> 16);
-    const int l = (int)(cs & 0xFFFF);
+    const int l = min((int)(cs & 0xFFFF), cpw);
     uint64_t k = 0;
-    for (int j = 0; j < cpw; j++) k = (k << ub) | (j < l ? code[u[j] & 127] : 0u);
+    for (int j0 = 0; j0 < cpw; j0 += 8) {
+      uint16_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = j0 + j < l ? u[j0 + j] : (uint16_t)0;
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        if (j0 + j < cpw) k = (k << ub) | (j0 + j < l ? s_code[v[j] & 127] : 0u);
+    }
     key[i] = k;
   }
 }
@@ -1719,13 +1734,26 @@ __global__ void k_final_rank(const uint32_t *order, int64_t V, const uint32_t *v
   }
 }
 
-__global__ void k_final_gather(const uint32_t *order, int64_t V, const uint64_t *vcs, const uint16_t *pool,
-                               const int64_t *term_off, uint16_t *term_chars) {
+// (eight units loaded together before they are stored: with possibly aliasing
+// pointers a unit-by-unit copy waited on each load in turn)
+__global__ __launch_bounds__(256) void k_final_gather(const uint32_t *__restrict__ order, int64_t V,
+                                                      const uint64_t *__restrict__ vcs,
+                                                      const uint16_t *__restrict__ pool,
+                                                      const int64_t *__restrict__ term_off,
+                                                      uint16_t *__restrict__ term_chars) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t cs = vcs[order[i]];
+    const uint64_t cs = vcs[order[i]];
     const uint16_t *w = pool + (cs >> 16);
-    int l = (int)(cs & 0xFFFF);
-    for (int k = 0; k < l; k++) term_chars[term_off[i] + k] = w[k];
+    const int l = (int)(cs & 0xFFFF);
+    uint16_t *d = term_chars + term_off[i];
+    for (int k0 = 0; k0 < l; k0 += 8) {
+      uint16_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[k] = k0 + k < l ? w[k0 + k] : (uint16_t)0;
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (k0 + k < l) d[k0 + k] = v[k];
+    }
   }
 }
 
