@@ -88,7 +88,7 @@ void sme_destroy(sme_ctx *ctx);
  * code path).  Every value gives bit-identical results; the options exist so
  * tests can hold each device path to the others and benches can sweep them.
  *   "query_kernel"  0 window-major scoring with seeded thresholds (default), 1 streaming
- *                   k_query (k <= 32), 2 per-query block-max sweep k_query_bm
+ *                   k_query, 2 per-query block-max sweep k_query_bm
  *   "heavy_div"     heavy tf / impact rows for terms with df >= docno span / div (default 128; 0 none)
  *   "seed_m"        seed postings per term for the window path's threshold, 0..4096 (default 64)
  *   "cand_cap"      candidate list per query of the window path, 1..2048 (default 1024; >= 1024:
@@ -220,7 +220,7 @@ int sme_lookup_terms(sme_index *ix, const uint8_t *terms, const int64_t *offs, i
 /* Batched rank(): query q has term ids term_ids[q_offsets[q] .. q_offsets[q+1])
  * in query-token order (duplicates count twice, -1 entries are skipped; an id
  * outside [-1, V) is SME_EINVAL here and skipped like -1 by the device entry).
- * k <= 448 (queries of more than 64 terms: k <= 32).
+ * k <= 448 (SME_ELIMIT above); queries of 65-128 terms take the streaming kernel.
  * Writes k docnos / scores per query (score desc, docno asc), padded with
  * docno -1 / score 0 when fewer than k documents match. */
 int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq,

@@ -15,8 +15,9 @@
 //
 // Two kernels: k_query_imp (tiled, impact-gated; queries of <= 64 terms, any
 // k <= 448), described below, and k_query (streaming; one 256-lane workgroup
-// per query with fp64 LDS accumulators over 4096-document tiles, k <= 32),
-// which takes batches holding a longer query.
+// per query with fp64 LDS accumulators over 4096-document tiles; per-lane
+// register lists for k <= 32, one LDS candidate list per workgroup above), which
+// takes batches holding a longer query.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -143,7 +144,41 @@ __device__ __forceinline__ void emit_topk(double (&ts)[KMAX], uint64_t (&td)[KMA
   }
 }
 
-template <int KMAX>
+// k > 32 on the streaming kernel: one candidate list per workgroup in LDS instead
+// of per-lane register lists. A tile's documents join it when they beat the
+// list's k-th best (score, key) so far; when the next kQNT might not fit, the
+// list is sorted (bitonic, best first) and cut to its k best, whose last entry
+// becomes the entry bar. Exact: a document below the k-th best of a subset
+// cannot be in the top k.
+constexpr int kListCap = 2048;
+
+// bitonic sort of l_s / l_k [0, kListCap), best first; entries >= n padded (all threads)
+__device__ void list_sort(double *l_s, uint64_t *l_k, int n) {
+  const int tid = threadIdx.x;
+  for (int i = n + tid; i < kListCap; i += kQNT) {
+    l_s[i] = -INFINITY;
+    l_k[i] = kNoKey;
+  }
+  __syncthreads();
+  for (int size = 2; size <= kListCap; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < kListCap / 2; t += kQNT) {
+        const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+        const double a = l_s[i], b = l_s[j];
+        const uint64_t ka = l_k[i], kb = l_k[j];
+        const bool swap = (i & size) == 0 ? better(b, kb, a, ka) : better(a, ka, b, kb);
+        if (swap) {
+          l_s[i] = b;
+          l_s[j] = a;
+          l_k[i] = kb;
+          l_k[j] = ka;
+        }
+      }
+      __syncthreads();
+    }
+}
+
+template <int KMAX, bool LIST>
 __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off, const int32_t *__restrict__ docno,
                                                 const int32_t *__restrict__ tf, const double *__restrict__ lut,
                                                 int max_tf, const double *__restrict__ idf, int64_t V,
@@ -160,6 +195,11 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
   __shared__ double red_s[kQNT / 64];
   __shared__ uint64_t red_d[kQNT / 64];
   __shared__ int32_t red_t[kQNT / 64];
+  __shared__ double l_s[LIST ? kListCap : 1];  // LIST: the candidate list
+  __shared__ uint64_t l_k[LIST ? kListCap : 1];
+  __shared__ int l_n;
+  __shared__ double l_ths;
+  __shared__ uint64_t l_thk;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   for (int j = tid; j < kTile; j += kQNT) acc[j] = -1.0;  // untouched (weights are >= 0)
   for (int j = tid; j < kLutLds; j += kQNT) s_lut[j] = j <= max_tf ? lut[j] : 0.0;
@@ -170,7 +210,12 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
       if (tid == 0) atomicOr(err, 1);
       nt = kMaxQTerms;
     }
-    if (tid == 0) s_next = 0x7FFFFFFF;
+    if (tid == 0) {
+      s_next = 0x7FFFFFFF;
+      l_n = 0;
+      l_ths = -INFINITY;
+      l_thk = kNoKey;
+    }
     __syncthreads();
     for (int i = tid; i < nt; i += kQNT) {
       const int32_t t0 = terms[q0 + i];
@@ -251,15 +296,56 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
         if (tid == 0) cur[i] = (int64_t)s_stop;
       }
       __syncthreads();
-      for (int j = tid; j < kTile; j += kQNT) {
-        const double sc = acc[j];
-        if (sc < 0.0) continue;
-        acc[j] = -1.0;
-        topk_insert<KMAX>(ts, td, sc, doc_key(reftie ? first[j] : 0u, lo + j));
+      if constexpr (LIST) {
+        for (int j0 = 0; j0 < kTile; j0 += kQNT) {  // uniform (l_n read after a barrier)
+          if (l_n + kQNT > kListCap) {
+            const int n = l_n;
+            list_sort(l_s, l_k, n);
+            if (tid == 0) {
+              l_n = min(n, k);
+              if (n >= k) {
+                l_ths = l_s[k - 1];
+                l_thk = l_k[k - 1];
+              }
+            }
+            __syncthreads();
+          }
+          const int j = j0 + tid;
+          const double sc = acc[j];
+          if (sc >= 0.0) {
+            acc[j] = -1.0;
+            const uint64_t key = doc_key(reftie ? first[j] : 0u, lo + j);
+            if (better(sc, key, l_ths, l_thk)) {
+              const int p = atomicAdd(&l_n, 1);
+              l_s[p] = sc;
+              l_k[p] = key;
+            }
+          }
+          __syncthreads();
+        }
+      } else {
+        for (int j = tid; j < kTile; j += kQNT) {
+          const double sc = acc[j];
+          if (sc < 0.0) continue;
+          acc[j] = -1.0;
+          topk_insert<KMAX>(ts, td, sc, doc_key(reftie ? first[j] : 0u, lo + j));
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
-    emit_topk<KMAX>(ts, td, k, q, out_d, out_s, out_t, red_s, red_d, red_t);
+    if constexpr (LIST) {
+      const int n = l_n;
+      list_sort(l_s, l_k, n);
+      for (int r = tid; r < k; r += kQNT) {
+        const bool valid = r < n;
+        out_d[(int64_t)q * k + r] = valid ? key_doc(l_k[r]) : -1;
+        out_s[(int64_t)q * k + r] = valid ? l_s[r] : 0.0;
+        if (out_t) out_t[(int64_t)q * k + r] = valid ? (uint32_t)(l_k[r] >> 32) : 0xFFFFFFFFu;
+      }
+      __syncthreads();  // the list is read before the next query resets it
+    } else {
+      emit_topk<KMAX>(ts, td, k, q, out_d, out_s, out_t, red_s, red_d, red_t);
+    }
   }
 }
 
@@ -2088,7 +2174,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       }
     }
   }
-  if (!tiled && k > 32) throw Error(SME_ENOTIMPL, "top-k with k > 32 for queries of more than 64 terms");
+  if (!tiled && k > kListCap - kQNT)
+    throw Error(SME_ELIMIT, "top-k with k > 1792 for queries of more than 64 terms");
   const int32_t *qord = nullptr;
   if (tiled && cx->opt_query_order) {
     // heaviest-term query order
@@ -2365,11 +2452,14 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     SME_HIP(hipEventRecord(e1, st));
     const unsigned grid = (unsigned)std::min(nq, 1 << 20);
     if (k <= 16)
-      hipLaunchKernelGGL(k_query<16>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
-                         d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
-    else
-      hipLaunchKernelGGL(k_query<32>, dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V, d_terms,
-                         d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
+      hipLaunchKernelGGL((k_query<16, false>), dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V,
+                         d_terms, d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
+    else if (k <= 32)
+      hipLaunchKernelGGL((k_query<32, false>), dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V,
+                         d_terms, d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
+    else  // k > 32: the LDS candidate list
+      hipLaunchKernelGGL((k_query<1, true>), dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V,
+                         d_terms, d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
     SME_CHECK_LAUNCH();
     SME_HIP(hipEventRecord(e2, st));
   }

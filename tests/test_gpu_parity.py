@@ -216,15 +216,14 @@ def _query_both_kernels(ix, terms, qoff, k):
     heavy, only full-span terms heavy, without seeds, with candidate lists so
     short that most queries overflow to the block-max sweep, the block-max sweep
     itself (4 / 0 / 8 seed tiles, batch order), and the streaming kernel
-    (k <= 32): all identical bits."""
+    (register lists for k <= 32, the LDS candidate list above): all identical bits."""
     dn, sc = ix.query_topk(terms, qoff, k)
     assert ix.ctx.last_build_profile()["query_kernel_name"] in ("k_query_win", "k_query")
     variants = [{"heavy_div": 0}, {"heavy_div": 1 << 30}, {"heavy_div": 1}, {"seed_m": 0}, {"cand_cap": 4},
                 {"win_sample": 0}, {"cand_cap": 16, "seed_m": 0},
                 {"cand_cap": 1, "heavy_div": 1}, {"query_kernel": 2}, {"query_kernel": 2, "seed_tiles": 0},
                 {"query_kernel": 2, "seed_tiles": 8, "query_order": 0}, {"query_kernel": 2, "heavy_div": 0}]
-    if k <= 32:
-        variants.append({"query_kernel": 1})
+    variants.append({"query_kernel": 1})
     for v in variants:
         dn2, sc2 = _query_opts(ix, terms, qoff, k, **v)
         assert np.array_equal(dn, dn2) and np.array_equal(sc, sc2), v
@@ -257,16 +256,19 @@ def test_queries_multi_tile(sme, synth):
     # every impact sum towards 64 x 254.  A 65-term query sends the whole batch
     # to the streaming kernel.
     heavy = np.argsort(-df, kind="stable")[:8].astype(np.int32)
-    for nlong in (64, 65):
+    # k > 32 with a 65-term query: the streaming kernel's LDS candidate list
+    # (round 3 returned SME_ENOTIMPL), several list compactions at k = 40
+    for nlong, k in ((64, 10), (65, 10), (65, 40), (65, 100), (65, 448)):
         q64 = np.concatenate([np.repeat(heavy, 4), np.arange(nlong - 32, dtype=np.int32)])
         long_terms = np.concatenate([tu[:ou[3]], q64])
         long_off = np.concatenate([ou[:4], [ou[3] + nlong]]).astype(np.int64)
-        dn, sc = ix.query_topk(long_terms, long_off, 10)
+        dn, sc = ix.query_topk(long_terms, long_off, k)
         assert ix.ctx.last_build_profile()["query_kernel_name"] == ("k_query_win" if nlong == 64 else "k_query")
         for q in range(4):
             tl = [names[t] for t in long_terms[long_off[q]:long_off[q + 1]] if t >= 0]
-            rd, rs = ref.query(tl, 10, 0, 0)
-            assert dn[q, :len(rd)].tolist() == rd and np.array_equal(sc[q, :len(rd)], np.array(rs)), (nlong, q)
+            rd, rs = ref.query(tl, k, 0, 0)
+            assert dn[q, :len(rd)].tolist() == rd and np.array_equal(sc[q, :len(rd)], np.array(rs)), (nlong, k, q)
+            assert (dn[q, len(rd):] == -1).all(), (nlong, k, q)
 
 
 def test_queries_dense_rows(sme, synth):
