@@ -34,7 +34,8 @@ namespace sme {
 constexpr int kQNT = 256;
 constexpr int kTile = 4096;
 constexpr int kQPer = 4;  // postings per lane per step
-constexpr int kMaxQTerms = 128;
+constexpr int kMaxQTerms = 128;      // register-list streaming kernel
+constexpr int kMaxQTermsList = 1024; // LDS-list streaming kernel
 constexpr int kLutLds = 256;  // 1 + ln(tf) for tf < 256 from LDS, the rare rest from HBM
 
 // Result order: score desc, then a 64-bit key asc.  key = tie << 32 | (docno
@@ -188,8 +189,9 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
   __shared__ double acc[kTile];
   __shared__ uint32_t first[kTile];  // SME_TIE_REFERENCE: ref_tie of the document's first token
   __shared__ double s_lut[kLutLds];
-  __shared__ int64_t cur[kMaxQTerms], endp[kMaxQTerms];
-  __shared__ double tidf[kMaxQTerms];
+  constexpr int QT = LIST ? kMaxQTermsList : kMaxQTerms;
+  __shared__ int64_t cur[QT], endp[QT];
+  __shared__ double tidf[QT];
   __shared__ int32_t s_next;
   __shared__ unsigned long long s_stop;
   __shared__ double red_s[kQNT / 64];
@@ -206,9 +208,9 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
   for (int q = blockIdx.x; q < nq; q += gridDim.x) {
     const int64_t q0 = qoff[q];
     int nt = (int)(qoff[q + 1] - q0);
-    if (nt > kMaxQTerms) {
+    if (nt > QT) {
       if (tid == 0) atomicOr(err, 1);
-      nt = kMaxQTerms;
+      nt = QT;
     }
     if (tid == 0) {
       s_next = 0x7FFFFFFF;
@@ -2070,6 +2072,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   int32_t *skt = nullptr;   // k_query_win: window skip table, transposed
   std::function<void()> build_sk;  // the tile skip table `sk` (k_query_bm), built on demand on the window path
   int h_mx = 0;
+  bool list_kernel = false;  // the streaming kernel with the LDS candidate list ran
   if (tiled) {
     hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
     SME_HIP(hipMemcpyAsync(&h_mx, err + 1, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -2449,16 +2452,27 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     SME_CHECK_LAUNCH();
     SME_HIP(hipEventRecord(e2, st));
   } else {
+    // the longest query picks the kernel: the register lists take <= 128 terms,
+    // the LDS list <= 1024
+    if (h_mx == 0 && nq > 0) {
+      hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
+      SME_HIP(hipMemcpyAsync(&h_mx, err + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+      SME_HIP(hipStreamSynchronize(st));
+    }
+    if (h_mx > kMaxQTermsList) throw Error(SME_ELIMIT, "a query has more than 1024 terms");
+    // ref_tie keys hold the token index in 8 bits
+    if (reftie && h_mx > 256) throw Error(SME_ELIMIT, "reference tie order with a query of more than 256 terms");
+    list_kernel = k > 32 || h_mx > kMaxQTerms;
     SME_HIP(hipEventRecord(e1, st));
     const unsigned grid = (unsigned)std::min(nq, 1 << 20);
-    if (k <= 16)
+    if (list_kernel)  // k > 32 or a query of more than 128 terms: the LDS candidate list
+      hipLaunchKernelGGL((k_query<1, true>), dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V,
+                         d_terms, d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
+    else if (k <= 16)
       hipLaunchKernelGGL((k_query<16, false>), dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V,
                          d_terms, d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
-    else if (k <= 32)
+    else
       hipLaunchKernelGGL((k_query<32, false>), dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V,
-                         d_terms, d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
-    else  // k > 32: the LDS candidate list
-      hipLaunchKernelGGL((k_query<1, true>), dim3(grid), dim3(kQNT), 0, st, off, dn, tf, lut, ix->max_tf, idf, V,
                          d_terms, d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, reftie, err);
     SME_CHECK_LAUNCH();
     SME_HIP(hipEventRecord(e2, st));
@@ -2495,7 +2509,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       fprintf(stderr, "SME_QSTATS tiles=%llu blocks_gated=%llu candidates=%llu compactions=%llu\n",
               (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3]);
   }
-  if (h_err) throw Error(SME_ELIMIT, "a query has more than 128 terms");
+  if (h_err) throw Error(SME_ELIMIT, list_kernel ? "a query has more than 1024 terms" : "a query has more than 128 terms");
 }
 
 static void query_subset(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, const int32_t *h_qlist,

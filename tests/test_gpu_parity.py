@@ -269,6 +269,22 @@ def test_queries_multi_tile(sme, synth):
             rd, rs = ref.query(tl, k, 0, 0)
             assert dn[q, :len(rd)].tolist() == rd and np.array_equal(sc[q, :len(rd)], np.array(rs)), (nlong, k, q)
             assert (dn[q, len(rd):] == -1).all(), (nlong, k, q)
+    # queries of more than 128 terms (up to 1024) take the LDS-list kernel at any k;
+    # reference tie order holds the token index in 8 bits (<= 256 terms)
+    rng = np.random.default_rng(17)
+    for nlong, k in ((300, 10), (300, 100), (1024, 10)):
+        ql = rng.integers(0, ix.V, size=nlong).astype(np.int32)
+        long_terms = np.concatenate([tu[:ou[3]], ql])
+        long_off = np.concatenate([ou[:4], [ou[3] + nlong]]).astype(np.int64)
+        dn, sc = ix.query_topk(long_terms, long_off, k)
+        assert ix.ctx.last_build_profile()["query_kernel_name"] == "k_query"
+        for q in range(4):
+            tl = [names[t] for t in long_terms[long_off[q]:long_off[q + 1]] if t >= 0]
+            rd, rs = ref.query(tl, k, 0, 0)
+            assert dn[q, :len(rd)].tolist() == rd and np.array_equal(sc[q, :len(rd)], np.array(rs)), (nlong, k, q)
+    too_long = np.zeros(1025, dtype=np.int32)
+    with pytest.raises(sme.SmeError):
+        ix.query_topk(too_long, np.array([0, 1025], dtype=np.int64), 10)
 
 
 def test_queries_dense_rows(sme, synth):
