@@ -220,8 +220,8 @@ int sme_lookup_terms(sme_index *ix, const uint8_t *terms, const int64_t *offs, i
 /* Batched rank(): query q has term ids term_ids[q_offsets[q] .. q_offsets[q+1])
  * in query-token order (duplicates count twice, -1 entries are skipped; an id
  * outside [-1, V) is SME_EINVAL here and skipped like -1 by the device entry).
- * k <= 448 (SME_ELIMIT above); queries of more than 64 terms take the streaming
- * kernel: up to 1024 terms (256 in SME_TIE_REFERENCE order), SME_ELIMIT beyond.
+ * k <= 1792 (SME_ELIMIT above; k > 448 and queries of more than 64 terms take the
+ * streaming kernel: up to 1024 terms, 256 in SME_TIE_REFERENCE order).
  * Writes k docnos / scores per query (score desc, docno asc), padded with
  * docno -1 / score 0 when fewer than k documents match. */
 int sme_query_topk(sme_index *ix, const int32_t *term_ids, const int64_t *q_offsets, int nq,

@@ -2041,7 +2041,9 @@ static void query_subset(sme_index *ix, const int32_t *d_terms, const int64_t *d
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k, int32_t *d_out_docno,
                 double *d_out_score, uint32_t *d_out_tie, hipStream_t st) {
   if (k < 1) throw Error(SME_EINVAL, "k must be >= 1");
-  if (k > 448) throw Error(SME_ELIMIT, "top-k with k > 448");
+  // k <= 448 on the window / block-max kernels; larger k up to 1792 on the streaming
+  // kernel's LDS candidate list
+  if (k > kListCap - kQNT) throw Error(SME_ELIMIT, "top-k with k > 1792");
   if (nq <= 0) return;
   sme_ctx *cx = ix->ctx;
   const int reftie = cx->cfg.tiebreak == SME_TIE_REFERENCE ? 1 : 0;
@@ -2060,7 +2062,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   // the block-max path unless a query is longer than kIMaxTerms or the batch's
   // skip table would be unreasonably large; option query_kernel = 1 forces the
   // streaming kernel (tests run both)
-  bool tiled = V > 0 && ix->P > 0 && ix->dmax >= ix->dmin && cx->opt_query_kernel != 1;
+  bool tiled = V > 0 && ix->P > 0 && ix->dmax >= ix->dmin && cx->opt_query_kernel != 1 && k <= 448;
   if (tiled) prepare_queries(ix, st);  // once per index (timed separately: q_prep_ms)
   hipEvent_t ep;
   SME_HIP(hipEventCreate(&ep));
@@ -2177,8 +2179,6 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       }
     }
   }
-  if (!tiled && k > kListCap - kQNT)
-    throw Error(SME_ELIMIT, "top-k with k > 1792 for queries of more than 64 terms");
   const int32_t *qord = nullptr;
   if (tiled && cx->opt_query_order) {
     // heaviest-term query order

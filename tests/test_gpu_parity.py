@@ -567,9 +567,10 @@ def test_unsorted_mapping_file(sme, synth):
         _check_build(sme, c, m, R=1)
 
 
-@pytest.mark.parametrize("k", [50, 100, 448])
+@pytest.mark.parametrize("k", [50, 100, 448, 1000])
 def test_queries_large_k(sme, synth, k):
-    """top-k beyond the register lists: k = 50 / 100 / 448 (c5's top-100)."""
+    """top-k beyond the register lists: k = 50 / 100 / 448 (c5's top-100); k = 1000
+    (above the window kernels' 448: the streaming kernel's LDS list, up to 1792)."""
     n = 3000
     c = synth.gen_corpus(n, V=400, seed=23, len_lo=5, len_hi=40)
     ix, ref = _check_build(sme, c, synth.docids(n), R=1)
@@ -583,6 +584,10 @@ def test_queries_large_k(sme, synth, k):
         assert dn[q, :len(rd)].tolist() == rd, q
         assert np.array_equal(sc[q, :len(rd)], np.array(rs)), q
         assert (dn[q, len(rd):] == -1).all()
+    if k > 448:
+        assert ix.ctx.last_build_profile()["query_kernel_name"] == "k_query"
+        with pytest.raises(sme.SmeError):
+            ix.query_topk(terms, qoff, 1793)
 
 
 def test_forward_index_on_device_output(sme, synth, tmp_path):
