@@ -1122,43 +1122,61 @@ static_assert(sizeof(QDesc) == 32 && sizeof(QPos) == 16, "record sizes");
 // Window-granular skip table of the k_query_win path, built directly (no tile
 // table, no transpose): skt[w * nrows + row] = first posting (term-relative) of
 // the row's term in window w or later; skt[nwin * nrows + row] = df.  Change
-// points (k_skipw_fill_rows), then a suffix minimum per row over the windows.
-// The same change points with one wave per row (lanes stride over the row's
-// postings): a chunk walk over a batch's many short sparse rows made every
-// thread advance row by row through dependent offset loads (0.84 ms per c2 batch)
-__global__ __launch_bounds__(256) void k_skipw_fill_rows(const int64_t *rdf, int64_t nrows, const int32_t *term_of_row,
-                                                         const int64_t *off, const int32_t *docno, int64_t dmin,
-                                                         int64_t nwin, int32_t *skt) {
+// points (k_skipw_fill_rm), then a suffix minimum per row over the windows
+// (k_skipw_suffix_tr). One wave per row: a chunk walk over a batch's many short
+// sparse rows made every thread advance row by row through dependent offset loads.
+// Row-major variant (R[row * (nwin + 1) + w]): a row's change points land in its
+// own contiguous run instead of one cache line per window of the window-major
+// table, and k_skipw_suffix_tr turns R into skt through LDS tiles with coalesced
+// reads and writes (the window-major fill's scattered 4-byte stores bound it)
+__global__ __launch_bounds__(256) void k_skipw_fill_rm(const int64_t *rdf, int64_t nrows, const int32_t *term_of_row,
+                                                       const int64_t *off, const int32_t *docno, int64_t dmin,
+                                                       int64_t nwin, int32_t *R) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
   for (int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < nrows; row += nw) {
     const int64_t n = rdf[row];
     if (n == 0) continue;  // (wave-uniform) heavy rows and absent terms
     const int64_t b = off[term_of_row[row]];
+    int32_t *rr = R + row * (nwin + 1);
     for (int64_t i = lane; i < n; i += 64) {
       const int64_t j = ((int64_t)docno[b + i] - dmin) >> kWinB;
       const int64_t jp = i == 0 ? -1 : (((int64_t)docno[b + i - 1] - dmin) >> kWinB);
-      if (jp < j) skt[j * nrows + row] = (int32_t)i;
-      if (i == n - 1) skt[nwin * nrows + row] = (int32_t)n;
+      if (jp < j) rr[j] = (int32_t)i;
+      if (i == n - 1) rr[nwin] = (int32_t)n;
     }
   }
 }
-// one thread per row (neighbouring rows: neighbouring words), eight windows'
-// loads in flight at a time; rows with df = 0 are all zeros
-__global__ __launch_bounds__(256) void k_skipw_suffix(const int64_t *rdf, int64_t nrows, int64_t nwin, int32_t *skt) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
-    const bool empty = rdf[r] == 0;
-    int32_t v = 0x7FFFFFFF;
-    for (int64_t w1 = nwin + 1; w1 > 0; w1 -= 8) {
-      int32_t u[8];
-#pragma unroll
-      for (int c = 0; c < 8; c++) u[c] = w1 - 1 - c >= 0 ? skt[(w1 - 1 - c) * nrows + r] : 0;
-#pragma unroll
-      for (int c = 0; c < 8; c++) {
-        if (w1 - 1 - c < 0) break;
-        v = min(v, u[c]);
-        skt[(w1 - 1 - c) * nrows + r] = empty ? 0 : v;
+// 64 rows per workgroup, windows in 64-wide chunks from the last: chunk rows
+// loaded along R's rows, a suffix minimum per row (thread t walks row t, the
+// carry from the chunk to its right in a register), then written along skt's
+// window rows; rows with df = 0 are all zeros
+__global__ __launch_bounds__(256) void k_skipw_suffix_tr(const int64_t *rdf, int64_t nrows, int64_t nwin,
+                                                         const int32_t *R, int32_t *skt) {
+  __shared__ int32_t tile[64][65];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t NW1 = nwin + 1;
+  for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < nrows; r0 += (int64_t)gridDim.x * 64) {  // block-uniform
+    const bool empty = tid < 64 && (r0 + tid >= nrows || rdf[r0 + tid] == 0);
+    int32_t carry = 0x7FFFFFFF;
+    for (int64_t w0 = ((NW1 - 1) >> 6) << 6; w0 >= 0; w0 -= 64) {
+      for (int rr = wv; rr < 64; rr += 4) {
+        const int64_t row = r0 + rr, w = w0 + lane;
+        tile[rr][lane] = (row < nrows && w < NW1) ? R[row * NW1 + w] : 0x7FFFFFFF;
       }
+      __syncthreads();
+      if (tid < 64) {
+        for (int c = 63; c >= 0; c--) {
+          carry = min(carry, tile[tid][c]);
+          tile[tid][c] = empty ? 0 : carry;
+        }
+      }
+      __syncthreads();
+      for (int ww = wv; ww < 64; ww += 4) {
+        const int64_t w = w0 + ww, row = r0 + lane;
+        if (w < NW1 && row < nrows) skt[w * nrows + row] = tile[lane][ww];
+      }
+      __syncthreads();
     }
   }
 }
@@ -2148,7 +2166,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           if (cx->opt_query_kernel == 0) {
             const int64_t nwin = T >> 2, ne = nrows * (nwin + 1);
             skt = W[31].as<int32_t>(ne);
-            SME_HIP(hipMemsetAsync(skt, 0x7F, (size_t)ne * sizeof(int32_t), st));
+            int32_t *rm = W[29].as<int32_t>(ne);  // row-major change points (prep only)
+            SME_HIP(hipMemsetAsync(rm, 0x7F, (size_t)ne * sizeof(int32_t), st));
             // only the sparse rows: k_query_win reads heavy terms from their impact
             // rows, never their skip entries (and heavy terms hold most postings)
             const int32_t *hro = ix->q_H > 0 ? (const int32_t *)ix->d_hrow_of.p : nullptr;
@@ -2158,10 +2177,10 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
               hipLaunchKernelGGL(k_sparse_rdf, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 16384)), dim3(256),
                                  0, st, tor, rdf, hro, nrows, rdfw);
             }
-            hipLaunchKernelGGL(k_skipw_fill_rows, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 65536)),
-                               dim3(256), 0, st, rdfw, nrows, tor, off, dn, ix->dmin, nwin, skt);
-            hipLaunchKernelGGL(k_skipw_suffix, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 16384)),
-                               dim3(256), 0, st, rdfw, nrows, nwin, skt);
+            hipLaunchKernelGGL(k_skipw_fill_rm, dim3((unsigned)std::min<int64_t>((nrows + 3) / 4, 65536)),
+                               dim3(256), 0, st, rdfw, nrows, tor, off, dn, ix->dmin, nwin, rm);
+            hipLaunchKernelGGL(k_skipw_suffix_tr, dim3((unsigned)std::min<int64_t>((nrows + 63) / 64, 16384)),
+                               dim3(256), 0, st, rdfw, nrows, nwin, rm, skt);
           } else {
             build_sk();
           }
