@@ -21,11 +21,18 @@ offsets monotone, docnos ascending per term), a cross-kernel check of a query
 sample (tiled default == postings-only == streaming kernel, bit for bit), and the
 I9 serialization of the partition records as its own stage.
 
-Multi-GPU (torchrun, one rank per GPU, RCCL): every rank owns a contiguous shard
-of docs (docids offset by rank), builds its local index, and the global document
-count is all-reduced in every step (reference-mode idf = log10(N_global)).
-Queries are run on every shard and the per-shard top-k lists are all-gathered and
-merged.
+Multi-GPU (one rank per GPU, RCCL): `--gpus N` under torchrun (WORLD_SIZE set)
+runs as one rank of N; `--gpus N` without WORLD_SIZE starts the N rank processes
+itself before anything touches the GPU (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1), and exits with rank 0's status.  The world size the
+ranks agree on must equal --gpus (and the node must have that many GPUs unless
+SME_BENCH_REHEARSE=1), so an N-GPU line cannot silently measure one GPU.  Every
+rank owns a contiguous shard of docs (docids offset by rank), builds its local
+index, and the global document count is all-reduced in every step
+(reference-mode idf = log10(N_global)).  The query batch is broadcast as one
+UTF-8 term blob + offsets (tensors); every shard scores it, and the per-shard
+top-k lists go to the queries' owner ranks (one all_to_all) and are merged there
+(dist.merge_topk_owner).
 
 Prints ONE JSON line on rank 0.
 """
@@ -59,7 +66,7 @@ CONFIGS = {
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default WORLD_SIZE or 1")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", choices=sorted(CONFIGS), default="c2")
@@ -83,9 +90,35 @@ def parse():
     return a
 
 
+def spawn_ranks(n):
+    """--gpus N > 1 without a launcher: start N rank processes of this script
+    (one per GPU) and return rank 0's exit status (any failing rank fails the
+    run).  Nothing here touches the GPU: the children initialise their own."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return codes[0] if codes[0] != 0 else (bad[0] if bad else 0)
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus is not None and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))
+    world = int(env_world or "1")
+    if a.gpus is None:
+        a.gpus = world
+    if a.gpus != world:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -95,6 +128,9 @@ def main():
     rehearse = os.environ.get("SME_BENCH_REHEARSE") == "1"
     if rehearse:
         local = local % max(1, torch.cuda.device_count())
+    elif world > torch.cuda.device_count():
+        raise SystemExit("bench.py: %d ranks but %d visible GPUs (SME_BENCH_REHEARSE=1 rehearses on fewer)"
+                         % (world, torch.cuda.device_count()))
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -103,6 +139,11 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # every rank must see the same world: the line's n_gpus is the agreed one
+        wt = torch.tensor([1], dtype=torch.int64, device="cpu" if rehearse else "cuda")
+        dist.all_reduce(wt)
+        if int(wt.item()) != a.gpus:
+            raise SystemExit("bench.py: %d ranks joined, --gpus %d" % (int(wt.item()), a.gpus))
     sme = importlib.import_module(PKG)
     synth = importlib.import_module(PKG + ".synth")
     L = sme.lib()
@@ -168,6 +209,19 @@ def main():
     profs.append(ctx.last_build_profile())
     prof = {k: round(sum(p.get(k, 0.0) for p in profs) / len(profs), 4) for k in profs[-1]}
     N, V, P = ix.N, ix.V, ix.P
+    # the drop-in's product is the part files' records (TermKGramDocIndexer.java:
+    # 269-275): the same steps again with the I9 device serialization inside the
+    # clock (sme_index_serialize), reported as value_with_records beside value
+    barrier()
+    gc.disable()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ix.close()
+        ix = step()
+        ix.serialize()
+    barrier()
+    dt_rec = (time.perf_counter() - t0) / a.steps
+    gc.enable()
     t_max = dt
     tot_bytes = nbytes
     df_ex = None
@@ -182,12 +236,14 @@ def main():
         barrier()
         df_ex["total_ms"] = round((time.perf_counter() - t_ex) * 1e3, 3)
         df_ex = {k2: (round(v, 3) if isinstance(v, float) else v) for k2, v in df_ex.items()}
-        tt = torch.tensor([dt, float(nbytes), float(N), float(V), float(P)], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt, float(nbytes), float(N), float(V), float(P), dt_rec], dtype=torch.float64,
+                          device="cpu" if rehearse else "cuda")
         ts = [torch.zeros_like(tt) for _ in range(world)]
         dist.all_gather(ts, tt)
         ts = torch.stack(ts).cpu().numpy()
         t_max = float(ts[:, 0].max())
         tot_bytes = float(ts[:, 1].sum())
+        dt_rec = float(ts[:, 5].max())
     gbs = tot_bytes / t_max / 1e9
     alg_bytes = nbytes + 8 * P + 8 * (V + 1)  # A_build = B + 8P + 8(V+1) per GPU
     # dominant kernel: the stream tokenizer (k_tok_fast).  Algorithmic bytes per
@@ -226,11 +282,20 @@ def main():
                      "what": "dominant kernel k_tok_fast: algorithmic bytes = text bytes B read once per launch, / "
                              "mean launch time (HIP events on its stream); traffic = PMC HBM bytes per launch "
                              "(profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)"},
+        "value_with_records": {"value": round(tot_bytes / dt_rec / 1e9, 4), "unit": "GB/s",
+                               "ms_per_step": round(dt_rec * 1e3, 3),
+                               "what": "build + TF-IDF + I9 serialization of the partition records in HBM "
+                                       "(sme_index_serialize) per step, max over ranks; the records stay in HBM"
+                                       + ("" if world == 1 else "; per-shard records (the reference layout "
+                                          "needs dist.reference_partitions' exchange, not timed)")},
         "build_roofline": {"achieved": round(achieved_build, 2), "unit": "GB/s",
                            "frac": round(achieved_build / HBM_PEAK_GBS, 5),
                            "what": "whole build step: A_build = B + 8P + 8(V+1) per GPU / step time"},
         "stage_ms": prof,
     }
+    if rehearse and world > 1:
+        result["rehearsal"] = "SME_BENCH_REHEARSE: %d ranks on %d GPU(s), gloo -- not a scaling measurement" % (
+            world, torch.cuda.device_count())
     if query is not None:
         result["query"] = query
     # calibration: the achievable HBM rate of a streaming copy on this device,
@@ -279,19 +344,10 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
     _, _, _, df = ix.csr()
     terms, qoff = synth.queries_by_df(df, a.queries, seed=a.cfg["qseed"])
     if dist is not None:
-        # queries are defined by term strings (rank 0's draw); every shard maps them to its own ids
-        uniq = np.unique(terms)
-        obj = [[ix.term(int(t)) for t in uniq], uniq, qoff] if rank == 0 else [None, None, None]
-        dist.broadcast_object_list(obj, src=0)
-        strs, uniq, qoff = obj
-        if rank == 0:
-            pos = np.searchsorted(uniq, terms)
-        else:
-            terms = None
-        loc = ix.lookup(strs)
-        obj2 = [pos if rank == 0 else None]
-        dist.broadcast_object_list(obj2, src=0)
-        terms = loc[obj2[0]].astype(np.int32)
+        # queries are defined by term strings (rank 0's draw); every shard maps them
+        # to its own ids.  The batch travels as tensors: one UTF-8 blob of the
+        # distinct terms + their offsets, and per query term its index among them
+        terms, qoff = broadcast_queries(ix, terms, qoff, dist, rank, torch)
     d_terms = torch.from_numpy(terms).cuda()
     d_qoff = torch.from_numpy(qoff).cuda()
     out_d = torch.empty((a.queries, k), dtype=torch.int32, device="cuda")
@@ -428,6 +484,46 @@ def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):
             "postings_touched_what": "8 B x postings of every query term (re-reads across queries included)"}
 
 
+def broadcast_queries(ix, terms, qoff, dist, rank, torch):
+    """Rank 0's query batch (its own term ids) -> every rank's local term ids of
+    the same term strings.  Broadcasts: sizes (int64 [3]), the distinct terms as
+    one UTF-8 blob (uint8) + offsets (int64), the per-term index into them (int32)
+    and the query offsets (int64); each rank resolves the strings with
+    sme_lookup_terms (Index.lookup)."""
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    if rank == 0:
+        uniq, pos = np.unique(terms, return_inverse=True)
+        bs = [ix.term(int(t)).encode("utf-8", "surrogatepass") for t in uniq]
+        blob = np.frombuffer(b"".join(bs), dtype=np.uint8)
+        boff = np.zeros(len(bs) + 1, np.int64)
+        boff[1:] = np.cumsum([len(b) for b in bs])
+        hdr = torch.tensor([len(blob), len(bs), len(terms)], dtype=torch.int64, device=dev)
+    else:
+        hdr = torch.zeros(3, dtype=torch.int64, device=dev)
+    dist.broadcast(hdr, 0)
+    nb, nu, nt = (int(x) for x in hdr.tolist())
+    nq1 = len(qoff) if rank == 0 else 0
+    t_nq = torch.tensor([nq1], dtype=torch.int64, device=dev)
+    dist.broadcast(t_nq, 0)
+    nq1 = int(t_nq.item())
+    if rank == 0:
+        tb = torch.from_numpy(blob.copy() if nb else np.zeros(1, np.uint8)).to(dev)
+        to = torch.from_numpy(boff).to(dev)
+        tp = torch.from_numpy(pos.astype(np.int32)).to(dev)
+        tq = torch.from_numpy(np.asarray(qoff, np.int64)).to(dev)
+    else:
+        tb = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+        to = torch.empty(nu + 1, dtype=torch.int64, device=dev)
+        tp = torch.empty(nt, dtype=torch.int32, device=dev)
+        tq = torch.empty(nq1, dtype=torch.int64, device=dev)
+    for t in (tb, to, tp, tq):
+        dist.broadcast(t, 0)
+    blob, boff = tb.cpu().numpy()[:nb].tobytes(), to.cpu().numpy()
+    strs = [blob[boff[i]:boff[i + 1]].decode("utf-8", "surrogatepass") for i in range(nu)]
+    loc = ix.lookup(strs)
+    return loc[tp.cpu().numpy()].astype(np.int32), tq.cpu().numpy()
+
+
 def post_checks(a, sme, synth, ix, n_local, d0, qinternal, rank, n_global=None):
     """Untimed, size-independent checks of the full-size build and query batch."""
     out = {}
@@ -554,15 +650,16 @@ def _hip_copy(dst, src, n, kind):
 
 def pmc_traffic(kernel, a, detail=False):
     """HBM bytes per launch of `kernel` from the committed PMC passes
-    (profiles/pmc_traffic.json, written by tools/pmc_summary.py from separate
+    (profiles/pmc_traffic[_CONFIG].json, written by tools/pmc_summary.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench config), or None.
     detail=True: (corrected total, raw FETCH_SIZE bytes, WRITE_SIZE bytes)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    name = "pmc_traffic.json" if a.config == "c2" else "pmc_traffic_%s.json" % a.config
+    path = os.path.join(ROOT, "profiles", name)
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return (None, None, None) if detail else None
-    if d.get("docs") != a.docs or d.get("vocab") != a.vocab or a.config != "c2":
+    if d.get("docs") != a.docs or d.get("vocab") != a.vocab:
         return (None, None, None) if detail else None
     k = d.get("kernels", {}).get(kernel)
     if k is None:

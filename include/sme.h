@@ -98,6 +98,8 @@ void sme_destroy(sme_ctx *ctx);
  *   "seed_tiles"    k_query_bm: best-bound tiles scored before the sweep, 0..8 (default 4)
  *   "query_order"   1 heaviest-term query order (default), 0 batch order
  *   "agg_two_pass"  1 count + emit aggregation passes (default 0: single pass)
+ *   "kgram_rank"    1: K >= 2 gram keys by iterated ranking (the path of K * ceil(log2 V) > 63)
+ *                   even when the packed term ids fit 64 bits (default 0: automatic)
  *   "tok_grid"      tokenizer workgroups, >= 1 (default 4096)
  *   "raw_load_pct"  raw-vocabulary table load of the next build, 10..90 (default 40)
  *   "query_table_budget"  bytes a batch's skip table may take (default 0 =
@@ -256,6 +258,25 @@ int sme_query_topk_device_tie(sme_index *ix, const int32_t *d_term_ids, const in
  * fingerprints, so a multi-GPU df exchange can key the all-reduce on them
  * without gathering and sorting term strings (dist.py global_df). */
 int sme_index_term_fingerprints(sme_index *ix, uint64_t *d_out, void *stream);
+
+/* Global df of a doc-sharded build by owner rank (the reducer's df =
+ * postings length summed over the map outputs, TermKGramDocIndexer.java:175-183).
+ * Rows are (fp[2i], fp[2i+1], df[i]) in device memory; a row's owner is
+ * fp[2i] % world.
+ *   pack:   rows grouped by owner into send_fp[2n] / send_df[n] (owner 0's rows
+ *           first, ...), pos[i] = send slot of row i, counts[world] (host) = rows
+ *           per owner -- the layout of one all_to_all
+ *   sum:    for every received row, out[i] = the sum of df over all received rows
+ *           with the same 128-bit fingerprint; *distinct = fingerprints seen
+ *   unpack: out[i] = ret[pos[i]] (the owners' sums, returned in send order, back
+ *           in local row order)
+ * Replaces the Hadoop shuffle's grouping of the doc-counter / df by key. */
+int sme_df_owner_pack(sme_ctx *ctx, const uint64_t *d_fp, const int64_t *d_df, int64_t n, int world,
+                      uint64_t *d_send_fp, int64_t *d_send_df, int64_t *d_pos, int64_t *counts, void *stream);
+int sme_df_owner_sum(sme_ctx *ctx, const uint64_t *d_fp, const int64_t *d_df, int64_t n, int64_t *d_out,
+                     int64_t *distinct, void *stream);
+int sme_df_owner_unpack(sme_ctx *ctx, const int64_t *d_ret, const int64_t *d_pos, int64_t n, int64_t *d_out,
+                        void *stream);
 
 /* Recompute the fp64 TF-IDF weights of a doc-sharded index with global
  * statistics: n_global = records over all shards (all-reduced doc counter),

@@ -49,7 +49,7 @@ EXPORTS = [
     "sme_build_chargram", "sme_build_chargram_device", "sme_chargram_partition_text", "sme_chargram_stats",
     "sme_split_points", "sme_split_points_device", "sme_index_term_fingerprints", "sme_set_option",
     "sme_index_prepare_queries", "sme_hbm_copy_bench", "sme_index_pack_pieces", "sme_merge_pieces",
-    "sme_index_record_docnos",
+    "sme_index_record_docnos", "sme_df_owner_pack", "sme_df_owner_sum", "sme_df_owner_unpack",
 ]
 
 
@@ -110,6 +110,9 @@ def lib():
     L.sme_index_pack_pieces.argtypes = [vp, C.c_int, vp, C.POINTER(C.c_uint64), vp]
     L.sme_merge_pieces.argtypes = [vp, vp, C.POINTER(C.c_uint64), C.c_int, vp, C.POINTER(vp)]
     L.sme_index_record_docnos.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_int64)]
+    L.sme_df_owner_pack.argtypes = [vp, vp, vp, C.c_int64, C.c_int, vp, vp, vp, i64p, vp]
+    L.sme_df_owner_sum.argtypes = [vp, vp, vp, C.c_int64, vp, i64p, vp]
+    L.sme_df_owner_unpack.argtypes = [vp, vp, vp, C.c_int64, vp, vp]
     _lib = L
     return L
 
@@ -220,6 +223,27 @@ class Context:
         _check(lib().sme_build_index_device(self._h, C.c_void_p(d_ptr), nbytes, C.c_void_p(stream or 0),
                                             C.byref(h)))
         return Index(h, self)
+
+    def df_owner_pack(self, d_fp, d_df, n, world, d_send_fp, d_send_df, d_pos, stream=None):
+        """sme_df_owner_pack: rows grouped by owner rank (fp word 0 mod world) for
+        one all_to_all; returns the rows per owner (list of `world` ints)."""
+        counts = (C.c_int64 * max(world, 1))()
+        _check(lib().sme_df_owner_pack(self._h, C.c_void_p(d_fp), C.c_void_p(d_df), n, world, C.c_void_p(d_send_fp),
+                                       C.c_void_p(d_send_df), C.c_void_p(d_pos), counts, C.c_void_p(stream or 0)))
+        return [int(c) for c in counts[:world]]
+
+    def df_owner_sum(self, d_fp, d_df, n, d_out, stream=None):
+        """sme_df_owner_sum: per received row, df summed over its fingerprint's
+        rows; returns the number of distinct fingerprints."""
+        dist = C.c_int64()
+        _check(lib().sme_df_owner_sum(self._h, C.c_void_p(d_fp), C.c_void_p(d_df), n, C.c_void_p(d_out),
+                                      C.byref(dist), C.c_void_p(stream or 0)))
+        return dist.value
+
+    def df_owner_unpack(self, d_ret, d_pos, n, d_out, stream=None):
+        """sme_df_owner_unpack: out[i] = ret[pos[i]]."""
+        _check(lib().sme_df_owner_unpack(self._h, C.c_void_p(d_ret), C.c_void_p(d_pos), n, C.c_void_p(d_out),
+                                         C.c_void_p(stream or 0)))
 
     def merge_pieces(self, d_blobs, sizes):
         """sme_merge_pieces: the blobs one rank received from every shard (device

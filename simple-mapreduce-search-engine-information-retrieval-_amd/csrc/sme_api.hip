@@ -294,6 +294,9 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
     } else if (n == "win_sample") {
       range(0, 1);
       cx->opt_win_sample = v;
+    } else if (n == "kgram_rank") {
+      range(0, 1);
+      cx->opt_kgram_rank = v;
     } else if (n == "win_slice") {
       range(1, int64_t(1) << 30);
       cx->opt_win_slice = v;
@@ -706,6 +709,37 @@ int sme_index_term_fingerprints(sme_index *ix, uint64_t *d_out, void *stream) {
     set_device(ix->ctx);
     hipStream_t st = stream_of(ix->ctx, stream);
     sme::term_fingerprints(ix, d_out, st);
+    SME_HIP(hipStreamSynchronize(st));
+  });
+}
+
+int sme_df_owner_pack(sme_ctx *ctx, const uint64_t *d_fp, const int64_t *d_df, int64_t n, int world,
+                      uint64_t *d_send_fp, int64_t *d_send_df, int64_t *d_pos, int64_t *counts, void *stream) {
+  return guard([&] {
+    if (!ctx || !counts || n < 0 || (n > 0 && (!d_fp || !d_df || !d_send_fp || !d_send_df || !d_pos)))
+      throw sme::Error(SME_EINVAL, "bad argument");
+    set_device(ctx);
+    sme::dfx_pack(ctx, d_fp, d_df, n, world, d_send_fp, d_send_df, d_pos, counts, stream_of(ctx, stream));
+  });
+}
+
+int sme_df_owner_sum(sme_ctx *ctx, const uint64_t *d_fp, const int64_t *d_df, int64_t n, int64_t *d_out,
+                     int64_t *distinct, void *stream) {
+  return guard([&] {
+    if (!ctx || !distinct || n < 0 || (n > 0 && (!d_fp || !d_df || !d_out)))
+      throw sme::Error(SME_EINVAL, "bad argument");
+    set_device(ctx);
+    sme::dfx_sum(ctx, d_fp, d_df, n, d_out, distinct, stream_of(ctx, stream));
+  });
+}
+
+int sme_df_owner_unpack(sme_ctx *ctx, const int64_t *d_ret, const int64_t *d_pos, int64_t n, int64_t *d_out,
+                        void *stream) {
+  return guard([&] {
+    if (!ctx || n < 0 || (n > 0 && (!d_ret || !d_pos || !d_out))) throw sme::Error(SME_EINVAL, "bad argument");
+    set_device(ctx);
+    hipStream_t st = stream_of(ctx, stream);
+    sme::dfx_unpack(d_ret, d_pos, n, d_out, st);
     SME_HIP(hipStreamSynchronize(st));
   });
 }

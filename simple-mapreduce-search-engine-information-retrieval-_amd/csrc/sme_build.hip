@@ -1819,6 +1819,7 @@ struct AggIn {
   const int32_t *raw_term;
   const int32_t *raw_nout;
   const int32_t *multi_term;
+  const int32_t *max_nout = nullptr;  // largest number of terms one raw token yields
   const int64_t *perm;   // records in docno order
   const int32_t *docno;  // per record
   // emit form: v32 != nullptr writes the sort's packed u32 value (docno - dmin) * F + tf
@@ -1965,7 +1966,10 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
       if (k < cap / 2) cnt2[k] = 0;
     }
     wave_sync_lds();
-    bool ok = nt < 65536;  // (more tokens: the big-record path, u16 counts could carry)
+    // the u16 counts hold up to 65535: bound the record's TERM count (a raw token
+    // can yield up to max_nout terms, e.g. a dotted split), not its token count;
+    // beyond it the record takes the big-record path
+    bool ok = (int64_t)nt * (int64_t)max(in.max_nout ? *in.max_nout : 1, 1) < 65536;
     // kAggU tokens per lane step: their stream loads, then their raw_term
     // gathers, are in flight together (one step was two dependent latencies)
     for (int32_t t0 = lane; t0 < nt; t0 += kAggU * 64) {
@@ -2412,11 +2416,13 @@ __device__ __forceinline__ bool gram_insert(uint64_t *keys, int32_t *cnt, uint64
 // per record (wave): k-gram tf in an LDS table.  Records with more than kGLimit
 // distinct grams emit one (gram, docno, 1) pair per occurrence instead (flag
 // big[i]); the reducer-style merge of equal (gram, docno) sums them afterwards.
+// pos_key != nullptr: the gram at term-stream position p is pos_key[p] (its rank,
+// k_gram_rank_round) instead of the packed term ids (K * tb > 63)
 template <bool EMIT>
 __global__ __launch_bounds__(kAggNT) void k_gram_agg(const int32_t *tstream, const int64_t *toff, int64_t nR,
                                                      const int64_t *perm, const int32_t *docno_r, int K, int tb,
                                                      int64_t *pcount, uint8_t *big, const int64_t *pair_off,
-                                                     uint64_t *pkey, uint64_t *pval) {
+                                                     uint64_t *pkey, uint64_t *pval, const uint32_t *pos_key) {
   __shared__ uint64_t keys_all[kAggNT / 64][kGCap];
   __shared__ int32_t cnt_all[kAggNT / 64][kGCap];
   __shared__ int32_t dist_all[kAggNT / 64];
@@ -2432,7 +2438,7 @@ __global__ __launch_bounds__(kAggNT) void k_gram_agg(const int32_t *tstream, con
     const uint64_t dn = (uint64_t)(uint32_t)docno_r[perm[i]] << 32;
     if (EMIT && big[i]) {
       for (int64_t j = lane; j < ng; j += 64) {
-        pkey[pair_off[i] + j] = gram_key(ts + j, K, tb);
+        pkey[pair_off[i] + j] = pos_key ? (uint64_t)pos_key[toff[i] + j] : gram_key(ts + j, K, tb);
         pval[pair_off[i] + j] = dn | 1u;
       }
       continue;
@@ -2444,7 +2450,8 @@ __global__ __launch_bounds__(kAggNT) void k_gram_agg(const int32_t *tstream, con
     if (lane == 0) *distinct = 0;
     wave_sync_lds();
     bool ok = true;
-    for (int64_t j = lane; j < ng; j += 64) ok &= gram_insert(keys, cnt, gram_key(ts + j, K, tb), distinct);
+    for (int64_t j = lane; j < ng; j += 64)
+      ok &= gram_insert(keys, cnt, pos_key ? (uint64_t)pos_key[toff[i] + j] : gram_key(ts + j, K, tb), distinct);
     wave_sync_lds();
     const int32_t d = *distinct;
     const bool isbig = __any(!ok) || d > kGLimit;
@@ -2484,6 +2491,50 @@ __global__ void k_gram_ids(const uint64_t *k, const uint32_t *incl, int64_t P, i
     if (i == 0 || k[i] != k[i - 1])
       for (int j = 0; j < K; j++) gcomp[(int64_t)g * K + j] = (int32_t)((k[i] >> (tb * (K - 1 - j))) & ((1ull << tb) - 1));
   }
+}
+
+// K * ceil(log2 V) > 63 (k-grams of a large vocabulary): gram keys by iterated
+// ranking.  The 1-gram at position p is its term id t_p; the j-gram at p is the
+// pair (rank of the (j-1)-gram at p, t_{p+j-1}), and its rank among the distinct
+// j-grams of the corpus, ordered by that pair, is the key of the next round.
+// Ranks preserve the lexicographic order of the id tuples, which is
+// TermDF.compareTo's order (TermDF.java:64-70: element-wise String.compareTo,
+// term ids being ranks in that order), so the last round's rank IS the gram id
+// in TermDF order, held in 32 bits whatever K is.  Positions whose j-gram leaves
+// the record get the all-ones key and sort last.
+__global__ __launch_bounds__(kAggNT) void k_gram_round_keys(const int32_t *tstream, const int64_t *toff, int64_t nR,
+                                                            int j, int tb, const uint32_t *rprev, uint64_t *key,
+                                                            uint32_t *pos) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
+  for (int64_t i = (int64_t)blockIdx.x * (kAggNT / 64) + wv; i < nR; i += nwaves) {
+    const int64_t a = toff[i], e = toff[i + 1];
+    for (int64_t p = a + lane; p < e; p += 64) {
+      const bool valid = p + j - 1 < e;
+      const uint64_t prev = rprev ? (uint64_t)rprev[p] : (uint64_t)(uint32_t)tstream[p];
+      key[p] = valid ? (prev << tb) | (uint64_t)(uint32_t)tstream[p + j - 1] : ~0ull;
+      pos[p] = (uint32_t)p;
+    }
+  }
+}
+__global__ void k_gram_round_heads(const uint64_t *ks, int64_t M, uint32_t *head) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < M; s += (int64_t)gridDim.x * blockDim.x)
+    head[s] = (ks[s] != ~0ull && (s == 0 || ks[s] != ks[s - 1])) ? 1u : 0u;
+}
+// rank of sorted item s = (inclusive head count) - 1, scattered to its position;
+// rep[rank] = one position holding the gram (last round: its components)
+__global__ void k_gram_round_scatter(const uint64_t *ks, const uint32_t *ps, const uint32_t *head,
+                                     const uint32_t *excl, int64_t M, uint32_t *rnew, uint32_t *rep) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < M; s += (int64_t)gridDim.x * blockDim.x) {
+    if (ks[s] == ~0ull) continue;
+    const uint32_t r = excl[s] + head[s] - 1u;
+    rnew[ps[s]] = r;
+    if (rep && head[s]) rep[r] = ps[s];
+  }
+}
+__global__ void k_gram_comp_rep(const uint32_t *rep, int64_t Vg, int K, const int32_t *tstream, int32_t *gcomp) {
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < Vg; g += (int64_t)gridDim.x * blockDim.x)
+    for (int c = 0; c < K; c++) gcomp[g * K + c] = tstream[(int64_t)rep[g] + c];
 }
 
 // ============================================================================
@@ -3363,6 +3414,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   ai.raw_term = raw_term;
   ai.raw_nout = co.raw_nout;
   ai.multi_term = multi;
+  ai.max_nout = co.max_nout;
   ai.perm = perm;
   ai.docno = docno;
   int64_t P = 0;
@@ -3521,8 +3573,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   } else if (K >= 2) {
     // K >= 2: term streams, k-gram pairs per record, gram ids in TermDF order
     const int tb = bits_for((uint64_t)std::max<int64_t>(V, 1));
-    if ((int64_t)K * tb > 63)
-      throw Error(SME_ENOTIMPL, "K * ceil(log2(V)) > 63: k-gram keys do not fit 64 bits");
+    const bool ranked = (int64_t)K * tb > 63 || cx->opt_kgram_rank;  // keys by iterated ranking (k_gram_round_*)
     const unsigned g_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
     int64_t *tcnt = W[W_T2].as<int64_t>(nR + 1), *toff = W[W_T3].as<int64_t>(nR + 1);
     if (nR > 0) hipLaunchKernelGGL(k_tcount, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, tcnt);
@@ -3532,24 +3583,59 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     const int64_t M = d2h(toff + nR, st);
     int32_t *tstream = W[W_U16].as<int32_t>(M + 1);
     if (nR > 0) hipLaunchKernelGGL(k_twrite, dim3(g_grid), dim3(kAggNT), 0, st, ai, nR, toff, tstream);
+    const uint32_t *pos_key = nullptr;
+    const uint32_t *grep = nullptr;  // ranked: one position of every gram id
+    int64_t Vr = 0;                  // ranked: distinct k-grams
+    if (ranked && M > 0) {
+      if (M > 0xFFFFFFFFll) throw Error(SME_ELIMIT, "k-gram ranking of more than 2^32 term positions");
+      uint64_t *ka = W[W_FKEYS].as<uint64_t>(M + 1), *kb = W[W_OVFKEY].as<uint64_t>(M + 1);
+      uint32_t *pa = W[W_FREPS].as<uint32_t>(M + 1), *pb = W[W_RREPS].as<uint32_t>(M + 1);
+      uint32_t *ra = W[W_RKEYS].as<uint32_t>(M + 1), *rb = W[W_CSTR].as<uint32_t>(M + 1);
+      uint32_t *head = W[W_RLIST].as<uint32_t>(M + 2), *excl = W[W_POFF].as<uint32_t>(M + 2);
+      uint32_t *rep = W[W_SEGB].as<uint32_t>(M + 1);
+      uint32_t *rscr = W[W_RADIX].as<uint32_t>(kv_sort_scratch(M) / sizeof(uint32_t) + 1);
+      const uint32_t *rprev = nullptr;
+      int64_t nprev = V;  // distinct (j-1)-grams: the ranks' range
+      for (int j = 2; j <= K; j++) {
+        hipLaunchKernelGGL(k_gram_round_keys, dim3(g_grid), dim3(kAggNT), 0, st, tstream, toff, nR, j, tb, rprev, ka,
+                           pa);
+        const int kbits = std::min(64, bits_for((uint64_t)std::max<int64_t>(nprev, 1)) + tb + 1);
+        uint32_t *ps = kv_sort<uint64_t>(ka, pa, kb, pb, M, kbits, rscr, st, true);
+        const uint64_t *ks = ps == pa ? ka : kb;
+        hipLaunchKernelGGL(k_gram_round_heads, dim3(grid_for(M)), dim3(256), 0, st, ks, M, head);
+        SME_HIP(hipMemsetAsync(head + M, 0, sizeof(uint32_t), st));
+        excl_scan(head, excl, M + 1, cx->ws[23], st);
+        uint32_t *rnew = (rprev == ra) ? rb : ra;
+        hipLaunchKernelGGL(k_gram_round_scatter, dim3(grid_for(M)), dim3(256), 0, st, ks, ps, head, excl, M, rnew,
+                           j == K ? rep : nullptr);
+        SME_CHECK_LAUNCH();
+        nprev = (int64_t)d2h(excl + M, st);
+        rprev = rnew;
+      }
+      pos_key = rprev;
+      grep = rep;
+      Vr = nprev;
+    }
     int64_t *pcount = W[W_T1].as<int64_t>(nR + 1), *pair_off = W[W_T0].as<int64_t>(nR + 1);
     uint8_t *bigf = W[W_SLOW].as<uint8_t>(nR + 1);
     if (nR > 0)
       hipLaunchKernelGGL(k_gram_agg<false>, dim3(g_grid), dim3(kAggNT), 0, st, tstream, toff, nR, perm, docno, K, tb,
-                         pcount, bigf, nullptr, nullptr, nullptr);
+                         pcount, bigf, nullptr, nullptr, nullptr, pos_key);
     SME_HIP(hipMemsetAsync(pcount + nR, 0, sizeof(int64_t), st));
     excl_scan(pcount, pair_off, (int64_t)(nR + 1), cx->ws[23], st);
     const int64_t Pg = d2h(pair_off + nR, st);
     uint64_t *pkey = W[W_KHI].as<uint64_t>(Pg + 1), *pval0 = W[W_KLO].as<uint64_t>(Pg + 1);
     if (nR > 0)
       hipLaunchKernelGGL(k_gram_agg<true>, dim3(g_grid), dim3(kAggNT), 0, st, tstream, toff, nR, perm, docno, K, tb,
-                         pcount, bigf, pair_off, pkey, pval0);
+                         pcount, bigf, pair_off, pkey, pval0, pos_key);
     SME_CHECK_LAUNCH();
     // sort pairs by gram key (stable: docno order within a gram)
     uint64_t *pkey_s = W[W_CKEY].as<uint64_t>(Pg + 1);
     p_val = W[W_PVAL].as<uint64_t>(Pg + 1);
     if (Pg > 0) {
-      sort_pairs_v64<uint64_t>(pkey, pkey_s, pval0, p_val, Pg, K * tb, cx->ws[120], cx->ws[121], cx->ws[122], st);
+      sort_pairs_v64<uint64_t>(pkey, pkey_s, pval0, p_val, Pg,
+                               ranked ? bits_for((uint64_t)std::max<int64_t>(Vr, 1)) : K * tb, cx->ws[120],
+                               cx->ws[121], cx->ws[122], st);
     }
     uint32_t *gflag = W[W_VSLOT].as<uint32_t>(Pg + 1), *gincl = W[W_VIDX].as<uint32_t>(Pg + 2);
     p_term = W[W_PTERM].as<uint32_t>(Pg + 1);
@@ -3562,7 +3648,12 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       gincl += 1;
       Vg = (int64_t)d2h(gincl + Pg - 1, st);
       int32_t *gcomp = ix->d_gram.as<int32_t>(Vg * K + 1);
-      hipLaunchKernelGGL(k_gram_ids, dim3(grid_for(Pg)), dim3(256), 0, st, pkey_s, gincl, Pg, K, tb, p_term, gcomp);
+      // (ranked: the keys are the gram ids themselves, the components come from
+      // one occurrence of each gram)
+      hipLaunchKernelGGL(k_gram_ids, dim3(grid_for(Pg)), dim3(256), 0, st, pkey_s, gincl, Pg, ranked ? 0 : K, tb,
+                         p_term, gcomp);
+      if (ranked)
+        hipLaunchKernelGGL(k_gram_comp_rep, dim3(grid_for(Vg)), dim3(256), 0, st, grep, Vg, K, tstream, gcomp);
       SME_CHECK_LAUNCH();
     } else {
       ix->d_gram.get(16);

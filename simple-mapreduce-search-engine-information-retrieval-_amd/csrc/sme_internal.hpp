@@ -49,6 +49,7 @@ struct sme_ctx {
   int64_t opt_raw_load_pct = 40;  // "raw_load_pct": raw-vocabulary table load of the next build (10..90)
   int64_t opt_cand_cap = 1024;    // "cand_cap": candidate list per query of k_query_win (1..2048; >= 1024: at least 16 k)
   int64_t opt_seed_m = 64;        // "seed_m": seed postings per term (k_query_seed; 0 = no seed)
+  int64_t opt_kgram_rank = 0;     // "kgram_rank": 1 = K >= 2 gram keys by iterated ranking even when packed ids fit
   int64_t opt_win_slice = 256;    // "win_slice": queries per k_query_win workgroup slice (>= 1)
   int64_t opt_win_sample = 1;     // "win_sample": 1 = every 8th window first, thresholds raised, then the rest
   int64_t opt_query_budget = 0;  // "query_table_budget": per-batch skip-table bytes (0: a quarter of free HBM)
@@ -223,6 +224,12 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
 void tokenize_string(sme_ctx *cx, const uint8_t *h_utf8, size_t n, std::vector<std::vector<uint16_t>> &out,
                      hipStream_t st);
 void term_fingerprints(sme_index *ix, uint64_t *d_out, hipStream_t st);
+// multi-GPU df exchange steps (sme_dfx.hip): owner grouping, owner sums, return gather
+void dfx_pack(sme_ctx *cx, const uint64_t *fp, const int64_t *df, int64_t n, int world, uint64_t *sfp, int64_t *sdf,
+              int64_t *pos, int64_t *h_counts, hipStream_t st);
+void dfx_sum(sme_ctx *cx, const uint64_t *fp, const int64_t *df, int64_t n, int64_t *out, int64_t *h_distinct,
+             hipStream_t st);
+void dfx_unpack(const int64_t *ret, const int64_t *pos, int64_t n, int64_t *out, hipStream_t st);
 void lookup_terms(sme_index *ix, const std::vector<std::vector<uint16_t>> &terms, int32_t *ids,
                   hipStream_t st);
 }  // namespace sme

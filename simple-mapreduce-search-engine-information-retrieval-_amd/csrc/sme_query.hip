@@ -1196,10 +1196,10 @@ __global__ void k_query_desc(const int32_t *terms, int64_t n, int64_t V, const i
     out[i] = d;
   }
 }
-__global__ void k_query_pos(const int32_t *qorder, const int64_t *qoff, int nq, QPos *out) {
+__global__ void k_query_pos(const int32_t *qorder, const int64_t *qoff, int nq, int64_t tbase, QPos *out) {
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < nq; p += gridDim.x * blockDim.x) {
     const int q = qorder ? qorder[p] : p;
-    out[p] = QPos{qoff[q], q, (int32_t)(qoff[q + 1] - qoff[q])};
+    out[p] = QPos{qoff[q] - tbase, q, (int32_t)(qoff[q + 1] - qoff[q])};
   }
 }
 // Streamed records (term / position records, thresholds): every window pass
@@ -1254,6 +1254,7 @@ struct QSeedArgs {
   const double *lut;
   const uint8_t *tfrow;           // [H][hstride] tf bytes at docno - dmin
   int64_t hstride, dmin;
+  int64_t tbase;                  // desc[i] describes term d_terms[tbase + i]
   int nq, k, M;
   double *th0;
   uint64_t *thk;  // key part of the threshold: kNoKey (every key passes at th0)
@@ -1267,7 +1268,7 @@ __global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
   for (int q = blockIdx.x; q < a.nq; q += gridDim.x) {
     const int64_t q0 = a.qoff[q];
     const int nt = (int)(a.qoff[q + 1] - q0);
-    const QDesc D = ld_desc(a.desc, q0, nt, lane);
+    const QDesc D = ld_desc(a.desc, q0 - a.tbase, nt, lane);
     const uint64_t am = (uint64_t)__ballot(D.mdf > 0);
     const uint64_t hm = (uint64_t)__ballot(D.hr >= 0);
     for (int i = lane; i < kSeedSlots; i += 64) {
@@ -2122,9 +2123,12 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       size_t fr = 0, tot = 0;
       SME_HIP(hipMemGetInfo(&fr, &tot));
       const bool winp = cx->opt_query_kernel == 0;
-      const double need = (double)nrows * (double)((winp ? (T >> 2) : T) + 1) * 4.0;
-      const double budget = cx->opt_query_budget > 0 ? (double)cx->opt_query_budget
-                                                     : (double)fr / 4.0 + (double)W[winp ? 31 : 60].cap;
+      // (the window path holds two tables of this size: the row-major change
+      // points W[29] and the window-major skip table W[31])
+      const double need = (double)nrows * (double)((winp ? (T >> 2) : T) + 1) * 4.0 * (winp ? 2.0 : 1.0);
+      const double budget = cx->opt_query_budget > 0
+                                ? (double)cx->opt_query_budget
+                                : (double)fr / 4.0 + (winp ? (double)W[31].cap + (double)W[29].cap : (double)W[60].cap);
       if (need > budget && nq > 1) {
         SME_HIP(hipEventDestroy(ep));
         QTimes acc;
@@ -2266,18 +2270,25 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   };
   const bool win = tiled && cx->opt_query_kernel == 0;
   int64_t n_ovf = 0;
+  bool subset_ran = false;  // the overflow fallback answered queries as nested compact batches
+  QTimes sub_times;
   if (win) {
     // per-batch records: term descriptors (batch term order), position records (query order)
-    int64_t nterm = 0;
+    // the batch's terms are d_terms[tbase, nterm): a sub-batch of a split keeps
+    // absolute offsets, so descriptors cover only its own terms and every record
+    // indexes them relative to tbase (QPos.q0, QSeedArgs.tbase)
+    int64_t nterm = 0, tbase = 0;
     SME_HIP(hipMemcpyAsync(&nterm, d_qoff + nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipMemcpyAsync(&tbase, d_qoff, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
-    QDesc *qdesc = reinterpret_cast<QDesc *>(W[34].as<uint4>(2 * (size_t)std::max<int64_t>(nterm, 1)));
+    const int64_t nbt = nterm - tbase;
+    QDesc *qdesc = reinterpret_cast<QDesc *>(W[34].as<uint4>(2 * (size_t)std::max<int64_t>(nbt, 1)));
     QPos *qpos = reinterpret_cast<QPos *>(W[33].as<uint4>((size_t)nq));
-    if (nterm > 0)
-      hipLaunchKernelGGL(k_query_desc, dim3((unsigned)std::min<int64_t>((nterm + 255) / 256, 8192)), dim3(256), 0, st,
-                         d_terms, nterm, V, off, idf, row_of, qa.hrow_of, qdesc);
+    if (nbt > 0)
+      hipLaunchKernelGGL(k_query_desc, dim3((unsigned)std::min<int64_t>((nbt + 255) / 256, 8192)), dim3(256), 0, st,
+                         d_terms + tbase, nbt, V, off, idf, row_of, qa.hrow_of, qdesc);
     hipLaunchKernelGGL(k_query_pos, dim3((unsigned)std::min((nq + 255) / 256, 8192)), dim3(256), 0, st, qord, d_qoff,
-                       nq, qpos);
+                       nq, tbase, qpos);
     SME_CHECK_LAUNCH();
     SME_HIP(hipEventRecord(e0, st));
     // 1. seed thresholds
@@ -2292,6 +2303,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     sa.tfrow = ix->q_tfrow;
     sa.hstride = T << kQB;
     sa.dmin = ix->dmin;
+    sa.tbase = tbase;
     sa.nq = nq;
     sa.k = k;
     sa.M = (int)std::min<int64_t>(std::max<int64_t>(cx->opt_seed_m, cx->opt_seed_m > 0 ? 2 * (int64_t)k : 0),
@@ -2396,7 +2408,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
         hipLaunchKernelGGL(k_reset_cnt, dim3((unsigned)std::min((n_round + 255) / 256, 4096)), dim3(256), 0, st,
                            round_list, n_round, ccnt, oflag);
         hipLaunchKernelGGL(k_query_pos, dim3((unsigned)std::min((n_round + 255) / 256, 8192)), dim3(256), 0, st,
-                           round_list, d_qoff, n_round, qpos);
+                           round_list, d_qoff, n_round, tbase, qpos);
       }
       wa.nq = n_round;
       wa.nslices = (int)std::max<int64_t>(1, std::min<int64_t>(n_round / cx->opt_win_slice, 4096));
@@ -2454,13 +2466,19 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
         std::vector<int32_t> hl((size_t)n_round);
         SME_HIP(hipMemcpyAsync(hl.data(), round_list, n_round * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         SME_HIP(hipStreamSynchronize(st));
+        // the nested calls store their own timings in the context: collected
+        // here and added to this call's below (with the split flag)
+        subset_ran = true;
         if (n_round < nq) {
           query_subset(ix, d_terms, d_qoff, nq, hl.data(), n_round, k, d_out_docno, d_out_score, d_out_tie, st);
+          sub_times.add(cx);
         } else {  // every query of the batch: two compact halves (each recursion has fewer queries)
           const int h = n_round / 2;
           query_subset(ix, d_terms, d_qoff, nq, hl.data(), h, k, d_out_docno, d_out_score, d_out_tie, st);
+          sub_times.add(cx);
           query_subset(ix, d_terms, d_qoff, nq, hl.data() + h, n_round - h, k, d_out_docno, d_out_score, d_out_tie,
                        st);
+          sub_times.add(cx);
         }
       }
     }
@@ -2514,7 +2532,14 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   cx->last_query_index_ms = tiled ? ix->q_prep_ms : 0.0f;
   cx->last_query_tiled = tiled;
   cx->last_query_name = win ? "k_query_win" : tiled ? "k_query_bm" : "k_query";
-  cx->last_query_split = false;
+  cx->last_query_split = subset_ran;
+  if (subset_ran) {  // the nested batches' kernel time (their events were not on this call's)
+    cx->last_query_ms += sub_times.ms;
+    cx->last_query_prep_ms += sub_times.prep;
+    cx->last_query_seed_ms += sub_times.seed;
+    cx->last_query_final_ms += sub_times.fin;
+    cx->last_query_total_ms += sub_times.tot;
+  }
   (void)hipEventDestroy(ep);
   for (hipEvent_t e : {e0, e1, e2, e3}) (void)hipEventDestroy(e);
   if (qstats) {

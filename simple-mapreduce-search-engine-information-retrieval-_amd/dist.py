@@ -16,7 +16,8 @@ the small global statistics and the query results:
                    returned per LOCAL term for sme_index_reweight
   global_df_index  the same for a libsme shard, keyed by 128-bit device term
                    fingerprints, exchanged by owner rank (df_exchange: all_to_all
-                   to the owner, dedup of 1/W of the terms, all_to_all back)
+                   to the owner, sums of 1/W of the terms, all_to_all back; the
+                   local steps are libsme kernels, sme_df_owner_*)
   reference_partitions  the reference's R term-partitioned part files from the
                    shards: all_to_all of per-owner term/postings blobs, per-term
                    reducer merge on the owner (sme_merge_pieces)
@@ -141,73 +142,90 @@ def global_df(local_df, l2g, n_global_terms, group=None):
     return g[torch.from_numpy(l2g).to(dev)] if len(l2g) else g[:0]
 
 
-def _unique_rows(fp):
-    """(unique rows, inverse) of an int64 [n, 2] fingerprint tensor.  Sorts on the
-    first word only (a 1-D unique is far cheaper than unique(dim=0)); rows whose
-    first words agree but second words differ (2^-64 per pair) take the exact
-    row-wise unique instead."""
-    if fp.shape[0] == 0:
-        return fp, torch.zeros(0, dtype=torch.int64, device=fp.device)
-    u0, inv = torch.unique(fp[:, 0], return_inverse=True)
-    lo = torch.full((u0.shape[0],), torch.iinfo(torch.int64).max, dtype=torch.int64, device=fp.device)
-    hi = torch.full((u0.shape[0],), torch.iinfo(torch.int64).min, dtype=torch.int64, device=fp.device)
-    lo.scatter_reduce_(0, inv, fp[:, 1], "amin")
-    hi.scatter_reduce_(0, inv, fp[:, 1], "amax")
-    if bool((lo != hi).any()):
-        return torch.unique(fp, dim=0, return_inverse=True)
-    return torch.stack([u0, lo], 1), inv
+class DeviceDfOps:
+    """The df exchange's local steps on the device, in libsme (sme_dfx.hip):
+    owner grouping (counting scatter), owner sums (fingerprint hash table) and
+    the return gather.  Tensors are CUDA tensors; libsme runs them on the
+    context's own stream, synchronized before torch reads the results."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def pack(self, fp, df, world):
+        n = int(fp.shape[0])
+        sfp = torch.empty((max(n, 1), 2), dtype=torch.int64, device=fp.device)
+        sdf = torch.empty(max(n, 1), dtype=torch.int64, device=fp.device)
+        pos = torch.empty(max(n, 1), dtype=torch.int64, device=fp.device)
+        fp, df = fp.contiguous(), df.contiguous()
+        torch.cuda.synchronize()
+        counts = self.ctx.df_owner_pack(fp.data_ptr(), df.data_ptr(), n, world, sfp.data_ptr(), sdf.data_ptr(),
+                                        pos.data_ptr())
+        return sfp[:n], sdf[:n], pos[:n], counts
+
+    def owner_sum(self, fp, df):
+        n = int(fp.shape[0])
+        out = torch.empty(max(n, 1), dtype=torch.int64, device=fp.device)
+        fp, df = fp.contiguous(), df.contiguous()
+        torch.cuda.synchronize()
+        distinct = self.ctx.df_owner_sum(fp.data_ptr(), df.data_ptr(), n, out.data_ptr())
+        return out[:n], distinct
+
+    def unpack(self, ret, pos):
+        n = int(pos.shape[0])
+        out = torch.empty(max(n, 1), dtype=torch.int64, device=pos.device)
+        ret = ret.contiguous()
+        torch.cuda.synchronize()
+        if n:
+            self.ctx.df_owner_unpack(ret.data_ptr(), pos.data_ptr(), n, out.data_ptr())
+        return out[:n]
 
 
-def df_exchange(fp, df, group=None, timings=None):
+def df_exchange(fp, df, group=None, timings=None, ops=None):
     """Global df per local term, keyed by term fingerprints (int64 [V, 2]; df int64
-    [V], on the collective's device).  Each fingerprint has ONE owner rank
-    (first word mod W): one all_to_all sends every local (fingerprint, df) to its
-    owner, each owner deduplicates and sums only the ~1/W of the terms it owns,
-    and a second all_to_all returns the summed df to the senders.  Per rank that
-    moves 24 B per local term out and 8 B back, and sorts ~(sum of shard
-    vocabularies) / W rows -- where an all_gather + unique on every rank would
-    move and sort all of them (the reducer's view of df, TermKGramDocIndexer.java
-    :175-183, is the postings length summed over the map outputs)."""
+    [V]).  Each fingerprint has ONE owner rank (first word, as u64, mod W): one
+    all_to_all sends every local (fingerprint, df) to its owner, each owner sums
+    only the ~1/W of the terms it owns, and a second all_to_all returns the summed
+    df to the senders.  Per rank that moves 24 B per local term out and 8 B back,
+    and groups ~(sum of shard vocabularies) / W rows -- where an all_gather +
+    unique on every rank would move and sort all of them (the reducer's view of
+    df, TermKGramDocIndexer.java:175-183, is the postings length summed over the
+    map outputs).  The local steps are `ops` (pack / owner_sum / unpack):
+    DeviceDfOps (libsme kernels, the product) -- there is no host path; the CPU
+    tests pass a numpy restatement of the same three steps."""
     import time
+    if ops is None:
+        raise ValueError("df_exchange needs its local steps (DeviceDfOps(ctx) on a GPU)")
     world = dist.get_world_size(group)
-    dev = fp.device
+    cdev = _dev(group)
     V = int(fp.shape[0])
     t0 = time.perf_counter()
-    owner = torch.remainder(fp[:, 0], world) if V else torch.zeros(0, dtype=torch.int64, device=dev)
-    order = torch.argsort(owner, stable=True)
-    send_fp = fp[order].contiguous()
-    send_df = df[order].contiguous()
-    counts = torch.bincount(owner, minlength=world).to(torch.int64)
+    send_fp, send_df, pos, cs = ops.pack(fp, df, world)
+    counts = torch.tensor(cs, dtype=torch.int64, device=cdev)
     rcounts = torch.empty_like(counts)
     dist.all_to_all_single(rcounts, counts, group=group)
-    cs, rc = counts.tolist(), rcounts.tolist()
+    rc = rcounts.tolist()
     nrecv = int(sum(rc))
-    recv_fp = torch.empty((nrecv, 2), dtype=torch.int64, device=dev)
-    recv_df = torch.empty(nrecv, dtype=torch.int64, device=dev)
-    dist.all_to_all_single(recv_fp.view(-1), send_fp.view(-1), [2 * c for c in rc], [2 * c for c in cs], group=group)
-    dist.all_to_all_single(recv_df, send_df, rc, cs, group=group)
-    if dev.type == "cuda":
+    recv_fp = torch.empty((nrecv, 2), dtype=torch.int64, device=cdev)
+    recv_df = torch.empty(nrecv, dtype=torch.int64, device=cdev)
+    dist.all_to_all_single(recv_fp.view(-1), send_fp.to(cdev).contiguous().view(-1), [2 * c for c in rc],
+                           [2 * c for c in cs], group=group)
+    dist.all_to_all_single(recv_df, send_df.to(cdev).contiguous(), rc, cs, group=group)
+    if cdev.type == "cuda":
         torch.cuda.synchronize()
     t1 = time.perf_counter()
-    uniq, inv = _unique_rows(recv_fp)
-    g = torch.zeros(uniq.shape[0], dtype=torch.int64, device=dev)
-    g.index_add_(0, inv, recv_df)
-    back = g[inv].contiguous()
-    n_owned = torch.tensor([int(uniq.shape[0])], dtype=torch.int64, device=dev)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
+    back, n_owned_local = ops.owner_sum(recv_fp.to(fp.device), recv_df.to(fp.device))
+    n_owned = torch.tensor([int(n_owned_local)], dtype=torch.int64, device=cdev)
     t2 = time.perf_counter()
-    ret = torch.empty(V, dtype=torch.int64, device=dev)
-    dist.all_to_all_single(ret, back, cs, rc, group=group)
+    ret = torch.empty(V, dtype=torch.int64, device=cdev)
+    dist.all_to_all_single(ret, back.to(cdev).contiguous(), cs, rc, group=group)
     dist.all_reduce(n_owned, group=group)
-    out = torch.empty(V, dtype=torch.int64, device=dev)
-    out[order] = ret
-    if dev.type == "cuda":
+    out = ops.unpack(ret.to(fp.device), pos)
+    if fp.device.type == "cuda":
         torch.cuda.synchronize()
     t3 = time.perf_counter()
     if timings is not None:
         timings.update(exchange_ms=(t1 - t0) * 1e3, dedup_ms=(t2 - t1) * 1e3, return_ms=(t3 - t2) * 1e3,
-                       local_terms=V, owned_rows=nrecv, owned_terms=int(uniq.shape[0]),
+                       local_terms=V, owned_rows=nrecv, owned_terms=int(n_owned_local),
                        global_terms=int(n_owned.item()), bytes_out_per_rank=24 * V, bytes_back_per_rank=8 * V)
     return out
 
@@ -238,10 +256,10 @@ def global_df_index(ix, group=None, timings=None):
         sme.memcpy(offs.data_ptr(), o_ptr, 8 * (V + 1), None)
     else:
         offs.zero_()
-    df = (offs[1:] - offs[:-1]).to(dev)
-    fp = fp[:V].to(dev)
+    df = offs[1:] - offs[:-1]
+    fp = fp[:V]
     t1 = time.perf_counter()
-    out = df_exchange(fp, df, group, timings)
+    out = df_exchange(fp, df, group, timings, ops=DeviceDfOps(ix.ctx))
     out = out.to("cuda").contiguous()
     torch.cuda.current_stream().synchronize()
     if timings is not None:

@@ -138,6 +138,36 @@ def test_cuts_own_every_record_and_quirks():
             assert got == recs, w
 
 
+class HostDfOps:
+    """numpy restatement of dist.DeviceDfOps' three local steps (sme_dfx.hip),
+    so the CPU tests drive dist.df_exchange's collectives without a GPU: owner =
+    fingerprint word 0 as u64 mod world, rows grouped by owner; per received row
+    the df summed over its 128-bit fingerprint; the return gather."""
+
+    def pack(self, fp, df, world):
+        f = fp.numpy()
+        owner = (f[:, 0].view(np.uint64) % np.uint64(world)).astype(np.int64)
+        order = np.argsort(owner, kind="stable")
+        pos = np.empty(len(order), np.int64)
+        pos[order] = np.arange(len(order))
+        counts = np.bincount(owner, minlength=world).tolist()
+        return (torch.from_numpy(f[order].copy()), torch.from_numpy(df.numpy()[order].copy()),
+                torch.from_numpy(pos), counts)
+
+    def owner_sum(self, fp, df):
+        f = fp.numpy()
+        if len(f) == 0:
+            return torch.zeros(0, dtype=torch.int64), 0
+        _, inv = np.unique(f, axis=0, return_inverse=True)
+        inv = inv.reshape(-1)
+        sums = np.zeros(int(inv.max()) + 1, np.int64)
+        np.add.at(sums, inv, df.numpy())
+        return torch.from_numpy(sums[inv]), len(sums)
+
+    def unpack(self, ret, pos):
+        return torch.from_numpy(ret.numpy()[pos.numpy()].copy())
+
+
 def _dfx_worker(rank, world, port, out_dir, collide):
     """df_exchange over random shard vocabularies: every local term's result must be
     the df summed over every shard holding its fingerprint."""
@@ -156,7 +186,8 @@ def _dfx_worker(rank, world, port, out_dir, collide):
             shards.append((ids, gr.integers(1, 50, size=ids.shape[0]).astype(np.int64)))
         ids, df = shards[rank]
         t = {}
-        out = D.df_exchange(torch.from_numpy(universe[ids].copy()), torch.from_numpy(df), timings=t).numpy()
+        out = D.df_exchange(torch.from_numpy(universe[ids].copy()), torch.from_numpy(df), timings=t,
+                            ops=HostDfOps()).numpy()
         want = {}
         for i2, d2 in shards:
             for i, d in zip(i2.tolist(), d2.tolist()):

@@ -36,10 +36,12 @@ def test_device_process_content_fuzz(ctx):
         assert ctx.process_content(doc) == O.process_content(doc), doc
 
 
-def _check_build(sme, corpus, mapping_ids, R=1, idf_mode=0, K=1, tiebreak=0):
+def _check_build(sme, corpus, mapping_ids, R=1, idf_mode=0, K=1, tiebreak=0, opts=None):
     mb = O.write_mapping(mapping_ids)
     ref = O.OracleIndex(corpus, mb, K, R)
     ctx = sme.Context(K, R, idf_mode, tiebreak=tiebreak)
+    for name, v in (opts or {}).items():
+        ctx.set_option(name, v)
     ctx.load_docno_mapping(mb)
     ix = ctx.build(corpus)
     assert ix.N == ref.N
@@ -135,6 +137,18 @@ def test_build_high_tf(sme, dup):
         docs.append(b"<DOC>\n<DOCNO>" + did.encode() + b"</DOCNO>\n" + " ".join(words).encode() + b"\n</DOC>\n")
     ix, _ = _check_build(sme, b"".join(docs), sorted(set(ids)), R=3)
     assert int(ix.csr()[2].max()) > 1023
+
+
+def test_build_dotted_token_tf_past_u16(sme):
+    """One dotted non-acronym raw token that splits into > 65535 copies of one
+    term (TagTokenizer.tokenAcronymProcessing's split branch, TagTokenizer.java:
+    508-522): the record has few raw tokens but a tf past the per-wave u16
+    counters, so the aggregation must bound the term count, not the token count."""
+    dotted = ".".join(["ab"] * 70000) + "." + ".".join(["cd"] * 3)
+    docs = [b"<DOC>\n<DOCNO>X00</DOCNO>\nalpha beta " + dotted.encode() + b" gamma\n</DOC>\n",
+            b"<DOC>\n<DOCNO>X01</DOCNO>\nab cd ab alpha\n</DOC>\n"]
+    ix, _ = _check_build(sme, b"".join(docs), ["X00", "X01"], R=3)
+    assert int(ix.csr()[2].max()) == 70000
 
 
 def test_build_many_tiny_records(sme):
@@ -384,6 +398,27 @@ def test_build_kgram_fuzz(sme, seed):
     corpus += b"<DOC><DOCNO>" + ids[0].encode() + b"</DOCNO>" + big + b"</DOC>"
     _check_build(sme, corpus, ids, R=1, K=2)
     _check_build(sme, corpus, ids, R=3, K=2)
+
+
+@pytest.mark.parametrize("K,R", [(2, 10), (3, 4), (5, 3)])
+def test_build_kgram_ranked_keys(sme, synth, K, R):
+    """The iterated-ranking gram keys (the path of K * ceil(log2 V) > 63, forced
+    here by the kgram_rank option on a small vocabulary): byte-equal records."""
+    n = 250
+    c = synth.gen_corpus(n, V=600, seed=21, len_lo=1, len_hi=60)
+    _check_build(sme, c, synth.docids(n), R=R, K=K, opts={"kgram_rank": 1})
+    corpus, ids = common.fuzz_corpus(4, 100)
+    _check_build(sme, corpus, ids, R=3, K=2, opts={"kgram_rank": 1})
+
+
+def test_build_kgram_wide_vocabulary(sme, synth):
+    """K = 4 over 1,500 documents of the c2 distribution (V ~ 2e5 terms: 4 x 18
+    bits > 63, so the packed term-id keys cannot hold a gram and the device ranks
+    them): records byte-equal to the oracle's TermKGramDocIndexer at R = 10."""
+    n = 1500
+    c = synth.gen_corpus(n, V=1 << 20, seed=42, len_lo=400, len_hi=600)
+    ix, _ = _check_build(sme, c, synth.docids(n), R=10, K=4)
+    assert ix.V > 100000
 
 
 def test_kgram_queries_first_element_lookup(sme, synth):

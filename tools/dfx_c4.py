@@ -4,8 +4,9 @@ c4 is 50 M docs doc-sharded over 8 GPUs: one shard is 6.25 M docs of
 the c4 distribution (V_w = 2^22, 200-360 tokens, Zipf s = 1, seed 44) with about
 6.8 M local terms (the words it holds + its 6.25 M docid terms).  This builds
 such a shard in HBM, runs the real global_df_index on a world-1 RCCL group
-(fingerprints + offsets, gather, unique, reduce), and then times the part that
-grows with the world on the device: the owner's unique + index_add + gather over the
+(fingerprints + offsets, owner pack, all_to_all, owner sums, return), and then
+times the part that grows with the world on the device: the owner's sums
+(sme_df_owner_sum, a fingerprint hash table) over the
 8-shard set, emulated from this shard's own fingerprints (rows with df > 1 --
 the words -- shared by all 8 shards, the df = 1 rows -- docid terms and rare
 words -- made shard-private by xoring the shard number into the fingerprint):
@@ -78,31 +79,29 @@ def main():
     allfp = torch.cat(parts, 0)
     alldf = torch.cat(dfs, 0)
     del parts, dfs
-    mine = torch.remainder(allfp[:, 0], a.world) == 0
+    # the owner of a row: word 0 as u64 mod W (sme_df_owner_pack's rule)
+    w0 = allfp[:, 0]
+    u_mod = (torch.remainder(w0, a.world) + torch.where(w0 < 0, (1 << 64) % a.world, 0)) % a.world
+    mine = u_mod == 0
     recv_fp = allfp[mine].contiguous()
     recv_df = alldf[mine].contiguous()
-    del allfp, alldf
+    del allfp, alldf, w0, u_mod
+    ops = D.DeviceDfOps(ctx)
     send_t, owner_t = [], []
     for _ in range(3):
         torch.cuda.synchronize()
         ts = time.perf_counter()
-        owner = torch.remainder(fp[:, 0], a.world)
-        order = torch.argsort(owner, stable=True)
-        send_fp = fp[order].contiguous()
-        send_df = df[order].contiguous()
+        send_fp, send_df, pos, counts = ops.pack(fp, df, a.world)  # libsme sme_df_owner_pack
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        uniq, inv = D._unique_rows(recv_fp)
-        g = torch.zeros(uniq.shape[0], dtype=torch.int64, device="cuda")
-        g.index_add_(0, inv, recv_df)
-        back = g[inv].contiguous()
+        back, n_owned = ops.owner_sum(recv_fp, recv_df)  # libsme sme_df_owner_sum
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         send_t.append((t1 - ts) * 1e3)
         owner_t.append((t2 - t1) * 1e3)
     out["emulated_world"] = a.world
     out["emulated_rows_received_by_owner"] = int(recv_fp.shape[0])
-    out["emulated_terms_owned"] = int(uniq.shape[0])
+    out["emulated_terms_owned"] = int(n_owned)
     out["emulated_send_prep_ms"] = round(min(send_t), 3)
     out["emulated_owner_dedup_reduce_ms"] = round(min(owner_t), 3)
     out["all_to_all_bytes_out_per_rank"] = int(24 * V)
@@ -110,7 +109,7 @@ def main():
     out["private_terms"] = int(private.sum().item())
     out["what"] = ("world-1 global_df_index at c4 shard size (real path), then the owner side of dist.df_exchange "
                    "for an emulated %d-shard set (df>1 rows shared, df=1 rows shard-private): one owner's received "
-                   "rows (1/%d of every shard's) deduplicated + summed, and the sender's owner sort; the two "
+                   "rows (1/%d of every shard's) summed per fingerprint (sme_df_owner_sum), and the sender's owner pack (sme_df_owner_pack); the two "
                    "all_to_alls need %d GPUs and are reported as bytes" % (a.world, a.world, a.world))
     res = back
     del res, gdf

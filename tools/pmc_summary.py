@@ -18,6 +18,20 @@ import os
 import sys
 
 
+def base_name(n):
+    """Kernel name without return type, template arguments or parameter list:
+    'void k_query_win<true>(Args)' -> 'k_query_win'.  Kernels are matched on this
+    EXACTLY (k_query must not collect k_query_win / k_query_seed / ...)."""
+    n = n.strip()
+    if n.startswith("void "):
+        n = n[5:]
+    for c in "(<":
+        i = n.find(c)
+        if i >= 0:
+            n = n[:i]
+    return n.strip()
+
+
 def per_kernel(d, counter):
     """{kernel name: [value per dispatch]} in dispatch order.  SME_PMC_BATCHES=n keeps
     only the dispatches before the (n+1)-th k_query_seed (the bench's headline query
@@ -30,9 +44,9 @@ def per_kernel(d, counter):
     out, seeds = {}, 0
     for r in rows:
         name = r["Kernel_Name"]
-        if "k_query_seed" in name:
+        if base_name(name) == "k_query_seed":
             seeds += 1
-        if nb and seeds > nb and "k_query" in name:
+        if nb and seeds > nb and base_name(name).startswith("k_query"):
             continue
         out.setdefault(name, []).append(float(r["Counter_Value"]))
     return out
@@ -40,32 +54,37 @@ def per_kernel(d, counter):
 
 def main():
     docs, vocab, fdir, wdir = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
-    wanted = sys.argv[5:] or ["k_tok_fast", "k_query"]
+    wanted = sys.argv[5:] or ["k_tok_fast", "k_agg_w", "k_rs_scatter", "k_query_win", "k_query_seed"]
     fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
     res = {"docs": docs, "vocab": vocab,
-           "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), mean over dispatches; separate --pmc passes",
+           "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), mean over dispatches; separate --pmc passes; "
+                     "kernels matched by exact base name (template instantiations summed per launch); "
+                     "query kernels per batch (total / k_query_seed dispatches)",
            "kernels": {}}
+    anchor = [v for n, v in fetch.items() if base_name(n) == "k_query_seed"]
     for k in wanted:
-        fk = [v for n, v in fetch.items() if k in n]
-        wk = [v for n, v in write.items() if k in n]
+        fk = [v for n, v in fetch.items() if base_name(n) == k]
+        wk = [v for n, v in write.items() if base_name(n) == k]
         if not fk or not wk:
             continue
-        # template instantiations of one kernel (e.g. the query kernel's register
-        # and LDS paths) are launched together: a "launch" is the sum of their means
-        # a kernel launched several times per batch (k_query_win: sample windows,
-        # the rest, overflow rounds) counts per batch: total / k_query_seed dispatches
-        anchor = [v for n, v in fetch.items() if "k_query_seed" in n] if "k_query_win" in k else []
-        if anchor:
+        # template instantiations of one kernel are launched together: a "launch"
+        # is the sum of their means.  A query kernel launched several times per
+        # batch (k_query_win: window stages, overflow rounds) counts per batch:
+        # total / k_query_seed dispatches
+        if k.startswith("k_query") and anchor:
             nb = len(anchor[0])
             f = sum(sum(v) for v in fk) / nb * 1024
             w = sum(sum(v) for v in wk) / nb * 1024
         else:
             f = sum(sum(v) / len(v) for v in fk) * 1024
             w = sum(sum(v) / len(v) for v in wk) * 1024
-        res["kernels"][k] = {"fetch_bytes_raw": round(f), "write_bytes": round(w), "dispatches": len(fk[0]),
-                             "instantiations": len(fk), "hbm_bytes_per_launch": round(2 * f + w)}
+        res["kernels"][k] = {"fetch_bytes_raw": round(f), "write_bytes": round(w),
+                             "dispatches": sum(len(v) for v in fk), "instantiations": len(fk),
+                             "batches": len(anchor[0]) if (k.startswith("k_query") and anchor) else None,
+                             "hbm_bytes_per_launch": round(2 * f + w)}
     os.makedirs("profiles", exist_ok=True)
-    json.dump(res, open("profiles/pmc_traffic.json", "w"), indent=1)
+    # SME_PMC_OUT: e.g. profiles/pmc_traffic_c5.json for bench.py --config c5
+    json.dump(res, open(os.environ.get("SME_PMC_OUT", "profiles/pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
