@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <memory>
+#include <parallel/algorithm>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -172,35 +173,48 @@ bool simple_record(const uint8_t *t, int64_t n) {
 }
 
 // open-addressing table of distinct raw tokens (byte strings): lookup returns the
-// token's id (insertion order); lp / ll hold each id's bytes
+// token's id (insertion order); lp / ll hold each id's bytes.  Entries carry the
+// first 16 bytes inline (no token byte is 0, so zero padding is unambiguous):
+// tokens of <= 16 bytes compare without touching the text
 struct RawTab {
   struct E {
     uint64_t h;  // hash | 1; 0 = empty
-    const uint8_t *p;
-    int32_t len, id;
+    uint64_t w0, w1;
+    int32_t len, id;  // (a long token's bytes: lp[id])
   };
   std::vector<E> e;
   std::vector<const uint8_t *> lp;
   std::vector<int32_t> ll;
+  std::vector<uint64_t> lh;  // each id's hash (the parallel merge's shard key)
   uint64_t mask = 0;
   RawTab() { rehash(1 << 14); }
-  static uint64_t hash(const uint8_t *s, int64_t l) {
-    uint64_t x = 0x9E3779B97F4A7C15ull ^ (uint64_t)l;
-    int64_t i = 0;
-    for (; i + 8 <= l; i += 8) {
-      uint64_t w;
-      memcpy(&w, s + i, 8);
-      x = (x ^ w) * 0xFF51AFD7ED558CCDull;
-      x ^= x >> 32;
+  static inline void head(const uint8_t *s, int64_t l, uint64_t *w0, uint64_t *w1) {
+    uint64_t a = 0, b = 0;
+    if (l >= 16) {
+      memcpy(&a, s, 8);
+      memcpy(&b, s + 8, 8);
+    } else if (l >= 8) {
+      memcpy(&a, s, 8);
+      memcpy(&b, s + 8, (size_t)(l - 8));
+    } else {
+      memcpy(&a, s, (size_t)l);
     }
-    uint64_t w = 0;
-    memcpy(&w, s + i, (size_t)(l - i));
-    x = (x ^ w) * 0xC4CEB9FE1A85EC53ull;
+    *w0 = a;
+    *w1 = b;
+  }
+  static inline uint64_t hash(const uint8_t *s, int64_t l, uint64_t w0, uint64_t w1) {
+    uint64_t x = (0x9E3779B97F4A7C15ull ^ (uint64_t)l ^ w0) * 0xFF51AFD7ED558CCDull;
+    x = (x ^ (x >> 32) ^ w1) * 0xC4CEB9FE1A85EC53ull;
+    for (int64_t i = 16; i < l; i += 8) {
+      uint64_t w = 0;
+      memcpy(&w, s + i, (size_t)std::min<int64_t>(8, l - i));
+      x = (x ^ (x >> 29) ^ w) * 0xFF51AFD7ED558CCDull;
+    }
     x ^= x >> 29;
     return x | 1ull;
   }
   void rehash(uint64_t cap) {
-    std::vector<E> o(cap, E{0, nullptr, 0, 0});
+    std::vector<E> o(cap, E{0, 0, 0, 0, 0});
     for (const E &x : e) {
       if (!x.h) continue;
       uint64_t s = x.h & (cap - 1);
@@ -210,19 +224,27 @@ struct RawTab {
     e.swap(o);
     mask = cap - 1;
   }
-  int32_t lookup(const uint8_t *s, int64_t l) {
-    const uint64_t x = hash(s, l);
+  inline int32_t find_or_add(const uint8_t *s, int64_t l, uint64_t x, uint64_t w0, uint64_t w1) {
     uint64_t i = x & mask;
     while (e[i].h) {
-      if (e[i].h == x && e[i].len == l && memcmp(e[i].p, s, (size_t)l) == 0) return e[i].id;
+      const E &q = e[i];
+      if (q.h == x && q.len == l && q.w0 == w0 && q.w1 == w1 &&
+          (l <= 16 || memcmp(lp[(size_t)q.id] + 16, s + 16, (size_t)(l - 16)) == 0))
+        return q.id;
       i = (i + 1) & mask;
     }
     const int32_t id = (int32_t)lp.size();
     lp.push_back(s);
     ll.push_back((int32_t)l);
-    e[i] = E{x, s, (int32_t)l, id};
+    lh.push_back(x);
+    e[i] = E{x, w0, w1, (int32_t)l, id};
     if (2 * lp.size() > mask + 1) rehash(2 * (mask + 1));
     return id;
+  }
+  int32_t lookup(const uint8_t *s, int64_t l) {
+    uint64_t w0, w1;
+    head(s, l, &w0, &w1);
+    return find_or_add(s, l, hash(s, l, w0, w1), w0, w1);
   }
 };
 
@@ -289,6 +311,12 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   {
     const int me = omp_get_thread_num();
     RawTab &raw = tabs[(size_t)me];
+    struct Pend {
+      const uint8_t *s;
+      int64_t l;
+      uint64_t w0, w1, h;
+    };
+    std::vector<Pend> pend;
     jstr text, st;
     js_init(&text);
     js_init(&st);
@@ -333,7 +361,11 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
         // byte-level TagTokenizer (the device's fast path, sme_build.hip k_tok_fast):
         // raw tokens = maximal runs of non-split bytes starting outside every
         // tag / comment / PI / entity span
+        // two passes over the record's tokens: bounds, head words and hashes with
+        // the home slots prefetched, then the table lookups (the slots of the
+        // record's tail tokens are in flight together instead of one miss each)
         auto &out = rtok[(size_t)r];
+        pend.clear();
         int64_t i = 0;
         while (i < len) {
           const uint8_t c = b[i];
@@ -351,9 +383,18 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
           }
           int64_t j = i + 1;
           while (j < len && !split_byte(b[j])) j++;
-          out.push_back(raw.lookup(b + i, j - i));
+          Pend q;
+          q.s = b + i;
+          q.l = j - i;
+          RawTab::head(q.s, q.l, &q.w0, &q.w1);
+          q.h = RawTab::hash(q.s, q.l, q.w0, q.w1);
+          __builtin_prefetch(&raw.e[q.h & raw.mask]);
+          pend.push_back(q);
           i = j;
         }
+        out.resize(pend.size());
+        for (size_t k = 0; k < pend.size(); k++)
+          out[k] = raw.find_or_add(pend[k].s, pend[k].l, pend[k].h, pend[k].w0, pend[k].w1);
       } else {
         // complex markup: the oracle's TagTokenizer over the decoded record
         utf8_to_utf16(b, (size_t)len, &text);
@@ -374,15 +415,57 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   }
   if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "tokens", omp_get_wtime() - t0);
   if (fail) return nullptr;
-  // 2. one table of the distinct raw tokens (local id -> global id per thread)
-  RawTab glob;
+  // 2. one table of the distinct raw tokens (local id -> global id per thread):
+  // the threads' tables merged in parallel, shard s (hash bits) by one thread,
+  // global id = shard base + id inside the shard
+  constexpr int kShards = 256;
+  std::vector<RawTab> shard((size_t)kShards);
   std::vector<std::vector<int32_t>> lmap((size_t)nthr);
+  for (int t = 0; t < nthr; t++) lmap[(size_t)t].resize(tabs[(size_t)t].lp.size());
+  // every thread's ids bucketed by shard (one pass per table), so a shard visits
+  // only its own entries
+  std::vector<std::vector<std::vector<int32_t>>> bucket((size_t)nthr);
+#pragma omp parallel for schedule(dynamic, 1)
   for (int t = 0; t < nthr; t++) {
     const RawTab &tb = tabs[(size_t)t];
-    lmap[(size_t)t].resize(tb.lp.size());
-    for (size_t i = 0; i < tb.lp.size(); i++) lmap[(size_t)t][i] = glob.lookup(tb.lp[i], tb.ll[i]);
+    auto &b = bucket[(size_t)t];
+    b.assign((size_t)kShards, {});
+    for (size_t i = 0; i < tb.lp.size(); i++) b[(size_t)((tb.lh[i] >> 56) % kShards)].push_back((int32_t)i);
   }
-  const int64_t G = (int64_t)glob.lp.size();
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int sh = 0; sh < kShards; sh++) {
+    RawTab &g = shard[(size_t)sh];
+    for (int t = 0; t < nthr; t++) {
+      const RawTab &tb = tabs[(size_t)t];
+      for (const int32_t i : bucket[(size_t)t][(size_t)sh]) {
+        uint64_t w0, w1;
+        RawTab::head(tb.lp[i], tb.ll[i], &w0, &w1);
+        lmap[(size_t)t][i] = g.find_or_add(tb.lp[i], tb.ll[i], tb.lh[i], w0, w1);
+      }
+    }
+  }
+  std::vector<int64_t> sbase((size_t)kShards + 1, 0);
+  for (int sh = 0; sh < kShards; sh++) sbase[(size_t)sh + 1] = sbase[(size_t)sh] + (int64_t)shard[(size_t)sh].lp.size();
+  const int64_t G = sbase[(size_t)kShards];
+  struct GTok {
+    std::vector<const uint8_t *> lp;
+    std::vector<int32_t> ll;
+  } glob;
+  glob.lp.resize((size_t)G);
+  glob.ll.resize((size_t)G);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int sh = 0; sh < kShards; sh++)
+    for (size_t i = 0; i < shard[(size_t)sh].lp.size(); i++) {
+      glob.lp[(size_t)sbase[(size_t)sh] + i] = shard[(size_t)sh].lp[i];
+      glob.ll[(size_t)sbase[(size_t)sh] + i] = shard[(size_t)sh].ll[i];
+    }
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int t = 0; t < nthr; t++) {
+    const RawTab &tb = tabs[(size_t)t];
+    for (size_t i = 0; i < tb.lp.size(); i++) lmap[(size_t)t][i] += (int32_t)sbase[(size_t)((tb.lh[i] >> 56) % kShards)];
+  }
+  std::vector<RawTab>().swap(shard);
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "merge", omp_get_wtime() - t0);
   // processContent of each distinct raw token, once (parallel)
   std::vector<std::vector<u16s>> gout((size_t)G);
 #pragma omp parallel
@@ -440,7 +523,7 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
     for (auto &w : v) keyed.push_back(tkey(&w));
   for (auto &v : rterm)
     for (auto &w : v) keyed.push_back(tkey(&w));
-  std::sort(keyed.begin(), keyed.end(), tless);
+  __gnu_parallel::sort(keyed.begin(), keyed.end(), tless);
   std::vector<u16s> vocab;
   std::vector<TK> vk;
   for (size_t i = 0; i < keyed.size(); i++)
@@ -496,17 +579,41 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   std::vector<int64_t> order((size_t)nR);
   for (int64_t r = 0; r < nR; r++) order[(size_t)r] = r;
   std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return rdocno[(size_t)a] < rdocno[(size_t)b]; });
-  // counting sort by term: counts, prefix, scatter in docno order
-  std::vector<int64_t> cnt((size_t)V + 1, 0);
-  for (int64_t r = 0; r < nR; r++)
-    for (auto &p : rid[(size_t)r]) cnt[(size_t)p.first]++;
+  // counting sort by term, in docno order: the docno-ordered records cut into one
+  // contiguous chunk per thread; per-thread term counts, a prefix over (term,
+  // thread), then every thread scatters its chunk (the chunks' order is docno order)
   std::vector<int64_t> start((size_t)V + 1, 0);
-  for (int64_t t = 0; t < V; t++) start[(size_t)t + 1] = start[(size_t)t] + cnt[(size_t)t];
+  std::vector<std::vector<int64_t>> tcnt((size_t)nthr);
+  auto chunk_of = [&](int t) { return std::make_pair(nR * t / nthr, nR * (t + 1) / nthr); };
+#pragma omp parallel num_threads(nthr)
+  {
+    const int t = omp_get_thread_num();
+    std::vector<int64_t> &c = tcnt[(size_t)t];
+    c.assign((size_t)V, 0);
+    const auto ch = chunk_of(t);
+    for (int64_t i = ch.first; i < ch.second; i++)
+      for (auto &p : rid[(size_t)order[(size_t)i]]) c[(size_t)p.first]++;
+  }
+  {
+    int64_t acc = 0;
+    for (int64_t v = 0; v < V; v++) {
+      start[(size_t)v] = acc;
+      for (int t = 0; t < nthr; t++) {
+        const int64_t n_ = tcnt[(size_t)t][(size_t)v];
+        tcnt[(size_t)t][(size_t)v] = acc;  // this thread's first slot of term v
+        acc += n_;
+      }
+    }
+    start[(size_t)V] = acc;
+  }
   const int64_t Pm = start[(size_t)V];
   std::vector<int32_t> pd((size_t)Pm), pf((size_t)Pm);
+#pragma omp parallel num_threads(nthr)
   {
-    std::vector<int64_t> cur(start.begin(), start.end());
-    for (int64_t i = 0; i < nR; i++) {
+    const int t = omp_get_thread_num();
+    std::vector<int64_t> &cur = tcnt[(size_t)t];
+    const auto ch = chunk_of(t);
+    for (int64_t i = ch.first; i < ch.second; i++) {
       const int64_t r = order[(size_t)i];
       for (auto &p : rid[(size_t)r]) {
         const int64_t x = cur[(size_t)p.first]++;
@@ -515,6 +622,7 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
       }
     }
   }
+  std::vector<std::vector<int64_t>>().swap(tcnt);
   if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "scatter", omp_get_wtime() - t0);
   rid.clear();
   rid.shrink_to_fit();

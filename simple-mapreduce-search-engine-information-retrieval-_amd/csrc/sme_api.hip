@@ -129,7 +129,7 @@ void ensure_host_terms(sme_index *ix) {
   if (ix->h_term_off[Vt] > 0)
     SME_HIP(hipMemcpy(ix->h_term_chars.data(), ix->d_term_chars.p, ix->h_term_off[Vt] * sizeof(uint16_t),
                       hipMemcpyDeviceToHost));
-  if (ix->K > 1 && ix->V > 0) {
+  if (ix->K > 1 && ix->V > 0 && ix->d_gram.p) {  // (a merged K >= 2 index holds joined gram strings instead)
     ix->h_gram.resize((size_t)(ix->V * ix->K));
     SME_HIP(hipMemcpy(ix->h_gram.data(), ix->d_gram.p, ix->h_gram.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
   }
@@ -586,9 +586,17 @@ int sme_index_term(sme_index *ix, int64_t t, const uint8_t **utf8, size_t *n) {
     set_device(ix->ctx);
     ensure_host_terms(ix);
     ix->h_term_tmp.clear();
-    const int64_t c = ix->K > 1 ? (int64_t)ix->h_gram[(size_t)(t * ix->K)] : t;  // k_gram[0] of a k-gram
-    u16_to_mutf8(ix->h_term_chars.data() + ix->h_term_off[c], (size_t)(ix->h_term_off[c + 1] - ix->h_term_off[c]),
-                 ix->h_term_tmp);
+    const bool joined = ix->K > 1 && ix->h_gram.empty();  // merged pieces: components joined by U+0000
+    const int64_t c = (ix->K > 1 && !joined) ? (int64_t)ix->h_gram[(size_t)(t * ix->K)] : t;  // k_gram[0] of a k-gram
+    const uint16_t *u = ix->h_term_chars.data() + ix->h_term_off[c];
+    size_t len = (size_t)(ix->h_term_off[c + 1] - ix->h_term_off[c]);
+    if (joined)
+      for (size_t i = 0; i < len; i++)
+        if (u[i] == 0) {
+          len = i;
+          break;
+        }
+    u16_to_mutf8(u, len, ix->h_term_tmp);
     *utf8 = ix->h_term_tmp.data();
     *n = ix->h_term_tmp.size();
   });

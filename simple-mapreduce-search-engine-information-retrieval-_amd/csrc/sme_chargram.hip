@@ -19,9 +19,10 @@
 //     head insertion, and each resize transfer reverses a chain.  (Checked against a
 //     direct simulation of the JDK 6 algorithm in oracle/oracle_chargram.c.)
 // So: first occurrence per term (atomic min over the stream) -> (gram, term) pairs with
-// UTF-8 gram keys packed into 128 bits (Text order = numeric order, k <= 5) -> sort by
-// (gram, first occurrence), dedup -> per-element HashSet rank key -> sort -> one pass
-// that writes every line at its scanned offset.
+// UTF-8 gram keys packed big-endian into W = ceil((3k + 2) / 8) 64-bit words, the byte
+// length in the last word's low 16 bits (Text order = numeric order of the word tuple,
+// any k) -> LSD sort by (gram words, first occurrence), dedup -> per-element HashSet
+// rank key -> sort -> one pass that writes every line at its scanned offset.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,7 +31,21 @@
 
 namespace sme {
 
-constexpr int kCgMaxK = 5;  // UTF-8 gram <= 15 bytes + length byte in a 128-bit key
+// key words of a k-unit gram: <= 3 bytes per unit (a surrogate pair: 4 bytes for 2
+// units) + the 16-bit byte length
+inline int cg_words(int K) { return (3 * K + 2 + 7) / 8; }
+// byte j of a gram key (word-major layout kw[w * stride + i])
+__device__ __forceinline__ uint8_t cg_byte(const uint64_t *kw, int64_t stride, int64_t i, int j) {
+  return (uint8_t)(kw[(int64_t)(j >> 3) * stride + i] >> (56 - 8 * (j & 7)));
+}
+__device__ __forceinline__ int cg_nbytes(const uint64_t *kw, int64_t stride, int W, int64_t i) {
+  return (int)(kw[(int64_t)(W - 1) * stride + i] & 0xFFFFu);
+}
+__device__ __forceinline__ bool cg_key_eq(const uint64_t *kw, int64_t stride, int W, int64_t a, int64_t b) {
+  for (int w = 0; w < W; w++)
+    if (kw[(int64_t)w * stride + a] != kw[(int64_t)w * stride + b]) return false;
+  return true;
+}
 
 // String.getBytes("UTF-8") of units [0, n) (unpaired surrogate -> '?'); returns bytes
 __device__ __forceinline__ int java_utf8_at(const uint16_t *u, int n, uint8_t *o) {
@@ -106,28 +121,58 @@ __global__ void k_rank_of(const uint32_t *order, int64_t V, uint32_t *rank) {
     rank[order[r]] = (uint32_t)r;
 }
 
-// every (gram position, term): the gram's Java UTF-8 bytes packed big-endian into
-// (hi, lo) with the byte length in the lowest byte -> numeric order = Text order
-__global__ void k_gram_pairs(const int64_t *toff, const uint16_t *tch, int64_t V, int K, const int64_t *goff,
-                             const uint32_t *rank, uint64_t *khi, uint64_t *klo, uint32_t *kord, uint32_t *kterm) {
+// every (gram position, term): the gram's Java UTF-8 bytes (String.getBytes, an
+// unpaired surrogate -> '?') packed big-endian into W words, the byte length in the
+// low 16 bits of the last -> numeric order of the words = Text order
+__global__ void k_gram_pairs(const int64_t *toff, const uint16_t *tch, int64_t V, int K, int W, const int64_t *goff,
+                             const uint32_t *rank, uint64_t *kw, int64_t NP, uint32_t *kord, uint32_t *kterm) {
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = toff[t], L = toff[t + 1] - b, g0 = goff[t], ng = goff[t + 1] - g0;
+    auto unit = [&](int64_t p) -> unsigned {  // position in '$' t '$'
+      return (p == 0 || p == L + 1) ? (unsigned)'$' : (unsigned)tch[b + p - 1];
+    };
     for (int64_t i = 0; i < ng; i++) {
-      uint16_t u[kCgMaxK];
+      const int64_t x = g0 + i;
+      uint64_t word = 0;
+      int nb = 0, w = 0;
+      auto put = [&](unsigned by) {
+        word |= (uint64_t)(by & 0xFFu) << (56 - 8 * (nb & 7));
+        nb++;
+        if ((nb & 7) == 0) {
+          kw[(int64_t)w * NP + x] = word;
+          w++;
+          word = 0;
+        }
+      };
       for (int j = 0; j < K; j++) {
-        const int64_t p = i + j;  // position in '$' t '$'
-        u[j] = (p == 0 || p == L + 1) ? (uint16_t)'$' : tch[b + p - 1];
+        const unsigned c = unit(i + j);
+        if (c >= 0xD800 && c <= 0xDBFF && j + 1 < K && unit(i + j + 1) >= 0xDC00 && unit(i + j + 1) <= 0xDFFF) {
+          const unsigned cp = 0x10000 + ((c - 0xD800) << 10) + (unit(i + j + 1) - 0xDC00);
+          put(0xF0 | (cp >> 18));
+          put(0x80 | ((cp >> 12) & 0x3F));
+          put(0x80 | ((cp >> 6) & 0x3F));
+          put(0x80 | (cp & 0x3F));
+          j++;
+        } else if (c >= 0xD800 && c <= 0xDFFF) {
+          put('?');
+        } else if (c < 0x80) {
+          put(c);
+        } else if (c < 0x800) {
+          put(0xC0 | (c >> 6));
+          put(0x80 | (c & 0x3F));
+        } else {
+          put(0xE0 | (c >> 12));
+          put(0x80 | ((c >> 6) & 0x3F));
+          put(0x80 | (c & 0x3F));
+        }
       }
-      uint8_t by[16];
-      const int nb = java_utf8_at(u, K, by);
-      uint64_t hi = 0, lo = 0;
-      for (int j = 0; j < 8; j++) hi = (hi << 8) | (j < nb ? by[j] : 0);
-      for (int j = 8; j < 15; j++) lo = (lo << 8) | (j < nb ? by[j] : 0);
-      lo = (lo << 8) | (uint64_t)nb;
-      khi[g0 + i] = hi;
-      klo[g0 + i] = lo;
-      kord[g0 + i] = rank[t];
-      kterm[g0 + i] = (uint32_t)t;
+      const int len = nb;
+      for (; w < W; w++) {  // the partial word, zero words, the length
+        kw[(int64_t)w * NP + x] = word | (w == W - 1 ? (uint64_t)len : 0ull);
+        word = 0;
+      }
+      kord[x] = rank[t];
+      kterm[x] = (uint32_t)t;
     }
   }
 }
@@ -147,22 +192,22 @@ __global__ void k_iota32(uint32_t *a, int64_t n) {
 }
 
 // sorted pairs (order idx): keep the first of each equal (gram, term), flag gram starts
-__global__ void k_cg_flags(const uint64_t *khi, const uint64_t *klo, const uint32_t *kterm, const uint32_t *idx,
+__global__ void k_cg_flags(const uint64_t *kw, int64_t NP, int W, const uint32_t *kterm, const uint32_t *idx,
                            int64_t n, uint8_t *keep) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t a = idx[i];
     bool k = true;
     if (i > 0) {
       const uint32_t p = idx[i - 1];
-      k = !(khi[a] == khi[p] && klo[a] == klo[p] && kterm[a] == kterm[p]);
+      k = !(kterm[a] == kterm[p] && cg_key_eq(kw, NP, W, a, p));
     }
     keep[i] = k ? 1 : 0;
   }
 }
 
-__global__ void k_cg_gstart(const uint64_t *khi, const uint64_t *klo, const uint32_t *u, int64_t n, uint32_t *gflag) {
+__global__ void k_cg_gstart(const uint64_t *kw, int64_t NP, int W, const uint32_t *u, int64_t n, uint32_t *gflag) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    gflag[i] = (i == 0 || khi[u[i]] != khi[u[i - 1]] || klo[u[i]] != klo[u[i - 1]]) ? 1u : 0u;
+    gflag[i] = (i == 0 || !cg_key_eq(kw, NP, W, u[i], u[i - 1])) ? 1u : 0u;
 }
 __global__ void k_cg_segs(const uint32_t *gincl, int64_t n, int64_t *gstart) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -199,17 +244,14 @@ __global__ void k_cg_setkey(const uint32_t *u, const uint32_t *kterm, const uint
 }
 
 // per gram (in key order): line length, partition (HashPartitioner on Text.hashCode)
-__global__ void k_cg_lines(const uint64_t *khi, const uint64_t *klo, const uint32_t *u, const int64_t *gstart,
+__global__ void k_cg_lines(const uint64_t *kw, int64_t NP, int W, const uint32_t *u, const int64_t *gstart,
                            int64_t ngr, int64_t n, const int64_t *elen_scan, int R, int64_t *llen, uint32_t *part) {
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < ngr; g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s0 = gstart[g], s1 = g + 1 < ngr ? gstart[g + 1] : n;
     const uint32_t a = u[s0];
-    const int nb = (int)(klo[a] & 0xFF);
+    const int nb = cg_nbytes(kw, NP, W, a);
     int32_t h = 1;
-    for (int j = 0; j < nb; j++) {
-      const uint8_t b = j < 8 ? (uint8_t)(khi[a] >> (56 - 8 * j)) : (uint8_t)(klo[a] >> (56 - 8 * (j - 8)));
-      h = 31 * h + (int32_t)(int8_t)b;
-    }
+    for (int j = 0; j < nb; j++) h = 31 * h + (int32_t)(int8_t)cg_byte(kw, NP, a, j);
     part[g] = (uint32_t)((h & 0x7fffffff) % R);
     // "gram" '\t' '[' (terms joined by ", ") ']' '\n'
     llen[g] = nb + 4 + (elen_scan[s1] - elen_scan[s0]) - 2;
@@ -217,28 +259,27 @@ __global__ void k_cg_lines(const uint64_t *khi, const uint64_t *klo, const uint3
 }
 
 // write the gram prefix of every line, and every element's term + separator
-__global__ void k_cg_write_keys(const uint64_t *khi, const uint64_t *klo, const uint32_t *u, const int64_t *gstart,
+__global__ void k_cg_write_keys(const uint64_t *kw, int64_t NP, int W, const uint32_t *u, const int64_t *gstart,
                                 const uint32_t *gorder, int64_t ngr, const int64_t *loff, uint8_t *out) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < ngr; r += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t g = gorder[r];
     const uint32_t a = u[gstart[g]];
-    const int nb = (int)(klo[a] & 0xFF);
+    const int nb = cg_nbytes(kw, NP, W, a);
     uint8_t *w = out + loff[r];
-    for (int j = 0; j < nb; j++)
-      w[j] = j < 8 ? (uint8_t)(khi[a] >> (56 - 8 * j)) : (uint8_t)(klo[a] >> (56 - 8 * (j - 8)));
+    for (int j = 0; j < nb; j++) w[j] = cg_byte(kw, NP, a, j);
     w[nb] = '\t';
     w[nb + 1] = '[';
   }
 }
 __global__ void k_cg_write_terms(const uint32_t *u, const uint32_t *kterm, const uint32_t *gincl, const int64_t *gstart,
                                  int64_t ngr, int64_t n, const uint32_t *rank_of_g, const int64_t *loff,
-                                 const int64_t *elen_scan, const uint64_t *khi, const uint64_t *klo,
+                                 const int64_t *elen_scan, const uint64_t *kw, int64_t NP, int W,
                                  const int64_t *toff, const uint16_t *tch, uint8_t *out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t g = gincl[i] - 1;
     const int64_t s0 = gstart[g], s1 = g + 1 < (uint64_t)ngr ? gstart[g + 1] : n;
     const uint32_t a0 = u[s0];
-    const int nb = (int)(klo[a0] & 0xFF);
+    const int nb = cg_nbytes(kw, NP, W, a0);
     uint8_t *w = out + loff[rank_of_g[g]] + nb + 2 + (elen_scan[i] - elen_scan[s0]);
     const uint32_t t = kterm[u[i]];
     const int64_t b = toff[t];
@@ -277,7 +318,7 @@ static T cg_d2h(const T *d, hipStream_t st) {
 void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t M, int64_t V, const int64_t *term_off,
                     const uint16_t *tch, hipStream_t st, Prof *prof) {
   const int K = cx->cfg.k, R = cx->cfg.num_partitions;
-  if (K < 1 || K > kCgMaxK) throw Error(SME_ENOTIMPL, "CharKGramTermIndexer with k > 5 is not built");
+  if (K < 1) throw Error(SME_EINVAL, "CharKGramTermIndexer needs k >= 1");
   ix->job = 1;
   auto &W = cx->ws;  // slots 48..63 (query / serializer region) are free during a build
   ix->part_start.assign((size_t)R + 1, 0);
@@ -315,23 +356,27 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
     return;
   }
   if (NP >= (1ll << 31)) throw Error(SME_ELIMIT, "more than 2^31 (gram, term) pairs");
-  // (gram, term) pairs sorted by (gram bytes, first occurrence): three stable LSD passes
-  uint64_t *khi = W[57].as<uint64_t>(NP), *klo = W[58].as<uint64_t>(NP);
+  // (gram, term) pairs sorted by (gram bytes, first occurrence): stable LSD passes,
+  // the insertion rank first, then the key words from the last to the first
+  const int KW = cg_words(K);
+  uint64_t *kw = W[57].as<uint64_t>((size_t)KW * NP);
   uint32_t *kord = W[59].as<uint32_t>(NP), *kterm = W[60].as<uint32_t>(NP);
-  hipLaunchKernelGGL(k_gram_pairs, dim3(cg_grid(V)), dim3(256), 0, st, term_off, tch, V, K, goff, rank, khi, klo, kord,
-                     kterm);
-  uint32_t *ia = W[61].as<uint32_t>(NP), *ib = W[62].as<uint32_t>(NP + 1);
+  hipLaunchKernelGGL(k_gram_pairs, dim3(cg_grid(V)), dim3(256), 0, st, term_off, tch, V, K, KW, goff, rank, kw, NP,
+                     kord, kterm);
+  // (either buffer ends up holding the permutation, then the gram-start flags: NP + 1)
+  uint32_t *ia = W[61].as<uint32_t>(NP + 1), *ib = W[62].as<uint32_t>(NP + 1);
   uint64_t *k64 = W[52].as<uint64_t>(NP), *k64s = W[48].as<uint64_t>(NP);
   uint32_t *k32s = W[49].as<uint32_t>(NP);
   hipLaunchKernelGGL(k_iota32, dim3(cg_grid(NP)), dim3(256), 0, st, ia, NP);
   sort_pairs<uint32_t>(kord, k32s, ia, ib, NP, 32, rs, st);
-  hipLaunchKernelGGL(k_gather<uint64_t>, dim3(cg_grid(NP)), dim3(256), 0, st, klo, ib, NP, k64);
-  sort_pairs<uint64_t>(k64, k64s, ib, ia, NP, 64, rs, st);
-  hipLaunchKernelGGL(k_gather<uint64_t>, dim3(cg_grid(NP)), dim3(256), 0, st, khi, ia, NP, k64);
-  sort_pairs<uint64_t>(k64, k64s, ia, ib, NP, 64, rs, st);
+  for (int w = KW - 1; w >= 0; w--) {  // permutation in ib; each pass: gather the word, sort, back into ib
+    hipLaunchKernelGGL(k_gather<uint64_t>, dim3(cg_grid(NP)), dim3(256), 0, st, kw + (int64_t)w * NP, ib, NP, k64);
+    sort_pairs<uint64_t>(k64, k64s, ib, ia, NP, 64, rs, st);
+    std::swap(ia, ib);
+  }
   // dedup equal (gram, term) -> u: pair indices in (gram, insertion) order
   uint8_t *keep = W[63].as<uint8_t>(NP);
-  hipLaunchKernelGGL(k_cg_flags, dim3(cg_grid(NP)), dim3(256), 0, st, khi, klo, kterm, ib, NP, keep);
+  hipLaunchKernelGGL(k_cg_flags, dim3(cg_grid(NP)), dim3(256), 0, st, kw, NP, KW, kterm, ib, NP, keep);
   uint32_t *u = ia;
   int32_t *d_nu = reinterpret_cast<int32_t *>(W[55].as<int64_t>(V + 1));
   int32_t *sel = cx->ws[120].as<int32_t>(NP + 1);
@@ -341,7 +386,7 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
                      n, u);
   // gram segments
   uint32_t *gflag = ib, *gincl = W[50].as<uint32_t>(std::max<int64_t>(NP, V) + 1);
-  hipLaunchKernelGGL(k_cg_gstart, dim3(cg_grid(n)), dim3(256), 0, st, khi, klo, u, n, gflag);
+  hipLaunchKernelGGL(k_cg_gstart, dim3(cg_grid(n)), dim3(256), 0, st, kw, NP, KW, u, n, gflag);
   // inclusive sum = the exclusive scan of (flags, 0) shifted by one
   SME_HIP(hipMemsetAsync(gflag + n, 0, sizeof(uint32_t), st));
   excl_scan(gflag, gincl, n + 1, cx->ws[23], st);
@@ -374,11 +419,11 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   int64_t *elen = W[53].as<int64_t>(n + 1), *escan = W[54].as<int64_t>(n + 1);
   hipLaunchKernelGGL(k_cg_elen, dim3(cg_grid(n + 1)), dim3(256), 0, st, u3, kterm, u8len, n, elen);
   excl_scan(elen, escan, (int64_t)(n + 1), cx->ws[23], st);
-  // khi/klo/kterm (slots 57, 58, 60) stay live until the lines are written
+  // kw/kterm (slots 57, 60) stay live until the lines are written
   DevBuf b_llen, b_loff, b_part;
   int64_t *llen = b_llen.as<int64_t>(ngr + 1), *loff = b_loff.as<int64_t>(ngr + 1);
   uint32_t *part = b_part.as<uint32_t>(ngr + 1), *part_s = W[62].as<uint32_t>(ngr + 1);
-  hipLaunchKernelGGL(k_cg_lines, dim3(cg_grid(ngr)), dim3(256), 0, st, khi, klo, u3, gstart, ngr, n, escan, R, llen,
+  hipLaunchKernelGGL(k_cg_lines, dim3(cg_grid(ngr)), dim3(256), 0, st, kw, NP, KW, u3, gstart, ngr, n, escan, R, llen,
                      part);
   uint32_t *gseq = W[51].as<uint32_t>(ngr + 1), *gorder = W[63].as<uint32_t>(ngr + 1);
   hipLaunchKernelGGL(k_iota32, dim3(cg_grid(ngr)), dim3(256), 0, st, gseq, ngr);
@@ -391,9 +436,10 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
   uint32_t *rank_of_g = W[51].as<uint32_t>(ngr + 1);  // gseq no longer needed
   hipLaunchKernelGGL(k_rank_of, dim3(cg_grid(ngr)), dim3(256), 0, st, gorder, ngr, rank_of_g);
   uint8_t *out = ix->d_ser.as<uint8_t>(total + 16);
-  hipLaunchKernelGGL(k_cg_write_keys, dim3(cg_grid(ngr)), dim3(256), 0, st, khi, klo, u3, gstart, gorder, ngr, loff, out);
+  hipLaunchKernelGGL(k_cg_write_keys, dim3(cg_grid(ngr)), dim3(256), 0, st, kw, NP, KW, u3, gstart, gorder, ngr, loff,
+                     out);
   hipLaunchKernelGGL(k_cg_write_terms, dim3(cg_grid(n)), dim3(256), 0, st, u3, kterm, gincl, gstart, ngr, n, rank_of_g,
-                     loff, escan, khi, klo, term_off, tch, out);
+                     loff, escan, kw, NP, KW, term_off, tch, out);
   int64_t *pstart = W[53].as<int64_t>((size_t)R + 1);
   hipLaunchKernelGGL(k_cg_part_start, dim3(cg_grid(ngr + 1)), dim3(256), 0, st, part_s, loff, ngr, R, total, pstart);
   SME_CHECK_LAUNCH();

@@ -56,13 +56,47 @@ PieceLayout layout_of(const PieceHdr &h) {
   return L;
 }
 
-// partition of a K = 1 term: Arrays.hashCode({s}) = 31 + s.hashCode()
+// partition of a term: Arrays.hashCode(k_gram) = fold of 31 * h + s.hashCode()
+// over the components from 1 (K = 1: 31 + s.hashCode()); a K >= 2 gram is its
+// components joined by U+0000 (never inside a term: 0 is a split character)
 __global__ void k_term_owner(const int64_t *toff, const uint16_t *tch, int64_t V, int R, int world, int32_t *owner) {
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t h = 0;
-    for (int64_t i = toff[t]; i < toff[t + 1]; i++) h = 31u * h + tch[i];
-    const uint32_t ah = 31u + h;
+    uint32_t h = 0, ah = 1u;
+    for (int64_t i = toff[t]; i < toff[t + 1]; i++) {
+      if (tch[i] == 0) {
+        ah = 31u * ah + h;
+        h = 0;
+      } else {
+        h = 31u * h + tch[i];
+      }
+    }
+    ah = 31u * ah + h;
     owner[t] = (int32_t)((uint32_t)((int32_t)(ah & 0x7fffffffu) % R) % (uint32_t)world);
+  }
+}
+// K >= 2: every gram as one string, its component terms joined by U+0000.  The
+// strings' UTF-16 order is TermDF.compareTo's (TermDF.java:64-70): at the first
+// differing component either a unit differs inside it, or one component is a
+// prefix of the other and the shorter one meets U+0000, below every term unit
+__global__ void k_gram_join_len(const int32_t *gram, int K, const int64_t *toff, int64_t V, int64_t *len) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t l = K - 1;
+    for (int j = 0; j < K; j++) {
+      const int64_t c = gram[t * K + j];
+      l += toff[c + 1] - toff[c];
+    }
+    len[t] = l;
+  }
+}
+__global__ void k_gram_join_write(const int32_t *gram, int K, const int64_t *toff, const uint16_t *tch, int64_t V,
+                                  const int64_t *joff, uint16_t *jch) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
+    uint16_t *o = jch + joff[t];
+    for (int j = 0; j < K; j++) {
+      const int64_t c = gram[t * K + j];
+      if (j > 0) *o++ = 0;
+      for (int64_t i = toff[c]; i < toff[c + 1]; i++) *o++ = tch[i];
+    }
   }
 }
 __global__ void k_owner_flags(const int32_t *owner, int64_t V, int o, uint8_t *f) {
@@ -311,7 +345,7 @@ T rd1(const T *d, hipStream_t st) {
 }  // namespace
 
 void pack_pieces(sme_index *ix, int world, uint8_t *d_out, uint64_t *sizes, hipStream_t st) {
-  if (ix->job != 0 || ix->K != 1) throw Error(SME_EINVAL, "reference-layout pieces need a K = 1 TermKGramDocIndexer index");
+  if (ix->job != 0 || ix->records_only) throw Error(SME_EINVAL, "reference-layout pieces need a TermKGramDocIndexer index");
   if (world < 1 || world > 65536) throw Error(SME_EINVAL, "world out of range");
   sme_ctx *cx = ix->ctx;
   auto &W = cx->ws;
@@ -319,10 +353,30 @@ void pack_pieces(sme_index *ix, int world, uint8_t *d_out, uint64_t *sizes, hipS
   const int R = ix->R;
   const int part_sp = (31 + 32) % R;  // Arrays.hashCode({" "}), partition of the doc counter
   const int32_t sp_owner = part_sp % world;
+  // the index terms' strings: the vocabulary (K = 1) or the grams' joined
+  // component strings (K >= 2)
+  const int64_t *toff = (const int64_t *)ix->d_term_off.p;
+  const uint16_t *tch = (const uint16_t *)ix->d_term_chars.p;
+  DevBuf jo, jc, jl;
+  jo.pool = jc.pool = jl.pool = &cx->pool;
+  if (ix->K > 1 && V > 0) {
+    int64_t *len = jl.as<int64_t>(V + 1);
+    int64_t *joff = jo.as<int64_t>(V + 1);
+    hipLaunchKernelGGL(k_gram_join_len, dim3(grid_n(V)), dim3(256), 0, st, (const int32_t *)ix->d_gram.p, ix->K, toff,
+                       V, len);
+    SME_HIP(hipMemsetAsync(len + V, 0, sizeof(int64_t), st));
+    excl_scan(len, joff, V + 1, W[9], st);
+    const int64_t nu = rd1(joff + V, st);
+    uint16_t *jch = jc.as<uint16_t>(nu + 1);
+    hipLaunchKernelGGL(k_gram_join_write, dim3(grid_n(V)), dim3(256), 0, st, (const int32_t *)ix->d_gram.p, ix->K,
+                       toff, tch, V, joff, jch);
+    SME_CHECK_LAUNCH();
+    toff = joff;
+    tch = jch;
+  }
   int32_t *owner = W[0].as<int32_t>(V + 1);
   if (V > 0)
-    hipLaunchKernelGGL(k_term_owner, dim3(grid_n(V)), dim3(256), 0, st, (const int64_t *)ix->d_term_off.p,
-                       (const uint16_t *)ix->d_term_chars.p, V, R, world, owner);
+    hipLaunchKernelGGL(k_term_owner, dim3(grid_n(V)), dim3(256), 0, st, toff, tch, V, R, world, owner);
   uint8_t *flag = W[1].as<uint8_t>(V + 1);
   int32_t *sel = W[2].as<int32_t>(V + 1);
   int32_t *d_n = W[3].as<int32_t>(4);
@@ -337,8 +391,8 @@ void pack_pieces(sme_index *ix, int world, uint8_t *d_out, uint64_t *sizes, hipS
       n = rd1(d_n, st);
     }
     if (n > 0)
-      hipLaunchKernelGGL(k_sel_lens, dim3(grid_n(n)), dim3(256), 0, st, sel, n, (const int64_t *)ix->d_term_off.p,
-                         (const int64_t *)ix->d_off.p, ulen, plen);
+      hipLaunchKernelGGL(k_sel_lens, dim3(grid_n(n)), dim3(256), 0, st, sel, n, toff, (const int64_t *)ix->d_off.p,
+                         ulen, plen);
     SME_HIP(hipMemsetAsync(ulen + n, 0, sizeof(int64_t), st));
     SME_HIP(hipMemsetAsync(plen + n, 0, sizeof(int64_t), st));
     excl_scan(ulen, uoff, n + 1, W[9], st);
@@ -351,6 +405,7 @@ void pack_pieces(sme_index *ix, int world, uint8_t *d_out, uint64_t *sizes, hipS
     h.nrec = o == sp_owner ? ix->N : 0;
     h.dmin = (int32_t)(ix->N > 0 ? ix->dmin : 1);
     h.dmax = (int32_t)(ix->N > 0 ? ix->dmax : 0);
+    h.pad[0] = ix->K;  // components per term (joined by U+0000 when K >= 2)
     const PieceLayout L = layout_of(h);
     sizes[o] = (uint64_t)L.total;
     if (d_out) {
@@ -359,8 +414,7 @@ void pack_pieces(sme_index *ix, int world, uint8_t *d_out, uint64_t *sizes, hipS
       SME_HIP(hipMemcpyAsync(b + L.term_off, uoff, (n + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
       SME_HIP(hipMemcpyAsync(b + L.post_off, poff, (n + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
       if (n > 0)
-        hipLaunchKernelGGL(k_pack_terms, dim3(grid_n(n * 64)), dim3(256), 0, st, sel, n,
-                           (const int64_t *)ix->d_term_off.p, (const uint16_t *)ix->d_term_chars.p,
+        hipLaunchKernelGGL(k_pack_terms, dim3(grid_n(n * 64)), dim3(256), 0, st, sel, n, toff, tch,
                            (const int64_t *)ix->d_off.p, (const int32_t *)ix->d_docno_o.p,
                            (const int32_t *)ix->d_tf_o.p, uoff, poff, (uint16_t *)(b + L.term_chars),
                            (int32_t *)(b + L.docno), (int32_t *)(b + L.tf));
@@ -386,6 +440,8 @@ sme_index *merge_pieces(sme_ctx *cx, const uint8_t *d_blobs, const uint64_t *siz
     if (hd[a].magic != kPieceMagic) throw Error(SME_EINVAL, "not a piece blob (sme_index_pack_pieces)");
     lay[a] = layout_of(hd[a]);
     if ((uint64_t)lay[a].total != sizes[a]) throw Error(SME_EINVAL, "piece blob size mismatch");
+    if (std::max<int64_t>(hd[a].pad[0], 1) != std::max<int64_t>(hd[0].pad[0], 1))
+      throw Error(SME_EINVAL, "pieces of different k-gram lengths");
     at += lay[a].total;
   }
   std::vector<PieceDev> hp(np);
@@ -425,7 +481,9 @@ sme_index *merge_pieces(sme_ctx *cx, const uint8_t *d_blobs, const uint64_t *siz
 
   sme_index *ix = new sme_index(cx);
   std::unique_ptr<sme_index> guard(ix);
-  ix->K = 1;
+  // K >= 2: each merged term is a gram's joined component strings (no gram
+  // table: the serializer splits the strings at U+0000)
+  ix->K = (int)std::max<int64_t>(hd[0].pad[0], 1);
   ix->R = cx->cfg.num_partitions;
   ix->idf_mode = cx->cfg.idf_mode;
   ix->records_only = true;

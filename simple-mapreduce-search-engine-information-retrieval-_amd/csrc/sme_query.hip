@@ -1398,16 +1398,23 @@ struct QWinArgs {
   int exper;                   // SME_EXPERIMENTS timing switches (0 in the product)
 };
 
-__global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
-  // LDS: 9.8 KB per wave + the LUT = 40 KB per workgroup, four workgroups per CU
-  // (the VGPR limit of 4 waves per SIMD; LDS-bound occupancy 3 measured 26 % slower)
-  __shared__ uint32_t lacc_all[kWNT / 64][kWin / 2];  // sparse impact sums, u16 pairs (see below)
-  __shared__ uint32_t slist_all[kWNT / 64][kSList];   // the window's sparse postings: r | tf << 12
+// waves per SIMD the register allocation targets (LDS allows far more)
+#ifndef SME_QWIN_WAVES
+#define SME_QWIN_WAVES 5
+#endif
+__global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) {
+  // LDS: 2.8 KB per wave + the LUT = 12 KB per workgroup, so LDS does not bound
+  // the occupancy (a per-document sparse accumulator, 8 KB per wave, held it at
+  // four workgroups per CU): the window's sparse postings are summed per
+  // 16-document block for the bounds, and a passing block's documents take
+  // their sparse impacts from the listed postings
+  __shared__ uint32_t bsum_all[kWNT / 64][kWin / 16];  // sparse impact sum of every block
+  __shared__ uint32_t slist_all[kWNT / 64][kSList];   // the window's sparse postings: r | q << 12 | tf << 20
   __shared__ uint16_t blist_all[kWNT / 64][kWin / 16];  // blocks over the gate
   __shared__ uint16_t clist_all[kWNT / 64][kCList];     // documents over the gate
   __shared__ double s_lut[kWinLut];                    // 1 + ln(tf) for tf < 128
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t *lacc = lacc_all[wv], *slist = slist_all[wv];
+  uint32_t *bsum = bsum_all[wv], *slist = slist_all[wv];
   uint16_t *blist = blist_all[wv], *clist = clist_all[wv];
   for (int i = threadIdx.x; i < kWinLut; i += kWNT) s_lut[i] = i <= a.max_tf ? a.lut[i] : 0.0;
   __syncthreads();
@@ -1424,7 +1431,7 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
   int pos = p_lo + wv;
   if (pos >= p_hi) return;
 #pragma unroll
-  for (int m = 0; m < kWDL / 2; m++) lacc[m * 64 + lane] = 0;
+  for (int m = 0; m < 4; m++) bsum[m * 64 + lane] = 0;
   // software pipeline over this wave's queries: the next query's position
   // record, term records, threshold and skip entries load while this one runs
   QPos P = ld_pos_nt(a.qpos + pos);
@@ -1484,15 +1491,14 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
         }
       }
     }
-    // sparse terms: the window's postings into LDS -- impact sums per document
-    // and per block, and the (document, tf) list for exact lookups
+    // sparse terms: the window's postings into LDS -- impact sums per block, and
+    // the (document, impact, tf) list (per term docno-ascending) for the exact
+    // sums of passing blocks and the candidates' tf lookups
     const int32_t cj = ((sm >> lane) & 1) ? me - mc : 0;
     const int32_t incl = wave_incl_sum(cj), prej = incl - cj;
     const int32_t total = __shfl(incl, 63, 64);
-    const bool listed = total <= kSList;  // else exact tf lookups search the global postings
+    const bool listed = total <= kSList;  // else the block sum bounds every document of the block
     if (total > 0) {
-      // lacc[m * 64 + l] holds documents 64 l + 2m (low), + 1 (high): lane l's
-      // 32 words are a conflict-free column (zero here: cleared after each pair)
       const int64_t plo = D.mb + mc;
       for (int32_t e0 = 0; e0 < total; e0 += 64) {
         const int32_t e = e0 + lane;
@@ -1511,8 +1517,8 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
           const int r = (int)((int64_t)d - wbase);
           // q(tf) computed here (the batch table would be a second dependent load)
           const uint32_t qv = impact(f < kWinLut ? s_lut[f] : a.lut[f], wj, a.alpha);
-          atomicAdd(&lacc[((r & 63) >> 1) * 64 + (r >> 6)], qv << ((r & 1) << 4));
-          if (listed) slist[e] = (uint32_t)r | ((uint32_t)min(f, 0xFFFFF) << 12);
+          atomicAdd(&bsum[r >> 4], qv);
+          if (listed) slist[e] = (uint32_t)r | (qv << 12) | ((uint32_t)min(f, 0xFFF) << 20);
         }
       }
       qwave_sync();
@@ -1526,18 +1532,9 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
     // blocks over the gate: heavy maxima + the block's sparse impact sum
     uint32_t ub[4] = {ub0 & 0xFFFFu, ub0 >> 16, ub1 & 0xFFFFu, ub1 >> 16};
     if (total > 0) {
-      // + the largest sparse sum of each block's documents (lane l's column of
-      // lacc: documents 64 l .. 64 l + 63, block m = words 8 m .. 8 m + 7)
+      // + the block's sparse impact sum (>= the sparse sum of any of its documents)
 #pragma unroll
-      for (int m = 0; m < 4; m++) {
-        uint32_t mx = 0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          const uint32_t v = lacc[(8 * m + i) * 64 + lane];
-          mx = max(mx, max(v & 0xFFFFu, v >> 16));
-        }
-        ub[m] += mx;
-      }
+      for (int m = 0; m < 4; m++) ub[m] += bsum[4 * lane + m];
     }
     uint32_t bm = 0;
 #pragma unroll
@@ -1565,13 +1562,37 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
         const int blk = hb ? (int)blist[b0 + lane] : 0;
         const int r0 = blk << 4;  // first document of the block in the window
         uint32_t acc[8];          // documents r0 + 2m (low u16), + 1 (high)
-        if (total > 0) {
-          // documents r0 .. r0 + 15 = lane blk >> 2, words m = 8 (blk & 3) + i
 #pragma unroll
-          for (int i = 0; i < 8; i++) acc[i] = hb ? lacc[(8 * (blk & 3) + i) * 64 + (blk >> 2)] : 0u;
-        } else {
+        for (int i = 0; i < 8; i++) acc[i] = 0;
+        if (total > 0 && hb) {
+          if (listed) {
+            // the block's sparse postings: per sparse term, its listed entries
+            // from the first with r >= r0 while r < r0 + 16
+            for (uint64_t m = sm; m; m &= m - 1) {
+              const int j = (int)__builtin_ctzll(m);
+              int lo = __builtin_amdgcn_readlane(prej, j);
+              const int hi0 = lo + __builtin_amdgcn_readlane(cj, j);
+              int hi = hi0;
+              while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((int)(slist[mid] & 0xFFFu) < r0) lo = mid + 1;
+                else hi = mid;
+              }
+              for (; lo < hi0; lo++) {
+                const uint32_t ent = slist[lo];
+                const int dr = (int)(ent & 0xFFFu) - r0;
+                if (dr >= 16) break;
+                const uint32_t add = ((ent >> 12) & 0xFFu) << ((dr & 1) << 4);
 #pragma unroll
-          for (int i = 0; i < 8; i++) acc[i] = 0;
+                for (int i = 0; i < 8; i++) acc[i] += (dr >> 1) == i ? add : 0u;
+              }
+            }
+          } else {
+            // too many postings to list: the block's sum bounds each document
+            const uint32_t bs = bsum[blk];
+#pragma unroll
+            for (int i = 0; i < 8; i++) acc[i] = bs | (bs << 16);
+          }
         }
         for (uint64_t mh = hm; mh;) {
           uint4 v[4];
@@ -1665,8 +1686,8 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
                     else hi = mid;
                   }
                   if (lo < hi0 && (int)(slist[lo] & 0xFFFu) == r) {
-                    f = (int)(slist[lo] >> 12);
-                    if (f == 0xFFFFF) f = -1;  // tf >= 2^20: read it from the postings
+                    f = (int)(slist[lo] >> 20);
+                    if (f == 0xFFF) f = -1;  // tf >= 4095: read it from the postings
                   }
                 } else {
                   f = -1;
@@ -1710,16 +1731,9 @@ __global__ __launch_bounds__(kWNT) void k_query_win(QWinArgs a) {
       }
     }
     if (!hasn) break;
-    if (total > 0) {  // clear the sums this pair wrote: its listed documents' words, else all
-      if (listed) {
-        for (int32_t e = lane; e < total; e += 64) {
-          const int r = (int)(slist[e] & 0xFFFu);
-          lacc[((r & 63) >> 1) * 64 + (r >> 6)] = 0u;
-        }
-      } else {
+    if (total > 0) {  // clear the block sums this pair wrote
 #pragma unroll
-        for (int m = 0; m < kWDL / 2; m++) lacc[m * 64 + lane] = 0;
-      }
+      for (int m = 0; m < 4; m++) bsum[m * 64 + lane] = 0;
     }
     qwave_sync();  // this wave's LDS is rewritten for the next query
     pos = npos;

@@ -29,9 +29,29 @@ __device__ __forceinline__ void put_be32(uint8_t *p, uint32_t v) {
   p[3] = (uint8_t)v;
 }
 
-// index term t has K components: the term ids gram[t*K ..] for K > 1, or t itself
-__device__ __forceinline__ int64_t comp_of(const int32_t *gram, int K, int64_t t, int j) {
-  return gram ? (int64_t)gram[t * K + j] : t;
+// index term t has K components: the term ids gram[t*K ..] (K > 1 with a gram
+// table), or -- gram == nullptr -- the segments of term t's own string split at
+// U+0000 (K = 1: the whole string; a K >= 2 index merged from shard pieces
+// stores each gram as its components joined by U+0000, sme_merge.hip).  f(units,
+// length) is called per component in order.
+template <typename F>
+__device__ __forceinline__ void for_each_comp(const int64_t *toff, const uint16_t *tch, const int32_t *gram, int K,
+                                              int64_t t, F f) {
+  if (gram) {
+    for (int j = 0; j < K; j++) {
+      const int64_t c = gram[t * K + j];
+      f(tch + toff[c], toff[c + 1] - toff[c]);
+    }
+    return;
+  }
+  const uint16_t *u = tch + toff[t];
+  const int64_t l = toff[t + 1] - toff[t];
+  int64_t s = 0;
+  for (int64_t i = 0; i <= l; i++)
+    if (i == l || u[i] == 0) {
+      f(u + s, i - s);
+      s = i + 1;
+    }
 }
 
 // Partition byte totals are summed in LDS first (one global atomic per block
@@ -49,17 +69,14 @@ __global__ __launch_bounds__(256) void k_ser_sizes(const int64_t *toff, const ui
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
     int64_t ul = 0;
     uint32_t ah = 1u;  // Arrays.hashCode: 31 * h + String.hashCode per element, seed 1
-    for (int j = 0; j < K; j++) {
-      const int64_t c = comp_of(gram, K, t, j);
-      const uint16_t *u = tch + toff[c];
-      const int64_t l = toff[c + 1] - toff[c];
+    for_each_comp(toff, tch, gram, K, t, [&](const uint16_t *u, int64_t l) {
       uint32_t h = 0;
       for (int64_t i = 0; i < l; i++) {
         ul += mutf8_unit_len(u[i]);
         h = 31u * h + u[i];
       }
       ah = 31u * ah + h;
-    }
+    });
     const int64_t df = off[t + 1] - off[t];
     const int64_t key = 4 + 2 * (int64_t)K + ul + 4;
     const int64_t val = 4 + (df > 0 ? 2 + kClassLen + 8 * df : 0);
@@ -131,10 +148,9 @@ __global__ void k_ser_bigtiles(const int32_t *big, int64_t nbig, const int64_t *
     const int64_t t = big[j], df = off[t + 1] - off[t];
     ntile[j] = (8 * df + kSerTileBytes - 1) / kSerTileBytes;
     int64_t ul = 0;
-    for (int c = 0; c < K; c++) {
-      const int64_t e = comp_of(gram, K, t, c);
-      for (int64_t i = toff[e]; i < toff[e + 1]; i++) ul += mutf8_unit_len(tch[i]);
-    }
+    for_each_comp(toff, tch, gram, K, t, [&](const uint16_t *u, int64_t l) {
+      for (int64_t i = 0; i < l; i++) ul += mutf8_unit_len(u[i]);
+    });
     post_rel[j] = 8 + (4 + 2 * (int64_t)K + ul + 4) + 4 + 2 + kClassLen;
   }
 }
@@ -160,10 +176,9 @@ __global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int3
     if (ascii) {
       ul = toff[t + 1] - toff[t];
     } else {
-      for (int j = 0; j < K; j++) {
-        const int64_t c = comp_of(gram, K, t, j);
-        for (int64_t i = toff[c]; i < toff[c + 1]; i++) ul += mutf8_unit_len(tch[i]);
-      }
+      for_each_comp(toff, tch, gram, K, t, [&](const uint16_t *u, int64_t l) {
+        for (int64_t i = 0; i < l; i++) ul += mutf8_unit_len(u[i]);
+      });
     }
     const int64_t key = 4 + 2 * (int64_t)K + ul + 4, val = 4 + (df > 0 ? 2 + kClassLen + 8 * df : 0);
     uint8_t *post = o + 8 + key + 4 + 2 + kClassLen;
@@ -193,10 +208,7 @@ __global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int3
       put_be32(o + 4, (uint32_t)key);
       put_be32(o + 8, (uint32_t)K);
       uint8_t *q = o + 12;
-      for (int j = 0; j < K; j++) {  // writeUTF per element
-        const int64_t c = comp_of(gram, K, t, j);
-        const uint16_t *u = tch + toff[c];
-        const int64_t l = toff[c + 1] - toff[c];
+      for_each_comp(toff, tch, gram, K, t, [&](const uint16_t *u, int64_t l) {  // writeUTF per element
         int64_t el = 0;
         for (int64_t i = 0; i < l; i++) el += mutf8_unit_len(u[i]);
         q[0] = (uint8_t)(el >> 8);
@@ -215,7 +227,7 @@ __global__ void k_ser_write(const int64_t *toff, const uint16_t *tch, const int3
             *q++ = (uint8_t)(0x80 | (ch & 0x3F));
           }
         }
-      }
+      });
       put_be32(q, 1u);  // stored df of a real term (T1)
       put_be32(q + 4, (uint32_t)df);
       if (df > 0) {

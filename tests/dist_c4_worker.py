@@ -13,7 +13,8 @@ corpus (tests/golden/scale_c4multi.json, tools/gen_scale_golden.py) -- the
 reference's one global reduce (TermKGramDocIndexer.java:175-183,246).  The
 shards' reference_partitions (term-partition all_to_all + per-term reducer merge)
 must reproduce the oracle's R = 10 part files for the same 4 map tasks
-(scale_c4multi.json split_parts, tools/gen_scale_golden.py c4multi-parts).
+(scale_c4multi.json split_parts, tools/gen_scale_golden.py c4multi-parts), and
+the K = 3 job's part files likewise (split_parts_k3, c4multi-parts-k3).
 usage: dist_c4_worker.py RANK WORLD PORT OUT_DIR"""
 import importlib
 import json
@@ -99,6 +100,24 @@ def main():
             for group in g["queries"]:
                 if group["idf_mode"] == idf_mode:
                     check_group(ix, D, group, checked, world, rank)
+            ix.close()
+            ctx.close()
+        # the K = 3 job (TermKGramDocIndexer.java:138-159) over the same 4 map
+        # tasks: the shards' 3-gram postings merged on the partition owners equal
+        # the oracle's R part files (scale_c4multi.json split_parts_k3)
+        sp3 = g.get("split_parts_k3")
+        if sp3 is not None:
+            import common
+            ctx = sme.Context(3, sp3["R"], 0)
+            cuts = D.split_points(corpus, world, ctx)
+            assert cuts == sp3["cuts"]
+            ctx.load_docno_mapping(mapping)
+            ix = ctx.build_device(corpus.ptr + cuts[rank], cuts[rank + 1] - cuts[rank])
+            merged, owned = D.reference_partitions(ix)
+            for p in owned:
+                assert common.canon_digest(merged.partition_records(p)) == sp3["parts"][p], ("K=3", p)
+            timing["k3_partitions_checked"] = len(owned)
+            merged.close()
             ix.close()
             ctx.close()
         timing["queries_checked"] = int(sum(checked))

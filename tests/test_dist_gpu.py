@@ -68,3 +68,12 @@ def test_reference_partitions(tmp_path, world):
     across shards merged as the single reducer merges them
     (tests/dist_parts_worker.py)."""
     _run_ranks("dist_parts_worker.py", world, [], tmp_path, 240)
+
+
+@pytest.mark.parametrize("K", [2, 3])
+def test_reference_partitions_kgrams(tmp_path, K):
+    """The same world-2 reference-layout exchange for a K-gram index: grams
+    travel as their component terms joined by U+0000 (TermDF.compareTo order,
+    Arrays.hashCode partitions over the components) and the owners' merged part
+    files equal the oracle's K-gram job over the same two map tasks."""
+    _run_ranks("dist_parts_worker.py", 2, [str(K)], tmp_path, 240)

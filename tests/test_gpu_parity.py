@@ -515,7 +515,7 @@ def test_chargram_kat(sme):
     assert b"at\t[cat, bat]\n" in out.partition_text(0)
 
 
-@pytest.mark.parametrize("k,R", [(1, 1), (2, 10), (3, 3), (5, 2)])
+@pytest.mark.parametrize("k,R", [(1, 1), (2, 10), (3, 3), (5, 2), (6, 3), (9, 2), (14, 1)])
 def test_chargram_fuzz(sme, k, R):
     corpus, _ = common.fuzz_corpus(20 + k, 120)
     _check_chargram(sme, corpus, k, R)

@@ -19,7 +19,8 @@ device against them:
 Queries are stored as term strings; expected results as docnos and the fp64
 scores' hex (bit-exact comparison).  Run from the repo root:
     python tools/gen_scale_golden.py [c2shard|c5shard|c4multi|c4multi-parts ...]
-(c4multi-parts: add the 4-split, R = 10 partition digests to scale_c4multi.json)
+(c4multi-parts: add the 4-split, R = 10 partition digests to scale_c4multi.json;
+ c4multi-parts-k3: the same for the K = 3 job)
 """
 import hashlib
 import importlib
@@ -51,7 +52,7 @@ CONFIGS = {
 }
 
 
-def split_parts(name, world=4, R=10):
+def split_parts(name, world=4, R=10, K=1):
     """Add to an existing golden the reference output of the doc-sharded job: the
     oracle run with one map task per shard (splits at the cuts the world-`world`
     test uses, dist.cuts_from_starts over one reader pass) and R reducers --
@@ -67,18 +68,24 @@ def split_parts(name, world=4, R=10):
     mapping = synth.mapping_bytes(cfg["n"])
     starts = [o for o, _ in O.split_records(corpus)]
     cuts = D.cuts_from_starts(starts, len(corpus), world)
-    ix = O.OracleIndex(corpus, mapping, 1, R, splits=cuts)
+    ix = O.OracleIndex(corpus, mapping, K, R, splits=cuts)
     parts = [common.canon_digest(ix.partition_bytes(p)) for p in range(R)]
-    g["split_parts"] = {"world": world, "R": R, "cuts": cuts, "parts": parts}
+    g["split_parts" if K == 1 else "split_parts_k%d" % K] = {"world": world, "R": R, "K": K, "cuts": cuts,
+                                                               "parts": parts}
     with open(path, "w") as f:
         json.dump(g, f, separators=(",", ":"))
-    print("%s: split parts (world %d, R %d) in %.1f s -> %s" % (name, world, R, time.time() - t0, path), flush=True)
+    print("%s: split parts (world %d, R %d, K %d) in %.1f s -> %s" % (name, world, R, K, time.time() - t0, path),
+          flush=True)
 
 
 def main(names):
     for name in names:
         if name.endswith("-parts"):
             split_parts(name[:-len("-parts")])
+            continue
+        if "-parts-k" in name:  # e.g. c4multi-parts-k3: the K-gram job's part files
+            base, k = name.split("-parts-k")
+            split_parts(base, K=int(k))
             continue
         cfg = CONFIGS[name]
         t0 = time.time()

@@ -76,7 +76,10 @@ def main():
         else:
             same = bool(np.array_equal(base[0], res[0]) and np.array_equal(base[1].view(np.int64),
                                                                             res[1].view(np.int64)))
-        print(json.dumps({"opts": s or "default", "kernel_ms": round(float(np.median(kms[1:])), 3),
+        import hashlib
+        digest = hashlib.sha256(res[0].tobytes() + res[1].tobytes()).hexdigest()[:16]
+        print(json.dumps({"opts": s or "default", "lib": os.path.basename(os.environ.get("SME_LIB_PATH", "libsme.so")),
+                          "digest": digest, "kernel_ms": round(float(np.median(kms[1:])), 3),
                           "prep_ms": round(float(np.median(pms[1:])), 3),
                           "wall_ms": round(float(np.median(walls[1:])), 3),
                           "qps": round(a.queries / (np.median(walls[1:]) / 1e3), 1),
