@@ -546,6 +546,19 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
 #pragma omp parallel for schedule(dynamic, 1024)
   for (int64_t g = 0; g < G; g++)
     for (size_t k = 0; k < gout[(size_t)g].size(); k++) gterm[(size_t)go0[(size_t)g] + k] = term_of(gout[(size_t)g][k]);
+  // per thread: local raw id -> its single term id (>= 0), no term (-1) or the
+  // first of several at gterm[-v - 2] (one random access per token below)
+  std::vector<std::vector<int32_t>> ltm((size_t)nthr);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int t = 0; t < nthr; t++) {
+    const std::vector<int32_t> &lm = lmap[(size_t)t];
+    std::vector<int32_t> &o = ltm[(size_t)t];
+    o.resize(lm.size());
+    for (size_t i = 0; i < lm.size(); i++) {
+      const int32_t g = lm[i], a = go0[(size_t)g], b = go0[(size_t)g + 1];
+      o[i] = b - a == 1 ? gterm[(size_t)a] : (b == a ? -1 : -2 - g);
+    }
+  }
   if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "vocab_sort", omp_get_wtime() - t0);
   // 3. per record: term ids -> tf
   std::vector<std::vector<std::pair<int32_t, int32_t>>> rid((size_t)nR);
@@ -558,10 +571,15 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
       auto count = [&](int32_t id) {
         if (tfc[(size_t)id]++ == 0) touched.push_back(id);
       };
-      const std::vector<int32_t> &lm = lmap[(size_t)rthr[(size_t)r]];
+      const std::vector<int32_t> &lm = ltm[(size_t)rthr[(size_t)r]];
       for (int32_t x : rtok[(size_t)r]) {
-        const int32_t g = lm[(size_t)x];
-        for (int32_t k = go0[(size_t)g]; k < go0[(size_t)g + 1]; k++) count(gterm[(size_t)k]);
+        const int32_t v = lm[(size_t)x];
+        if (v >= 0) {
+          count(v);
+        } else if (v <= -2) {
+          const int32_t g = -v - 2;
+          for (int32_t k = go0[(size_t)g]; k < go0[(size_t)g + 1]; k++) count(gterm[(size_t)k]);
+        }
       }
       for (const u16s &w : rterm[(size_t)r]) count(term_of(w));
       auto &out = rid[(size_t)r];

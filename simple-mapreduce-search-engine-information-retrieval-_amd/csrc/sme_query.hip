@@ -1402,19 +1402,27 @@ struct QWinArgs {
 #ifndef SME_QWIN_WAVES
 #define SME_QWIN_WAVES 5
 #endif
+#ifndef SME_QWIN_SPARSE_NT
+#define SME_QWIN_SPARSE_NT 0
+#endif
 __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) {
   // LDS: 2.8 KB per wave + the LUT = 12 KB per workgroup, so LDS does not bound
   // the occupancy (a per-document sparse accumulator, 8 KB per wave, held it at
   // four workgroups per CU): the window's sparse postings are summed per
   // 16-document block for the bounds, and a passing block's documents take
   // their sparse impacts from the listed postings
-  __shared__ uint32_t bsum_all[kWNT / 64][kWin / 16];  // sparse impact sum of every block
+  // per block: sparse postings << 16 | their impact sum (<= 256 x 254 < 2^16), and
+  // the first two postings inline ((r & 15) | q << 4), so a passing block reads its
+  // documents' sparse impacts without searching the list
+  __shared__ uint32_t bsum_all[kWNT / 64][kWin / 16];
+  __shared__ uint16_t bent_all[kWNT / 64][2 * (kWin / 16)];
   __shared__ uint32_t slist_all[kWNT / 64][kSList];   // the window's sparse postings: r | q << 12 | tf << 20
   __shared__ uint16_t blist_all[kWNT / 64][kWin / 16];  // blocks over the gate
   __shared__ uint16_t clist_all[kWNT / 64][kCList];     // documents over the gate
   __shared__ double s_lut[kWinLut];                    // 1 + ln(tf) for tf < 128
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t *bsum = bsum_all[wv], *slist = slist_all[wv];
+  uint16_t *bent = bent_all[wv];
   uint16_t *blist = blist_all[wv], *clist = clist_all[wv];
   for (int i = threadIdx.x; i < kWinLut; i += kWNT) s_lut[i] = i <= a.max_tf ? a.lut[i] : 0.0;
   __syncthreads();
@@ -1513,12 +1521,19 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
           }
         }
         if (e < total) {
+#if SME_QWIN_SPARSE_NT  // the window's sparse postings without L2 allocation (kept for the heavy rows)
+          const int32_t d = __builtin_nontemporal_load(a.docno + pb + e), f = __builtin_nontemporal_load(a.tf + pb + e);
+#else
           const int32_t d = a.docno[pb + e], f = a.tf[pb + e];
+#endif
           const int r = (int)((int64_t)d - wbase);
           // q(tf) computed here (the batch table would be a second dependent load)
           const uint32_t qv = impact(f < kWinLut ? s_lut[f] : a.lut[f], wj, a.alpha);
-          atomicAdd(&bsum[r >> 4], qv);
-          if (listed) slist[e] = (uint32_t)r | (qv << 12) | ((uint32_t)min(f, 0xFFF) << 20);
+          const uint32_t c = atomicAdd(&bsum[r >> 4], (1u << 16) | qv) >> 16;
+          if (listed) {
+            slist[e] = (uint32_t)r | (qv << 12) | ((uint32_t)min(f, 0xFFF) << 20);
+            if (c < 2) bent[2 * (r >> 4) + c] = (uint16_t)((r & 15) | (qv << 4));
+          }
         }
       }
       qwave_sync();
@@ -1534,7 +1549,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     if (total > 0) {
       // + the block's sparse impact sum (>= the sparse sum of any of its documents)
 #pragma unroll
-      for (int m = 0; m < 4; m++) ub[m] += bsum[4 * lane + m];
+      for (int m = 0; m < 4; m++) ub[m] += bsum[4 * lane + m] & 0xFFFFu;
     }
     uint32_t bm = 0;
 #pragma unroll
@@ -1564,7 +1579,17 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
         uint32_t acc[8];          // documents r0 + 2m (low u16), + 1 (high)
 #pragma unroll
         for (int i = 0; i < 8; i++) acc[i] = 0;
-        if (total > 0 && hb) {
+        const uint32_t bw = (total > 0 && hb) ? bsum[blk] : 0u;
+        const uint32_t bs = bw & 0xFFFFu, bn = bw >> 16;
+        if (bs != 0 && listed && bn <= 2) {  // the common case: the inline entries
+          for (uint32_t k2 = 0; k2 < bn; k2++) {
+            const uint32_t ent = bent[2 * blk + k2];
+            const int dr = (int)(ent & 15u);
+            const uint32_t add = (ent >> 4) << ((dr & 1) << 4);
+#pragma unroll
+            for (int i = 0; i < 8; i++) acc[i] += (dr >> 1) == i ? add : 0u;
+          }
+        } else if (bs != 0) {  // (most passing blocks hold no sparse posting)
           if (listed) {
             // the block's sparse postings: per sparse term, its listed entries
             // from the first with r >= r0 while r < r0 + 16
@@ -1589,7 +1614,6 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
             }
           } else {
             // too many postings to list: the block's sum bounds each document
-            const uint32_t bs = bsum[blk];
 #pragma unroll
             for (int i = 0; i < 8; i++) acc[i] = bs | (bs << 16);
           }

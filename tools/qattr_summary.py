@@ -1,0 +1,64 @@
+"""Summarise a tools/gpu_qattr.sh run: per SME_QEXP part switch the k_query_win time
+(tools/qexp.py) and the raw FETCH_SIZE of one batch, and the differences between
+consecutive switches = the time / beyond-L2 bytes of each part of the kernel.
+
+    python tools/qattr_summary.py [gpurun_out/qattr] [--pairs N] > profiles/<name>.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+PARTS = [(0, "full kernel"), (2, "- exact candidate scoring"), (3, "- passing-block impact sums"),
+         (7, "- sparse postings"), (15, "- heavy block bounds (records / skip entries / pipeline left)")]
+WHAT = {0: "candidates: tf bytes, LDS / global tf search, list appends",
+        2: "passing blocks: heavy impact rows (+ inline sparse entries)",
+        3: "sparse postings of the window: docno / tf loads, LDS block sums and list",
+        7: "heavy block bounds: bmq rows",
+        15: "per-pair overhead: position / term records, thresholds, skip entries"}
+
+
+def fetch_bytes(d):
+    tot, n = 0.0, 0
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == "FETCH_SIZE" and "k_query_win" in r["Kernel_Name"]:
+                tot += float(r["Counter_Value"]) * 1024
+                n += 1
+    return tot, n
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    root = args[0] if args else "gpurun_out/qattr"
+    pairs = None
+    if "--pairs" in sys.argv:
+        pairs = float(sys.argv[sys.argv.index("--pairs") + 1])
+    rows = []
+    for e, name in PARTS:
+        t = None
+        log = os.path.join(root, "time_%d.log" % e)
+        if os.path.exists(log):
+            for line in open(log):
+                if line.startswith("{") and '"opts"' in line:
+                    t = json.loads(line)
+        fb, nd = fetch_bytes(os.path.join(root, "f_%d" % e))
+        rows.append({"qexp": e, "switch": name, "kernel_ms": t["kernel_ms"] if t else None,
+                     "fetch_bytes_raw_per_batch": round(fb), "dispatches": nd})
+    parts = []
+    for a, b in zip(rows, rows[1:] + [None]):
+        ms = a["kernel_ms"] - (b["kernel_ms"] if b else 0.0) if a["kernel_ms"] is not None else None
+        fb = a["fetch_bytes_raw_per_batch"] - (b["fetch_bytes_raw_per_batch"] if b else 0)
+        p = {"part": WHAT[a["qexp"]], "ms": round(ms, 3) if ms is not None else None, "fetch_bytes_raw": fb}
+        if pairs:
+            p["fetch_bytes_raw_per_pair"] = round(fb / pairs, 1)
+        parts.append(p)
+    print(json.dumps({"runs": rows, "parts": parts, "pairs": pairs,
+                      "method": "SME_QEXP part switches of the experiment build (timing only; results wrong by "
+                                "design), each run timed by tools/qexp.py and measured by its own rocprofv3 --pmc "
+                                "FETCH_SIZE pass; a part = the difference between consecutive switches"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
