@@ -82,6 +82,22 @@ def test_scale_build_and_queries(sme, synth, name):
             _check_queries(ix, group)
 
 
+@pytest.mark.parametrize("opts", [{"win_sample": 0}, {"cand_cap": 64}])
+def test_scale_queries_window_modes(sme, synth, opts):
+    """The window scorer without the sampled-window stages, and with short
+    candidate lists (overflow re-runs), on the c2-shard golden: docnos and fp64
+    score bits equal to the oracle's in every mode."""
+    g = _gold("c2shard")
+    corpus, ctx, ix = _build(sme, synth, g)
+    for n, v in opts.items():
+        ctx.set_option(n, v)
+    for group in g["queries"]:
+        if group["idf_mode"] == 0:
+            _check_queries(ix, group)
+    ix.close()
+    corpus.close()
+
+
 def test_c2_full_properties(sme, synth):
     import common
     n, V, seed, lo, hi = 1_000_000, 1 << 20, 42, 400, 600
