@@ -53,9 +53,13 @@ __device__ __forceinline__ uint64_t doc_key(uint32_t tie, int32_t d) {
   return ((uint64_t)tie << 32) | ((uint32_t)d ^ 0x80000000u);
 }
 __device__ __forceinline__ int32_t key_doc(uint64_t k) { return (int32_t)((uint32_t)k ^ 0x80000000u); }
-// first-encounter rank of a document first met at query token j with tf f
-// (tf < 2^24: the host checks max_tf in this mode)
-__device__ __forceinline__ uint32_t ref_tie(int j, int f) { return ((uint32_t)j << 24) | (0xFFFFFFu - (uint32_t)f); }
+// first-encounter rank of a document first met at query token j with tf f: the
+// token index above tb bits of (2^tb - 1 - tf).  tb = 24 for batches of queries of
+// <= 256 terms, 22 for longer ones (<= 1024 terms); the host checks max_tf < 2^tb.
+// (`reftie` in the kernels' arguments is tb, 0 for the north-star order.)
+__device__ __forceinline__ uint32_t ref_tie(int j, int f, int tb) {
+  return ((uint32_t)j << tb) | (((1u << tb) - 1u) - (uint32_t)f);
+}
 constexpr uint64_t kNoKey = ~0ull;
 
 // insert (s, d) into the descending register list ts/td (fully unrolled: no
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(kQNT) void k_query(const int64_t *__restrict__ off,
             const double w = __dmul_rn(l, w_idf);
             const double v = acc[d];
             acc[d] = v < 0.0 ? w : __dadd_rn(v, w);
-            if (reftie && v < 0.0) first[d] = ref_tie(i, fv[u]);  // terms run in token order
+            if (reftie && v < 0.0) first[d] = ref_tie(i, fv[u], reftie);  // terms run in token order
           }
           if (stop) break;
           p += (int64_t)kQPer * kQNT;
@@ -699,7 +703,7 @@ struct QBmArgs {
   const int64_t *qoff;
   const int32_t *qorder;
   int nq, k, nseed;
-  int reftie;             // SME_TIE_REFERENCE order (ref_tie keys)
+  int reftie;             // SME_TIE_REFERENCE order: ref_tie's tf bits (0: docno order)
   int32_t *out_d;
   double *out_s;
   uint32_t *out_t;        // optional: tie word of every result (multi-shard merges)
@@ -966,7 +970,7 @@ __global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
             }
             if (f != 0) {
               S = __dadd_rn(S, __dmul_rn(a.lut[f], rld(midf, j)));
-              if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f);
+              if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f, a.reftie);
             }
           }
           key = doc_key(a.reftie ? tie : 0u, d);
@@ -1619,6 +1623,33 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
           }
         }
         for (uint64_t mh = hm; mh;) {
+#if SME_QIMP2
+          // pair impact rows: byte i of the block's 8 = the larger impact of documents
+          // r0 + 2i and r0 + 2i + 1 (a bound of both): each byte into both halves
+          uint2 v[4];
+#pragma unroll
+          for (int g = 0; g < 4; g++) {
+            v[g] = make_uint2(0, 0);
+            if (mh) {
+              const int j = (int)__builtin_ctzll(mh);
+              mh &= mh - 1;
+              if (hb)
+                v[g] = *reinterpret_cast<const uint2 *>(a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j) *
+                                                                    (a.hstride >> 1) + (((x << kWinB) + r0) >> 1));
+            }
+          }
+#pragma unroll
+          for (int g = 0; g < 4; g++) {
+            acc[0] += __builtin_amdgcn_perm(0u, v[g].x, 0x0C000C00u);
+            acc[1] += __builtin_amdgcn_perm(0u, v[g].x, 0x0C010C01u);
+            acc[2] += __builtin_amdgcn_perm(0u, v[g].x, 0x0C020C02u);
+            acc[3] += __builtin_amdgcn_perm(0u, v[g].x, 0x0C030C03u);
+            acc[4] += __builtin_amdgcn_perm(0u, v[g].y, 0x0C000C00u);
+            acc[5] += __builtin_amdgcn_perm(0u, v[g].y, 0x0C010C01u);
+            acc[6] += __builtin_amdgcn_perm(0u, v[g].y, 0x0C020C02u);
+            acc[7] += __builtin_amdgcn_perm(0u, v[g].y, 0x0C030C03u);
+          }
+#else
           uint4 v[4];
 #pragma unroll
           for (int g = 0; g < 4; g++) {
@@ -1640,6 +1671,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
               acc[2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
             }
           }
+#endif
         }
         uint32_t cm = 0;  // documents of the block over the gate
         if (hb) {
@@ -1730,7 +1762,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
                 }
                 if (f != 0) {
                   S = __dadd_rn(S, __dmul_rn(f < kWinLut ? s_lut[f] : a.lut[f], rld(D.idf, j)));
-                  if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f);
+                  if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f, a.reftie);
                 }
               }
               key = doc_key(a.reftie ? tie : 0u, d);
@@ -1882,7 +1914,11 @@ __global__ void k_reset_cnt(const int32_t *qlist, int n, unsigned int *ccnt, uns
   }
 }
 
-// impact rows from tf rows: q(tf) = floor(lut[tf] * idf * alpha) + 1 (0 for tf = 0)
+#ifndef SME_QIMP2
+#define SME_QIMP2 0
+#endif
+// impact rows from tf rows: q(tf) = floor(lut[tf] * idf * alpha) + 1 (0 for tf = 0);
+// SME_QIMP2: one byte per PAIR of documents, the larger of their impacts
 __global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const int32_t *hterm, int64_t H,
                                                    int64_t stride, const double *lut, int max_tf, const double *idf,
                                                    double alpha, uint8_t *imp) {
@@ -1896,15 +1932,28 @@ __global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const i
     ql[f] = (uint8_t)(f == 0 ? 0u : f <= max_tf ? impact(lut[f], wi, alpha) : 255u);
     __syncthreads();
     const uint4 *src = reinterpret_cast<const uint4 *>(tfrow + c * 4096);
-    uint4 *dst = reinterpret_cast<uint4 *>(imp + c * 4096);
     const uint4 v = src[threadIdx.x];
     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#if SME_QIMP2
+    uint32_t o[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const uint32_t a0 = w4[2 * u], a1 = w4[2 * u + 1];
+      auto mx = [&](uint32_t w, int h) {
+        return (uint32_t)max(ql[(w >> (16 * h)) & 0xFF], ql[(w >> (16 * h + 8)) & 0xFF]);
+      };
+      o[u] = mx(a0, 0) | (mx(a0, 1) << 8) | (mx(a1, 0) << 16) | (mx(a1, 1) << 24);
+    }
+    reinterpret_cast<uint2 *>(imp + c * 2048)[threadIdx.x] = make_uint2(o[0], o[1]);
+#else
+    uint4 *dst = reinterpret_cast<uint4 *>(imp + c * 4096);
     uint32_t o[4];
 #pragma unroll
     for (int u = 0; u < 4; u++)
       o[u] = (uint32_t)ql[w4[u] & 0xFF] | ((uint32_t)ql[(w4[u] >> 8) & 0xFF] << 8) |
              ((uint32_t)ql[(w4[u] >> 16) & 0xFF] << 16) | ((uint32_t)ql[w4[u] >> 24] << 24);
     dst[threadIdx.x] = make_uint4(o[0], o[1], o[2], o[3]);
+#endif
   }
 }
 // impact bound rows of the 16-document blocks: q(block's largest tf) (q is
@@ -2103,13 +2152,24 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   if (k > kListCap - kQNT) throw Error(SME_ELIMIT, "top-k with k > 1792");
   if (nq <= 0) return;
   sme_ctx *cx = ix->ctx;
-  const int reftie = cx->cfg.tiebreak == SME_TIE_REFERENCE ? 1 : 0;
-  if (reftie && ix->max_tf > 0xFFFFFF)
-    throw Error(SME_ELIMIT, "reference tie order with a term frequency >= 2^24");
   auto &W = cx->ws;
   int *err = W[63].as<int>(4);
   unsigned long long *wmax = reinterpret_cast<unsigned long long *>(err + 2);
   SME_HIP(hipMemsetAsync(err, 0, 4 * sizeof(int), st));
+  int h_mx = 0;  // the batch's longest query (terms)
+  // reference tie order: ref_tie keys hold the token index above tb tf bits, 24
+  // for queries of <= 256 terms, 22 for longer ones (the batch decides, so doc
+  // shards answering one batch build the same keys)
+  int reftie = 0;
+  if (cx->cfg.tiebreak == SME_TIE_REFERENCE) {
+    hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
+    SME_HIP(hipMemcpyAsync(&h_mx, err + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    reftie = h_mx > 256 ? 22 : 24;
+    if ((int64_t)ix->max_tf >= (int64_t(1) << reftie))
+      throw Error(SME_ELIMIT, reftie == 24 ? "reference tie order with a term frequency >= 2^24"
+                                           : "reference tie order, a query of > 256 terms and a term frequency >= 2^22");
+  }
   const int64_t *off = (const int64_t *)ix->d_off.p;
   const int32_t *dn = (const int32_t *)ix->d_docno_d.p;
   const int32_t *tf = (const int32_t *)ix->d_tf_d.p;
@@ -2130,7 +2190,6 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   int64_t nrows_b = 0;      // distinct batch terms (rows of the skip / impact tables)
   int32_t *skt = nullptr;   // k_query_win: window skip table, transposed
   std::function<void()> build_sk;  // the tile skip table `sk` (k_query_bm), built on demand on the window path
-  int h_mx = 0;
   bool list_kernel = false;  // the streaming kernel with the LDS candidate list ran
   if (tiled) {
     hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
@@ -2535,8 +2594,6 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       SME_HIP(hipStreamSynchronize(st));
     }
     if (h_mx > kMaxQTermsList) throw Error(SME_ELIMIT, "a query has more than 1024 terms");
-    // ref_tie keys hold the token index in 8 bits
-    if (reftie && h_mx > 256) throw Error(SME_ELIMIT, "reference tie order with a query of more than 256 terms");
     list_kernel = k > 32 || h_mx > kMaxQTerms;
     SME_HIP(hipEventRecord(e1, st));
     const unsigned grid = (unsigned)std::min(nq, 1 << 20);

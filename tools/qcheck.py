@@ -1,0 +1,64 @@
+"""Cross-kernel check of a full query batch on the device (no CPU reference): the
+window-major scorer (default) against the streaming kernel (query_kernel=1) and
+the per-query block-max sweep (query_kernel=2), per query docnos and fp64 score
+bits.  Prints the mismatch count per alternative and the first mismatching
+queries.
+    python tools/qcheck.py [--config c2|c5] [--docs N] [--queries Q] [--k K]
+"""
+import argparse
+import hashlib
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "simple-mapreduce-search-engine-information-retrieval-_amd"
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--docs", type=int, default=1_000_000)
+    p.add_argument("--queries", type=int, default=100_000)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--config", default="c2")
+    p.add_argument("--alts", default="query_kernel=1;query_kernel=2")
+    p.add_argument("--check", type=int, default=20000, help="the batch's first queries the alternatives score")
+    a = p.parse_args()
+    import torch
+    sme = importlib.import_module(PKG)
+    synth = importlib.import_module(PKG + ".synth")
+    cfg = dict(c2=dict(V=1 << 20, seed=42, lo=400, hi=600, qseed=7),
+               c5=dict(V=30000, seed=9, lo=40, hi=72, qseed=9))[a.config]
+    dc = sme.DeviceCorpus(a.docs, V=cfg["V"], seed=cfg["seed"], len_lo=cfg["lo"], len_hi=cfg["hi"])
+    ctx = sme.Context(k=1, num_partitions=1, device=0)
+    ctx.load_docno_mapping(synth.mapping_bytes(a.docs))
+    ix = ctx.build_device(dc.ptr, dc.nbytes)
+    dc.close()
+    _, _, _, df = ix.csr()
+    terms, qoff = synth.queries_by_df(df, a.queries, seed=cfg["qseed"])
+    base = ix.query_topk(terms, qoff, a.k)
+    out = {"config": a.config, "queries": a.queries, "k": a.k,
+           "digest_default": hashlib.sha256(base[0].astype("<i4").tobytes() + base[1].astype("<f8").tobytes()).hexdigest()}
+    for alt in [x for x in a.alts.split(";") if x]:
+        n, v = alt.split("=")
+        ctx.set_option(n, int(v))
+        nc = min(a.check, a.queries)
+        d, s = ix.query_topk(terms[:qoff[nc]], qoff[:nc + 1], a.k)
+        ctx.set_option(n, {"query_kernel": 0}.get(n, 0))
+        bd, bs = base[0][:nc], base[1][:nc]
+        bad = np.nonzero(~((d == bd).all(1) & (s.view(np.int64) == bs.view(np.int64)).all(1)))[0]
+        first = []
+        for q in bad[:3].tolist():
+            first.append({"q": q, "terms": terms[qoff[q]:qoff[q + 1]].tolist(), "default": base[0][q][:12].tolist(),
+                          "alt": d[q][:12].tolist()})
+        out[alt] = {"checked": nc, "mismatching_queries": int(len(bad)), "first": first}
+        print(json.dumps(out[alt])[:2000], flush=True)
+    print(json.dumps(out)[:4000])
+
+
+if __name__ == "__main__":
+    main()
