@@ -1623,33 +1623,6 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
           }
         }
         for (uint64_t mh = hm; mh;) {
-#if SME_QIMP2
-          // pair impact rows: byte i of the block's 8 = the larger impact of documents
-          // r0 + 2i and r0 + 2i + 1 (a bound of both): each byte into both halves
-          uint2 v[4];
-#pragma unroll
-          for (int g = 0; g < 4; g++) {
-            v[g] = make_uint2(0, 0);
-            if (mh) {
-              const int j = (int)__builtin_ctzll(mh);
-              mh &= mh - 1;
-              if (hb)
-                v[g] = *reinterpret_cast<const uint2 *>(a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j) *
-                                                                    (a.hstride >> 1) + (((x << kWinB) + r0) >> 1));
-            }
-          }
-#pragma unroll
-          for (int g = 0; g < 4; g++) {
-            acc[0] += __builtin_amdgcn_perm(0u, v[g].x, 0x0C000C00u);
-            acc[1] += __builtin_amdgcn_perm(0u, v[g].x, 0x0C010C01u);
-            acc[2] += __builtin_amdgcn_perm(0u, v[g].x, 0x0C020C02u);
-            acc[3] += __builtin_amdgcn_perm(0u, v[g].x, 0x0C030C03u);
-            acc[4] += __builtin_amdgcn_perm(0u, v[g].y, 0x0C000C00u);
-            acc[5] += __builtin_amdgcn_perm(0u, v[g].y, 0x0C010C01u);
-            acc[6] += __builtin_amdgcn_perm(0u, v[g].y, 0x0C020C02u);
-            acc[7] += __builtin_amdgcn_perm(0u, v[g].y, 0x0C030C03u);
-          }
-#else
           uint4 v[4];
 #pragma unroll
           for (int g = 0; g < 4; g++) {
@@ -1671,7 +1644,6 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
               acc[2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
             }
           }
-#endif
         }
         uint32_t cm = 0;  // documents of the block over the gate
         if (hb) {
@@ -1914,11 +1886,7 @@ __global__ void k_reset_cnt(const int32_t *qlist, int n, unsigned int *ccnt, uns
   }
 }
 
-#ifndef SME_QIMP2
-#define SME_QIMP2 0
-#endif
-// impact rows from tf rows: q(tf) = floor(lut[tf] * idf * alpha) + 1 (0 for tf = 0);
-// SME_QIMP2: one byte per PAIR of documents, the larger of their impacts
+// impact rows from tf rows: q(tf) = floor(lut[tf] * idf * alpha) + 1 (0 for tf = 0)
 __global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const int32_t *hterm, int64_t H,
                                                    int64_t stride, const double *lut, int max_tf, const double *idf,
                                                    double alpha, uint8_t *imp) {
@@ -1934,18 +1902,6 @@ __global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const i
     const uint4 *src = reinterpret_cast<const uint4 *>(tfrow + c * 4096);
     const uint4 v = src[threadIdx.x];
     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#if SME_QIMP2
-    uint32_t o[2];
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-      const uint32_t a0 = w4[2 * u], a1 = w4[2 * u + 1];
-      auto mx = [&](uint32_t w, int h) {
-        return (uint32_t)max(ql[(w >> (16 * h)) & 0xFF], ql[(w >> (16 * h + 8)) & 0xFF]);
-      };
-      o[u] = mx(a0, 0) | (mx(a0, 1) << 8) | (mx(a1, 0) << 16) | (mx(a1, 1) << 24);
-    }
-    reinterpret_cast<uint2 *>(imp + c * 2048)[threadIdx.x] = make_uint2(o[0], o[1]);
-#else
     uint4 *dst = reinterpret_cast<uint4 *>(imp + c * 4096);
     uint32_t o[4];
 #pragma unroll
@@ -1953,7 +1909,6 @@ __global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const i
       o[u] = (uint32_t)ql[w4[u] & 0xFF] | ((uint32_t)ql[(w4[u] >> 8) & 0xFF] << 8) |
              ((uint32_t)ql[(w4[u] >> 16) & 0xFF] << 16) | ((uint32_t)ql[w4[u] >> 24] << 24);
     dst[threadIdx.x] = make_uint4(o[0], o[1], o[2], o[3]);
-#endif
   }
 }
 // impact bound rows of the 16-document blocks: q(block's largest tf) (q is
