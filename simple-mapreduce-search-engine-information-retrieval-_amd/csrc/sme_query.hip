@@ -852,7 +852,7 @@ __global__ __launch_bounds__(64) void k_query_bm(QBmArgs a) {
         // entry e belongs to the last term j of spm with pre_j <= e
         const int32_t cj = ((spm >> lane) & 1) ? me - mc : 0;
         const int32_t incl = wave_incl_sum(cj), prej = incl - cj;
-        const int32_t total = __shfl(incl, 63, 64);
+        const int32_t total = __builtin_amdgcn_readlane(incl, 63);
         const int64_t plo = mb + mc;
         for (int32_t e0 = 0; e0 < total; e0 += 256) {
           const int nu = min(4, (total - e0 + 63) >> 6);  // 64-entry chunks in this step (wave-uniform)
@@ -1206,13 +1206,17 @@ __global__ void k_query_pos(const int32_t *qorder, const int64_t *qoff, int nq, 
     out[p] = QPos{qoff[q] - tbase, q, (int32_t)(qoff[q + 1] - qoff[q])};
   }
 }
-// Streamed records (term / position records, thresholds): every window pass
-// reads the whole batch's once, with no reuse inside the pass, so they are
-// loaded non-temporally and do not evict the window's index rows from L2.
+// Streamed records: every window pass reads the whole batch's once, with no
+// reuse inside the pass, so the per-lane term records are loaded non-temporally
+// (they do not evict the window's index rows from L2); the wave-uniform position
+// records and thresholds go through the scalar cache (ld_uni below).
 typedef uint32_t qu32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ QDesc ld_desc_nt(const QDesc *d, int64_t q0, int nt, int lane) {
   if (lane < nt) {
-    const qu32x4 *p = reinterpret_cast<const qu32x4 *>(d + q0 + lane);
+    // (q0 is wave-uniform: scalar base + 32-bit lane offset, no per-lane 64-bit address)
+    uint32_t lo = (uint32_t)lane << 5;
+    asm volatile("" : "+v"(lo));  // (keeps the compiler from hoisting d + 32 lane into a 64-bit register pair)
+    const qu32x4 *p = reinterpret_cast<const qu32x4 *>(reinterpret_cast<const char *>(d + q0) + lo);
     const qu32x4 u = __builtin_nontemporal_load(p), v = __builtin_nontemporal_load(p + 1);
     QDesc r;
     r.mb = (int64_t)(((uint64_t)u.y << 32) | u.x);
@@ -1225,8 +1229,14 @@ __device__ __forceinline__ QDesc ld_desc_nt(const QDesc *d, int64_t q0, int nt, 
   }
   return QDesc{0, 0, 0, -1, 0, 0.0};
 }
-__device__ __forceinline__ QPos ld_pos_nt(const QPos *p) {
-  const qu32x4 u = __builtin_nontemporal_load(reinterpret_cast<const qu32x4 *>(p));
+// wave-uniform records through the scalar cache (read-only here: written by
+// earlier launches), so the pipelined next-query records hold no VGPRs
+template <typename T>
+__device__ __forceinline__ T ld_uni(const T *p) {
+  return *reinterpret_cast<const __attribute__((address_space(4))) T *>(reinterpret_cast<uintptr_t>(p));
+}
+__device__ __forceinline__ QPos ld_pos_uni(const QPos *p) {
+  const qu32x4 u = ld_uni(reinterpret_cast<const qu32x4 *>(p));
   return QPos{(int64_t)(((uint64_t)u.y << 32) | u.x), (int32_t)u.z, (int32_t)u.w};
 }
 __device__ __forceinline__ QDesc ld_desc(const QDesc *d, int64_t q0, int nt, int lane) {
@@ -1402,9 +1412,18 @@ struct QWinArgs {
   int exper;                   // SME_EXPERIMENTS timing switches (0 in the product)
 };
 
-// waves per SIMD the register allocation targets (LDS allows far more)
+// waves per SIMD the register allocation targets (LDS allows far more): six,
+// with two heavy terms' impact loads in flight per passing block (SME_QIMPG) and
+// the uniform records in SGPRs, fit 80 VGPRs without spilling (c3 31.2 ms at five
+// waves / four loads -> 28.3 ms); seven and eight waves gain nothing more
 #ifndef SME_QWIN_WAVES
-#define SME_QWIN_WAVES 5
+#define SME_QWIN_WAVES 6
+#endif
+#ifndef SME_QIMPG
+#define SME_QIMPG 2
+#endif
+#ifndef SME_QFB
+#define SME_QFB 8
 #endif
 #ifndef SME_QWIN_SPARSE_NT
 #define SME_QWIN_SPARSE_NT 0
@@ -1424,7 +1443,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
   __shared__ uint16_t blist_all[kWNT / 64][kWin / 16];  // blocks over the gate
   __shared__ uint16_t clist_all[kWNT / 64][kCList];     // documents over the gate
   __shared__ double s_lut[kWinLut];                    // 1 + ln(tf) for tf < 128
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   uint32_t *bsum = bsum_all[wv], *slist = slist_all[wv];
   uint16_t *bent = bent_all[wv];
   uint16_t *blist = blist_all[wv], *clist = clist_all[wv];
@@ -1446,17 +1465,17 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
   for (int m = 0; m < 4; m++) bsum[m * 64 + lane] = 0;
   // software pipeline over this wave's queries: the next query's position
   // record, term records, threshold and skip entries load while this one runs
-  QPos P = ld_pos_nt(a.qpos + pos);
+  QPos P = ld_pos_uni(a.qpos + pos);
   QDesc D = ld_desc_nt(a.desc, P.q0, P.nt, lane);
-  double th0 = __builtin_nontemporal_load(a.th0 + P.q);
-  uint64_t thk = __builtin_nontemporal_load(a.thk + P.q);
+  double th0 = ld_uni(a.th0 + P.q);
+  uint64_t thk = ld_uni(a.thk + P.q);
   int32_t mc = 0, me = 0;
   if (D.mdf > 0 && D.hr < 0) {
     mc = a.skt[x * a.nrows + D.brow];
     me = a.skt[(x + 1) * a.nrows + D.brow];
   }
   QPos NP{0, 0, 0};  // next query's position record, loaded a pair ahead
-  if (pos + kWNT / 64 < p_hi) NP = ld_pos_nt(a.qpos + pos + kWNT / 64);
+  if (pos + kWNT / 64 < p_hi) NP = ld_pos_uni(a.qpos + pos + kWNT / 64);
   for (;;) {
     const int npos = pos + kWNT / 64;
     const bool hasn = npos < p_hi;
@@ -1467,9 +1486,9 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     QPos NNP{0, 0, 0};
     if (hasn) {
       ND = ld_desc_nt(a.desc, NP.q0, NP.nt, lane);
-      nth0 = __builtin_nontemporal_load(a.th0 + NP.q);
-      nthk = __builtin_nontemporal_load(a.thk + NP.q);
-      if (npos + kWNT / 64 < p_hi) NNP = ld_pos_nt(a.qpos + npos + kWNT / 64);
+      nth0 = ld_uni(a.th0 + NP.q);
+      nthk = ld_uni(a.thk + NP.q);
+      if (npos + kWNT / 64 < p_hi) NNP = ld_pos_uni(a.qpos + npos + kWNT / 64);
     }
 #ifdef SME_EXPERIMENTS  // timing switches: 4 = no sparse terms, 8 = no heavy terms
     const uint64_t hm = (a.exper & 8) ? 0ull : (uint64_t)__ballot(D.hr >= 0);
@@ -1478,7 +1497,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     const uint64_t hm = (uint64_t)__ballot(D.hr >= 0);
     const uint64_t sm = (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
 #endif
-    const uint32_t gate = gate_of(th0, a.alpha);
+    const uint32_t gate = (uint32_t)__builtin_amdgcn_readfirstlane((int)gate_of(th0, a.alpha));
     // heavy terms' block maxima: one dword per term = the impact bound of this
     // lane's four 16-document blocks (index-resident bmq rows), all loads in flight
     uint32_t ub0 = 0, ub1 = 0;  // blocks 4 lane + {0, 1} | {2, 3} as u16 pairs
@@ -1508,7 +1527,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     // sums of passing blocks and the candidates' tf lookups
     const int32_t cj = ((sm >> lane) & 1) ? me - mc : 0;
     const int32_t incl = wave_incl_sum(cj), prej = incl - cj;
-    const int32_t total = __shfl(incl, 63, 64);
+    const int32_t total = __builtin_amdgcn_readlane(incl, 63);
     const bool listed = total <= kSList;  // else the block sum bounds every document of the block
     if (total > 0) {
       const int64_t plo = D.mb + mc;
@@ -1560,7 +1579,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     for (int m = 0; m < 4; m++) bm |= (ub[m] >= gate ? 1u : 0u) << m;
     const int32_t bl = __popc(bm);
     const int32_t bincl = wave_incl_sum(bl);
-    const int32_t nblk = __shfl(bincl, 63, 64);
+    const int32_t nblk = __builtin_amdgcn_readlane(bincl, 63);
     if (a.stats && lane == 0) {
       atomicAdd(a.stats + 0, 1ull);
       atomicAdd(a.stats + 1, (unsigned long long)total);
@@ -1623,9 +1642,9 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
           }
         }
         for (uint64_t mh = hm; mh;) {
-          uint4 v[4];
+          uint4 v[SME_QIMPG];
 #pragma unroll
-          for (int g = 0; g < 4; g++) {
+          for (int g = 0; g < SME_QIMPG; g++) {
             v[g] = make_uint4(0, 0, 0, 0);
             if (mh) {
               const int j = (int)__builtin_ctzll(mh);
@@ -1636,7 +1655,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
             }
           }
 #pragma unroll
-          for (int g = 0; g < 4; g++) {
+          for (int g = 0; g < SME_QIMPG; g++) {
             const uint32_t w4[4] = {v[g].x, v[g].y, v[g].z, v[g].w};
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -1656,7 +1675,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
         // candidates listed in LDS, scored one per lane
         const int32_t cl = __popc(cm);
         const int32_t cincl = wave_incl_sum(cl);
-        const int32_t ncand = (a.exper & 2) ? 0 : __shfl(cincl, 63, 64);
+        const int32_t ncand = (a.exper & 2) ? 0 : __builtin_amdgcn_readlane(cincl, 63);
         if (a.stats && lane == 0) atomicAdd(a.stats + 4, (unsigned long long)ncand);
         for (int32_t k0 = 0; k0 < ncand; k0 += kCList) {
           const int32_t kn = min(ncand - k0, kCList);
@@ -1682,7 +1701,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
                 uint64_t mh = hm;
                 uint32_t fb[8];
 #pragma unroll
-                for (int c = 0; c < 8; c++) {
+                for (int c = 0; c < SME_QFB; c++) {
                   fb[c] = 0;
                   if (mh) {
                     const int j = (int)__builtin_ctzll(mh);
@@ -1691,14 +1710,14 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
                   }
                 }
 #pragma unroll
-                for (int c = 0; c < 8; c++) hb |= (uint64_t)fb[c] << (8 * c);
+                for (int c = 0; c < SME_QFB; c++) hb |= (uint64_t)fb[c] << (8 * c);
               }
               int hseen = 0;
               for (uint64_t m = amask; m; m &= m - 1) {
                 const int j = (int)__builtin_ctzll(m);
                 int f = 0;
                 if ((hm >> j) & 1) {
-                  if (hseen < 8) {
+                  if (hseen < SME_QFB) {
                     f = (int)(hb & 0xFFu);
                     hb >>= 8;
                   } else {
