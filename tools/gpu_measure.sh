@@ -2,7 +2,9 @@
 #   PART=a  parity tests (-m gpu), smoke(), the default bench line -> gpurun_out/{pytest_gpu,smoke,bench}.log
 #   PART=b  rocprofv3 kernel-trace stats of a c2 bench run (checks + serializer included), then separate
 #           PMC passes (FETCH_SIZE, WRITE_SIZE; one counter group per run) over the build, serializer and
-#           query kernels -> gpurun_out/{prof,pmc_f,pmc_w}
+#           query kernels -> gpurun_out/{prof,pmc_f,pmc_w}; then, here,
+#           SME_PMC_BATCHES=40 python tools/pmc_summary.py 1000000 1048576 gpurun_out/pmc_f gpurun_out/pmc_w
+#           writes profiles/pmc_traffic.json (the first 40 query batches are the headline c3 ones)
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
 if [ "${PART:-a}" = a ]; then

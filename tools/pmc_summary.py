@@ -25,11 +25,13 @@ def base_name(n):
     n = n.strip()
     if n.startswith("void "):
         n = n[5:]
+    n = n.replace("(anonymous namespace)::", "")
     for c in "(<":
         i = n.find(c)
         if i >= 0:
             n = n[:i]
-    return n.strip()
+    # namespace qualifiers ('sme::k_tok_fast' -> 'k_tok_fast')
+    return n.strip().rsplit("::", 1)[-1]
 
 
 def per_kernel(d, counter):
