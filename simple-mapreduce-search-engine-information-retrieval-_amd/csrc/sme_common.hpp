@@ -105,15 +105,30 @@ inline uint64_t next_pow2(uint64_t x) {
 // ---- device scans ---------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Inclusive wave sum (every lane of the wave active).  32-bit values scan with
+// DPP moves and no LDS: shifts 1, 2, 4, 8 inside each 16-lane row, then the
+// row_bcast:15 / row_bcast:31 carries into rows 1, 3 and 2, 3 (6 adds, where
+// the ds_bpermute ladder took 6 LDS round trips and ~24 VALU).
 template <typename T>
 __device__ __forceinline__ T wave_incl_sum(T v) {
-  const int l = lane_id();
+  if constexpr (sizeof(T) == 4) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return (T)x;
+  } else {
+    const int l = lane_id();
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    T u = __shfl_up(v, o, 64);
-    if (l >= o) v += u;
+    for (int o = 1; o < 64; o <<= 1) {
+      T u = __shfl_up(v, o, 64);
+      if (l >= o) v += u;
+    }
+    return v;
   }
-  return v;
 }
 template <typename T>
 __device__ __forceinline__ T wave_incl_max(T v) {

@@ -52,6 +52,7 @@ struct sme_ctx {
   int64_t opt_kgram_rank = 0;     // "kgram_rank": 1 = K >= 2 gram keys by iterated ranking even when packed ids fit
   int64_t opt_win_slice = 256;    // "win_slice": queries per k_query_win workgroup slice (>= 1)
   int64_t opt_win_sample = 1;     // "win_sample": 1 = every 8th window first, thresholds raised, then the rest
+  int64_t opt_win_stage_min = 16;  // "win_stage_min": windows of the first stage (at least; the stage count follows)
   int64_t opt_query_budget = 0;  // "query_table_budget": per-batch skip-table bytes (0: a quarter of free HBM)
   int64_t opt_corpus_keep = int64_t(16) << 30;  // "corpus_keep_bytes": host-corpus builds keep their device copy
                                                 // (no hipMalloc next build) only up to this size
@@ -117,6 +118,10 @@ struct sme_index {
   sme::DevBuf d_hrow_of;  // int32 [V] heavy row or -1
   sme::DevBuf d_heavy;    // u8 [H][T * 1024] tf | [H][T * 64] bm16 | [H][T] bm1k
   const uint8_t *q_tfrow = nullptr, *q_bm16 = nullptr, *q_bm1k = nullptr, *q_imp = nullptr, *q_bmq = nullptr;
+  // k_query_win's sparse postings, one word per docno-order posting of a term
+  // without a heavy row: (docno - dmin) mod 4096 | q(tf) << 12 | min(tf, 4095) << 20
+  sme::DevBuf d_spk;
+  const uint32_t *q_spk = nullptr;
   double q_alpha = 1.0;                 // impact scale 253.5 / (largest weight of any term)
   unsigned long long q_wmax_bits = 0;   // that weight's bits
   int64_t q_T = 0, q_H = 0, q_div = -1;
@@ -128,7 +133,7 @@ struct sme_index {
   explicit sme_index(sme_ctx *c) : ctx(c) {
     c->live_indexes++;
     for (sme::DevBuf *b : {&d_term_off, &d_term_chars, &d_off, &d_docno_d, &d_tf_d, &d_w, &d_idf, &d_lut, &d_gram, &d_docno_o,
-                           &d_tf_o, &d_rec_docno, &d_rec_first, &d_ser, &d_hrow_of, &d_heavy})
+                           &d_tf_o, &d_rec_docno, &d_rec_first, &d_ser, &d_hrow_of, &d_heavy, &d_spk})
       b->pool = &c->pool;
   }
 };

@@ -1391,6 +1391,7 @@ struct QWinArgs {
   const QDesc *desc;
   const QPos *qpos;
   const int32_t *docno, *tf;   // docno-order CSR
+  const uint32_t *spk;         // sparse posting words of the docno-order CSR (prepare_queries)
   const double *lut;
   int max_tf;
   const int32_t *skt;          // window skip table, transposed [nwin + 1][nrows]
@@ -1534,27 +1535,23 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
       for (int32_t e0 = 0; e0 < total; e0 += 64) {
         const int32_t e = e0 + lane;
         int64_t pb = 0;
-        double wj = 0.0;
         for (uint64_t m = sm; m; m &= m - 1) {
           const int j = (int)__builtin_ctzll(m);
           const int32_t pj = __builtin_amdgcn_readlane(prej, j);
-          if (e >= pj) {
-            pb = rl64(plo, j) - pj;
-            wj = rld(D.idf, j);
-          }
+          if (e >= pj) pb = rl64(plo, j) - pj;
         }
         if (e < total) {
+          // the posting's word: its place in the window, q(tf) and tf, as the list keeps them
 #if SME_QWIN_SPARSE_NT  // the window's sparse postings without L2 allocation (kept for the heavy rows)
-          const int32_t d = __builtin_nontemporal_load(a.docno + pb + e), f = __builtin_nontemporal_load(a.tf + pb + e);
+          const uint32_t pw = __builtin_nontemporal_load(a.spk + pb + e);
 #else
-          const int32_t d = a.docno[pb + e], f = a.tf[pb + e];
+          const uint32_t pw = a.spk[pb + e];
 #endif
-          const int r = (int)((int64_t)d - wbase);
-          // q(tf) computed here (the batch table would be a second dependent load)
-          const uint32_t qv = impact(f < kWinLut ? s_lut[f] : a.lut[f], wj, a.alpha);
+          const int r = (int)(pw & 0xFFFu);
+          const uint32_t qv = (pw >> 12) & 0xFFu;
           const uint32_t c = atomicAdd(&bsum[r >> 4], (1u << 16) | qv) >> 16;
           if (listed) {
-            slist[e] = (uint32_t)r | (qv << 12) | ((uint32_t)min(f, 0xFFF) << 20);
+            slist[e] = pw;
             if (c < 2) bent[2 * (r >> 4) + c] = (uint16_t)((r & 15) | (qv << 4));
           }
         }
@@ -1956,6 +1953,28 @@ __global__ __launch_bounds__(256) void k_heavy_bmq(const uint8_t *bm16, const in
     }
   }
 }
+// k_query_win's sparse posting words (index-resident, like the impact rows):
+// (docno - dmin) mod 4096 = the posting's place in its 4096-document window, its
+// impact q(tf) at the index's scale and its tf (4095 = "4095 or more"), so the
+// window pass loads one word per posting and does no arithmetic on it.  One
+// wave per term; terms with a heavy row are skipped (the window pass reads rows).
+__global__ __launch_bounds__(256) void k_sparse_pack(const int64_t *off, int64_t V, const int32_t *hrow_of,
+                                                     const int32_t *docno, const int32_t *tf, const double *lut,
+                                                     const double *idf, double alpha, int64_t dmin, uint32_t *spk) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwv = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t t = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); t < V; t += nwv) {
+    if (hrow_of && hrow_of[t] >= 0) continue;  // (wave-uniform)
+    const int64_t b = off[t], e = off[t + 1];
+    const double wi = idf[t];
+    for (int64_t i = b + lane; i < e; i += 64) {
+      const int32_t f = tf[i];
+      spk[i] = (uint32_t)(((int64_t)docno[i] - dmin) & (kWin - 1)) | (impact(lut[f], wi, alpha) << 12) |
+               ((uint32_t)min(f, 0xFFF) << 20);
+    }
+  }
+}
+
 // largest weight of any term (its max tf is the first posting of the
 // reduce-order CSR): the index's impact scale alpha = 253.5 / wmax
 __global__ void k_index_wmax(const int64_t *off, int64_t V, const int32_t *tf_o, const double *lut,
@@ -2060,6 +2079,24 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
       ix->q_bm1k = bm1k;
     }
     ix->q_H = H;
+  }
+  // sparse posting words for the window pass, if 4 B per posting fits a quarter
+  // of the free memory (else query_topk takes the block-max path)
+  ix->q_spk = nullptr;
+  if (T > 0 && ix->P > 0) {
+    size_t fr = 0, tot = 0;
+    SME_HIP(hipMemGetInfo(&fr, &tot));
+    const size_t need = (size_t)ix->P * sizeof(uint32_t);
+    if (ix->d_spk.cap >= need || need <= fr / 4) {
+      uint32_t *spk = ix->d_spk.as<uint32_t>((size_t)ix->P);
+      const int32_t *hro = ix->q_H > 0 ? (const int32_t *)ix->d_hrow_of.p : nullptr;
+      hipLaunchKernelGGL(k_sparse_pack, dim3((unsigned)std::min<int64_t>((V + 3) / 4, 65536)), dim3(256), 0, st,
+                         (const int64_t *)ix->d_off.p, V, hro, (const int32_t *)ix->d_docno_d.p,
+                         (const int32_t *)ix->d_tf_d.p, (const double *)ix->d_lut.p, (const double *)ix->d_idf.p,
+                         ix->q_alpha, ix->dmin, spk);
+      SME_CHECK_LAUNCH();
+      ix->q_spk = spk;
+    }
   }
   SME_HIP(hipEventRecord(e1, st));
   SME_HIP(hipEventSynchronize(e1));
@@ -2193,7 +2230,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       // of <= 64 terms is answered on this path
       size_t fr = 0, tot = 0;
       SME_HIP(hipMemGetInfo(&fr, &tot));
-      const bool winp = cx->opt_query_kernel == 0;
+      const bool winp = cx->opt_query_kernel == 0 && ix->q_spk;
       // (the window path holds two tables of this size: the row-major change
       // points W[29] and the window-major skip table W[31])
       const double need = (double)nrows * (double)((winp ? (T >> 2) : T) + 1) * 4.0 * (winp ? 2.0 : 1.0);
@@ -2238,7 +2275,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
                                0, st, nrows, T, skw);
             SME_CHECK_LAUNCH();
           };
-          if (cx->opt_query_kernel == 0) {
+          if (winp) {
             const int64_t nwin = T >> 2, ne = nrows * (nwin + 1);
             skt = W[31].as<int32_t>(ne);
             int32_t *rm = W[29].as<int32_t>(ne);  // row-major change points (prep only)
@@ -2339,7 +2376,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     else
       hipLaunchKernelGGL(k_query_bm<512>, dim3(wgrid), dim3(64), 0, st, x);
   };
-  const bool win = tiled && cx->opt_query_kernel == 0;
+  const bool win = tiled && cx->opt_query_kernel == 0 && ix->q_spk;
   int64_t n_ovf = 0;
   bool subset_ran = false;  // the overflow fallback answered queries as nested compact batches
   QTimes sub_times;
@@ -2401,6 +2438,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     wa.qpos = qpos;
     wa.docno = dn;
     wa.tf = tf;
+    wa.spk = ix->q_spk;
     wa.lut = lut;
     wa.max_tf = ix->max_tf;
     wa.skt = skt;
@@ -2441,7 +2479,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     // only the first one runs on the seed threshold, and L makes it small (about
     // 16 windows, 1/8 .. 1/256 of the index).
     int L = 3;
-    while (L < 8 && (nwin >> (L + 1)) >= 16) L++;
+    while (L < 8 && (nwin >> (L + 1)) >= cx->opt_win_stage_min) L++;
     int64_t n_samp = 0, stage_start[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     {
       std::vector<int32_t> &h = cx->h_wlist;  // outlives the async copy

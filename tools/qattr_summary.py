@@ -19,14 +19,16 @@ WHAT = {0: "candidates: tf bytes, LDS / global tf search, list appends",
         15: "per-pair overhead: position / term records, thresholds, skip entries"}
 
 
-def fetch_bytes(d):
-    tot, n = 0.0, 0
+def counters(d):
+    """{counter: total over the run's k_query_win dispatches} (FETCH_SIZE in bytes), dispatches"""
+    tot, disp = {}, set()
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == "FETCH_SIZE" and "k_query_win" in r["Kernel_Name"]:
-                tot += float(r["Counter_Value"]) * 1024
-                n += 1
-    return tot, n
+            if "k_query_win" in r["Kernel_Name"]:
+                v = float(r["Counter_Value"]) * (1024 if r["Counter_Name"] == "FETCH_SIZE" else 1)
+                tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + v
+                disp.add(r["Dispatch_Id"])
+    return tot, len(disp)
 
 
 def main():
@@ -43,9 +45,13 @@ def main():
             for line in open(log):
                 if line.startswith("{") and '"opts"' in line:
                     t = json.loads(line)
-        fb, nd = fetch_bytes(os.path.join(root, "f_%d" % e))
-        rows.append({"qexp": e, "switch": name, "kernel_ms": t["kernel_ms"] if t else None,
-                     "fetch_bytes_raw_per_batch": round(fb), "dispatches": nd})
+        cs, nd = counters(os.path.join(root, "f_%d" % e))
+        row = {"qexp": e, "switch": name, "kernel_ms": t["kernel_ms"] if t else None,
+               "fetch_bytes_raw_per_batch": round(cs.get("FETCH_SIZE", 0.0)), "dispatches": nd}
+        for c, v in sorted(cs.items()):
+            if c != "FETCH_SIZE":
+                row[c] = round(v)
+        rows.append(row)
     parts = []
     for a, b in zip(rows, rows[1:] + [None]):
         ms = a["kernel_ms"] - (b["kernel_ms"] if b else 0.0) if a["kernel_ms"] is not None else None
@@ -53,6 +59,10 @@ def main():
         p = {"part": WHAT[a["qexp"]], "ms": round(ms, 3) if ms is not None else None, "fetch_bytes_raw": fb}
         if pairs:
             p["fetch_bytes_raw_per_pair"] = round(fb / pairs, 1)
+        for c in [c for c in a if c.startswith("SQ_")]:
+            p[c] = a[c] - (b.get(c, 0) if b else 0)
+            if pairs:
+                p[c + "_per_pair"] = round(p[c] / pairs, 1)
         parts.append(p)
     print(json.dumps({"runs": rows, "parts": parts, "pairs": pairs,
                       "method": "SME_QEXP part switches of the experiment build (timing only; results wrong by "
