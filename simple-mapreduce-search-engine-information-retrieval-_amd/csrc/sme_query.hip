@@ -1530,6 +1530,10 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     const int32_t incl = wave_incl_sum(cj), prej = incl - cj;
     const int32_t total = __builtin_amdgcn_readlane(incl, 63);
     const bool listed = total <= kSList;  // else the block sum bounds every document of the block
+    // a block holds at most 16 postings per sparse term: with more than 16 sparse
+    // terms an unlisted window's block may hold > 258 postings, whose 16-bit impact
+    // sum can wrap -- such blocks pass the bounds and all their documents are scored
+    const bool wide_nl = !listed && __popcll(sm) > 16;
     if (total > 0) {
       const int64_t plo = D.mb + mc;
       for (int32_t e0 = 0; e0 < total; e0 += 64) {
@@ -1569,7 +1573,10 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     if (total > 0) {
       // + the block's sparse impact sum (>= the sparse sum of any of its documents)
 #pragma unroll
-      for (int m = 0; m < 4; m++) ub[m] += bsum[4 * lane + m] & 0xFFFFu;
+      for (int m = 0; m < 4; m++) {
+        const uint32_t bw = bsum[4 * lane + m];
+        ub[m] += wide_nl ? (bw ? 0x10000u : 0u) : (bw & 0xFFFFu);
+      }
     }
     uint32_t bm = 0;
 #pragma unroll
@@ -1668,6 +1675,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
             if ((acc[i] & 0xFFFFu) >= gate) cm |= 1u << (2 * i);
             if ((acc[i] >> 16) >= gate) cm |= 1u << (2 * i + 1);
           }
+          if (wide_nl && bw != 0u) cm = 0xFFFFu;  // (its sum may have wrapped: every document)
         }
         // candidates listed in LDS, scored one per lane
         const int32_t cl = __popc(cm);

@@ -301,6 +301,38 @@ def test_queries_multi_tile(sme, synth):
         ix.query_topk(too_long, np.array([0, 1025], dtype=np.int64), 10)
 
 
+def test_queries_block_sum_past_16_bits(sme, synth):
+    """A 16-document block whose sparse impact sum passes 2^16 in a window whose
+    postings are too many to list: 27 rare terms in every document of two groups
+    of 16 -- group A in window 0 (first stage), group B in window 3 (last stage),
+    where one term occurs twice, so B outranks A and B's block must pass the gate
+    that A's scores raised.  Its true sum (16 x (26 x 150 + 254) = 66,464) wraps to
+    928 in 16 bits; the window kernel must still score B."""
+    n = 17 * 4096
+    rare = ["xq" + a + b for a in "bcdfg" for b in "hjklmn"][:27]
+    fill = ["zub", "zuc", "zud", "zuf", "zug"]
+    ids = synth.docids(n)
+    A, B = set(range(16)), set(range(3 * 4096 + 32, 3 * 4096 + 48))
+    docs = []
+    for i in range(n):
+        words = [fill[i % 5], fill[(i + 2) % 5]]
+        if i in A:
+            words += rare
+        if i in B:
+            words += rare + rare[:1]
+        docs.append(b"<DOC>\n<DOCNO>%s</DOCNO>\n<TEXT>\n%s\n</TEXT>\n</DOC>\n" % (ids[i].encode(), " ".join(words).encode()))
+    ix, ref = _check_build(sme, b"".join(docs), ids)
+    names = [ix.term(i) for i in range(ix.V)]
+    terms = np.array([names.index(w) for w in rare], dtype=np.int32)
+    qoff = np.array([0, len(terms)], dtype=np.int64)
+    dn, sc = ix.query_topk(terms, qoff, 10)
+    assert ix.ctx.last_build_profile()["query_kernel_name"] == "k_query_win"
+    rd, rs = ref.query(rare, 10, 0, 0)
+    assert dn[0].tolist() == rd and np.array_equal(sc[0], np.array(rs))
+    dn2, sc2 = _query_opts(ix, terms, qoff, 10, query_kernel=1)
+    assert np.array_equal(dn, dn2) and np.array_equal(sc, sc2)
+
+
 def test_queries_dense_rows(sme, synth):
     """Hot terms read from per-batch dense tf rows: a small vocabulary makes most
     terms dense, a few documents push one hot term's tf past 255 (its row is
