@@ -1413,12 +1413,13 @@ struct QWinArgs {
   int exper;                   // SME_EXPERIMENTS timing switches (0 in the product)
 };
 
-// waves per SIMD the register allocation targets (LDS allows far more): six,
-// with two heavy terms' impact loads in flight per passing block (SME_QIMPG) and
-// the uniform records in SGPRs, fit 80 VGPRs without spilling (c3 31.2 ms at five
-// waves / four loads -> 28.3 ms); seven and eight waves gain nothing more
+// waves per SIMD the register allocation targets (16 KB of LDS per workgroup
+// allows eight): with two heavy terms' impact loads in flight per passing block
+// (SME_QIMPG), the uniform records in SGPRs and the biased block accumulators the
+// kernel fits 64 VGPRs without spilling (c3: 31.2 ms at five waves / four loads,
+// 28.3 at six, 23.7 at eight with the scans and posting words of round 5)
 #ifndef SME_QWIN_WAVES
-#define SME_QWIN_WAVES 6
+#define SME_QWIN_WAVES 8
 #endif
 #ifndef SME_QIMPG
 #define SME_QIMPG 2
@@ -1598,6 +1599,11 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
       }
       qwave_sync();
       const uint64_t amask = hm | sm;
+      // every u16 accumulator starts at 2^15 - gate, so A(d) >= gate is
+      // its bit 15 (A(d) < 2^14 and gate <= 2^14 + 1 leave no carry between halves;
+      // a gate past 2^15 - 1 takes no bias, and no document reaches bit 15)
+      const uint32_t bias = gate > 0x7FFFu ? 0u : 0x8000u - gate;
+      const uint32_t bias2 = bias | (bias << 16);
       // one passing block per lane: exact A(d) of its 16 documents
       for (int32_t b0 = 0; b0 < nblk; b0 += 64) {
         const bool hb = b0 + lane < nblk;
@@ -1605,10 +1611,10 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
         const int r0 = blk << 4;  // first document of the block in the window
         uint32_t acc[8];          // documents r0 + 2m (low u16), + 1 (high)
 #pragma unroll
-        for (int i = 0; i < 8; i++) acc[i] = 0;
+        for (int i = 0; i < 8; i++) acc[i] = bias2;
         const uint32_t bw = (total > 0 && hb) ? bsum[blk] : 0u;
         const uint32_t bs = bw & 0xFFFFu, bn = bw >> 16;
-        if (bs != 0 && listed && bn <= 2) {  // the common case: the inline entries
+        if (bs != 0 && listed && bn <= 2) {  // the common case: the block's inline entries
           for (uint32_t k2 = 0; k2 < bn; k2++) {
             const uint32_t ent = bent[2 * blk + k2];
             const int dr = (int)(ent & 15u);
@@ -1641,8 +1647,10 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
             }
           } else {
             // too many postings to list: the block's sum bounds each document
+            // (clamped: any sum >= 2^14 passes every gate, A(d) <= 64 x 254 < 2^14)
+            const uint32_t bsc = min(bs, 0x4000u);
 #pragma unroll
-            for (int i = 0; i < 8; i++) acc[i] = bs | (bs << 16);
+            for (int i = 0; i < 8; i++) acc[i] = bias2 + (bsc | (bsc << 16));
           }
         }
         for (uint64_t mh = hm; mh;) {
@@ -1670,11 +1678,11 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
         }
         uint32_t cm = 0;  // documents of the block over the gate
         if (hb) {
+          // biased accumulators: bit 15 of a half is set exactly when A(d) >= gate
+          uint32_t hi = 0;
 #pragma unroll
-          for (int i = 0; i < 8; i++) {
-            if ((acc[i] & 0xFFFFu) >= gate) cm |= 1u << (2 * i);
-            if ((acc[i] >> 16) >= gate) cm |= 1u << (2 * i + 1);
-          }
+          for (int i = 0; i < 8; i++) hi |= (acc[i] & 0x80008000u) >> (15 - 2 * i);
+          cm = (hi & 0x5555u) | ((hi >> 15) & 0xAAAAu);
           if (wide_nl && bw != 0u) cm = 0xFFFFu;  // (its sum may have wrapped: every document)
         }
         // candidates listed in LDS, scored one per lane
