@@ -1533,7 +1533,8 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     const bool listed = total <= kSList;  // else the block sum bounds every document of the block
     // a block holds at most 16 postings per sparse term: with more than 16 sparse
     // terms an unlisted window's block may hold > 258 postings, whose 16-bit impact
-    // sum can wrap -- such blocks pass the bounds and all their documents are scored
+    // sum can wrap -- such blocks pass the bounds (their documents' exact sums
+    // decide, below)
     const bool wide_nl = !listed && __popcll(sm) > 16;
     if (total > 0) {
       const int64_t plo = D.mb + mc;
@@ -1573,11 +1574,12 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     uint32_t ub[4] = {ub0 & 0xFFFFu, ub0 >> 16, ub1 & 0xFFFFu, ub1 >> 16};
     if (total > 0) {
       // + the block's sparse impact sum (>= the sparse sum of any of its documents)
+      int li = lane;
+      asm volatile("" : "+v"(li));  // (an address recomputed here, not a hoisted register that spills)
+      const uint4 b4 = reinterpret_cast<const uint4 *>(bsum)[li];
+      const uint32_t bws[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-      for (int m = 0; m < 4; m++) {
-        const uint32_t bw = bsum[4 * lane + m];
-        ub[m] += wide_nl ? (bw ? 0x10000u : 0u) : (bw & 0xFFFFu);
-      }
+      for (int m = 0; m < 4; m++) ub[m] += wide_nl ? (bws[m] ? 0x10000u : 0u) : (bws[m] & 0xFFFFu);
     }
     uint32_t bm = 0;
 #pragma unroll
@@ -1604,6 +1606,41 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
       // a gate past 2^15 - 1 takes no bias, and no document reaches bit 15)
       const uint32_t bias = gate > 0x7FFFu ? 0u : 0x8000u - gate;
       const uint32_t bias2 = bias | (bias << 16);
+      const bool unl = !listed && total > 0;  // (wave-uniform)
+      // slots: the first 64 passing blocks, 32 bytes each, the first 32 in slist, the rest in bent
+      uint32_t *const slot0 = slist, *const slot32 = reinterpret_cast<uint32_t *>(bent);
+      if (unl) {
+        // a window whose sparse postings are too many to list: its first 64 passing
+        // blocks take slots (bit 31 | slot over their block sums: the bounds are
+        // done), and a second pass over the postings sums each slot's documents
+        // exactly into a u16 table in the list's LDS, which this pair leaves unused
+        if (lane < nblk) bsum[blist[lane]] = 0x80000000u | (uint32_t)lane;
+        uint32_t *my = lane < 32 ? slot0 + 8 * lane : slot32 + 8 * (lane - 32);
+        *reinterpret_cast<uint4 *>(my) = make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4 *>(my + 4) = make_uint4(0, 0, 0, 0);
+        qwave_sync();
+        const int64_t plo = D.mb + mc;
+        for (int32_t e0 = 0; e0 < total; e0 += 64) {
+          const int32_t e = e0 + lane;
+          int64_t pb = 0;
+          for (uint64_t m = sm; m; m &= m - 1) {
+            const int j = (int)__builtin_ctzll(m);
+            const int32_t pj = __builtin_amdgcn_readlane(prej, j);
+            if (e >= pj) pb = rl64(plo, j) - pj;
+          }
+          if (e < total) {
+            const uint32_t pw = a.spk[pb + e];
+            const int r = (int)(pw & 0xFFFu);
+            const uint32_t sw = bsum[r >> 4];
+            if (sw >> 31) {
+              const int sl = (int)(sw & 0xFFu);
+              uint32_t *t = sl < 32 ? slot0 + 8 * sl : slot32 + 8 * (sl - 32);
+              atomicAdd(t + ((r & 15) >> 1), ((pw >> 12) & 0xFFu) << ((r & 1) << 4));  // A(d) < 2^14: no carry
+            }
+          }
+        }
+        qwave_sync();
+      }
       // one passing block per lane: exact A(d) of its 16 documents
       for (int32_t b0 = 0; b0 < nblk; b0 += 64) {
         const bool hb = b0 + lane < nblk;
@@ -1612,9 +1649,28 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
         uint32_t acc[8];          // documents r0 + 2m (low u16), + 1 (high)
 #pragma unroll
         for (int i = 0; i < 8; i++) acc[i] = bias2;
-        const uint32_t bw = (total > 0 && hb) ? bsum[blk] : 0u;
+        if (unl && hb) {
+          if (b0 == 0) {  // a slot: exact sums
+            const uint32_t *my = lane < 32 ? slot0 + 8 * lane : slot32 + 8 * (lane - 32);
+            const uint4 u0 = *reinterpret_cast<const uint4 *>(my), u1 = *reinterpret_cast<const uint4 *>(my + 4);
+            acc[0] += u0.x;
+            acc[1] += u0.y;
+            acc[2] += u0.z;
+            acc[3] += u0.w;
+            acc[4] += u1.x;
+            acc[5] += u1.y;
+            acc[6] += u1.z;
+            acc[7] += u1.w;
+          } else {  // past 64 passing blocks: the block's sum bounds each document
+            // (clamped: any sum >= 2^14 passes every gate, A(d) <= 64 x 254 < 2^14)
+            const uint32_t bsc = wide_nl ? 0x4000u : min(bsum[blk] & 0xFFFFu, 0x4000u);
+#pragma unroll
+            for (int i = 0; i < 8; i++) acc[i] += bsc | (bsc << 16);
+          }
+        }
+        const uint32_t bw = (listed && total > 0 && hb) ? bsum[blk] : 0u;
         const uint32_t bs = bw & 0xFFFFu, bn = bw >> 16;
-        if (bs != 0 && listed && bn <= 2) {  // the common case: the block's inline entries
+        if (bs != 0 && bn <= 2) {  // the common case: the block's inline entries
           for (uint32_t k2 = 0; k2 < bn; k2++) {
             const uint32_t ent = bent[2 * blk + k2];
             const int dr = (int)(ent & 15u);
@@ -1623,7 +1679,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
             for (int i = 0; i < 8; i++) acc[i] += (dr >> 1) == i ? add : 0u;
           }
         } else if (bs != 0) {  // (most passing blocks hold no sparse posting)
-          if (listed) {
+          {
             // the block's sparse postings: per sparse term, its listed entries
             // from the first with r >= r0 while r < r0 + 16
             for (uint64_t m = sm; m; m &= m - 1) {
@@ -1645,12 +1701,6 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
                 for (int i = 0; i < 8; i++) acc[i] += (dr >> 1) == i ? add : 0u;
               }
             }
-          } else {
-            // too many postings to list: the block's sum bounds each document
-            // (clamped: any sum >= 2^14 passes every gate, A(d) <= 64 x 254 < 2^14)
-            const uint32_t bsc = min(bs, 0x4000u);
-#pragma unroll
-            for (int i = 0; i < 8; i++) acc[i] = bias2 + (bsc | (bsc << 16));
           }
         }
         for (uint64_t mh = hm; mh;) {
@@ -1683,7 +1733,6 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
 #pragma unroll
           for (int i = 0; i < 8; i++) hi |= (acc[i] & 0x80008000u) >> (15 - 2 * i);
           cm = (hi & 0x5555u) | ((hi >> 15) & 0xAAAAu);
-          if (wide_nl && bw != 0u) cm = 0xFFFFu;  // (its sum may have wrapped: every document)
         }
         // candidates listed in LDS, scored one per lane
         const int32_t cl = __popc(cm);
@@ -2057,11 +2106,13 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     int32_t nh = 0;
     SME_HIP(hipMemcpyAsync(&nh, scan + V, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
-    // memory budget for the rows: 1/8 of the device's free memory, at most 16 GB
+    // memory budget for the rows: a quarter of the device's free memory, at most
+    // 64 GB (a heavy term without a row reaches the window pass as a long sparse
+    // list; the c4 shard's ~2,300 heavy terms need ~30 GB of rows)
     size_t fr = 0, tot = 0;
     SME_HIP(hipMemGetInfo(&fr, &tot));
     const double per_row = 2.0 * (double)stride + 2.0 * (double)(T << 6) + (double)T;
-    const int64_t cap = (int64_t)(std::min<double>((double)fr / 8.0, 16e9) / per_row);
+    const int64_t cap = (int64_t)(std::min<double>((double)fr / 4.0, 64e9) / per_row);
     const int64_t H = std::min<int64_t>(nh, cap);
     int32_t *hrow_of = ix->d_hrow_of.as<int32_t>(V);
     int32_t *hterm = W[38].as<int32_t>(H + 1);

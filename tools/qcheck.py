@@ -3,7 +3,7 @@ window-major scorer (default) against the streaming kernel (query_kernel=1) and
 the per-query block-max sweep (query_kernel=2), per query docnos and fp64 score
 bits.  Prints the mismatch count per alternative and the first mismatching
 queries.
-    python tools/qcheck.py [--config c2|c5] [--docs N] [--queries Q] [--k K]
+    python tools/qcheck.py [--config c2|c5|c4shard] [--docs N] [--queries Q] [--k K]
 """
 import argparse
 import hashlib
@@ -32,7 +32,8 @@ def main():
     sme = importlib.import_module(PKG)
     synth = importlib.import_module(PKG + ".synth")
     cfg = dict(c2=dict(V=1 << 20, seed=42, lo=400, hi=600, qseed=7),
-               c5=dict(V=30000, seed=9, lo=40, hi=72, qseed=9))[a.config]
+               c5=dict(V=30000, seed=9, lo=40, hi=72, qseed=9),
+               c4shard=dict(V=1 << 22, seed=44, lo=200, hi=360, qseed=7))[a.config]
     dc = sme.DeviceCorpus(a.docs, V=cfg["V"], seed=cfg["seed"], len_lo=cfg["lo"], len_hi=cfg["hi"])
     ctx = sme.Context(k=1, num_partitions=1, device=0)
     ctx.load_docno_mapping(synth.mapping_bytes(a.docs))

@@ -37,7 +37,8 @@ def main():
     sme = importlib.import_module(PKG)
     synth = importlib.import_module(PKG + ".synth")
     cfg = dict(c2=dict(V=1 << 20, seed=42, lo=400, hi=600, qseed=7),
-               c5=dict(V=30000, seed=9, lo=40, hi=72, qseed=9))[a.config]
+               c5=dict(V=30000, seed=9, lo=40, hi=72, qseed=9),
+               c4shard=dict(V=1 << 22, seed=44, lo=200, hi=360, qseed=7))[a.config]
     dc = sme.DeviceCorpus(a.docs, V=cfg["V"], seed=cfg["seed"], len_lo=cfg["lo"], len_hi=cfg["hi"])
     ctx = sme.Context(k=1, num_partitions=1, device=0, tiebreak=a.tiebreak)
     ctx.load_docno_mapping(synth.mapping_bytes(a.docs))
