@@ -130,15 +130,29 @@ __device__ __forceinline__ T wave_incl_sum(T v) {
     return v;
   }
 }
+// Inclusive wave max (every lane active); signed 32-bit values by the DPP ladder
+// of wave_incl_sum with INT32_MIN for the lanes a move does not reach.
 template <typename T>
 __device__ __forceinline__ T wave_incl_max(T v) {
-  const int l = lane_id();
+  if constexpr (sizeof(T) == 4 && T(-1) < T(0)) {
+    int x = (int)v;
+    constexpr int kLo = (int)0x80000000;
+    x = max(x, __builtin_amdgcn_update_dpp(kLo, x, 0x111, 0xF, 0xF, false));  // row_shr:1
+    x = max(x, __builtin_amdgcn_update_dpp(kLo, x, 0x112, 0xF, 0xF, false));  // row_shr:2
+    x = max(x, __builtin_amdgcn_update_dpp(kLo, x, 0x114, 0xF, 0xF, false));  // row_shr:4
+    x = max(x, __builtin_amdgcn_update_dpp(kLo, x, 0x118, 0xF, 0xF, false));  // row_shr:8
+    x = max(x, __builtin_amdgcn_update_dpp(kLo, x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    x = max(x, __builtin_amdgcn_update_dpp(kLo, x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return (T)x;
+  } else {
+    const int l = lane_id();
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    T u = __shfl_up(v, o, 64);
-    if (l >= o) v = v > u ? v : u;
+    for (int o = 1; o < 64; o <<= 1) {
+      T u = __shfl_up(v, o, 64);
+      if (l >= o) v = v > u ? v : u;
+    }
+    return v;
   }
-  return v;
 }
 
 // Block-wide exclusive sum for blockDim.x == NT (multiple of 64); scratch >= NT/64+1.
@@ -168,8 +182,13 @@ template <int NT, typename T>
 __device__ __forceinline__ T block_excl_max(T v, T lo, T *scratch, T *total) {
   const int w = threadIdx.x >> 6, l = lane_id();
   T inc = wave_incl_max(v);
-  T exc = __shfl_up(inc, 1, 64);
-  if (l == 0) exc = lo;
+  T exc;
+  if constexpr (sizeof(T) == 4) {
+    exc = (T)__builtin_amdgcn_update_dpp((int)lo, (int)inc, 0x138, 0xF, 0xF, false);  // wave_shr:1 (lane 0: lo)
+  } else {
+    exc = __shfl_up(inc, 1, 64);
+    if (l == 0) exc = lo;
+  }
   if (l == 63) scratch[w] = inc;
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -1430,6 +1430,15 @@ struct QWinArgs {
 #ifndef SME_QWIN_SPARSE_NT
 #define SME_QWIN_SPARSE_NT 0
 #endif
+// the experiment build's counters and timing switches; constants in the product
+// (so the product kernel holds no registers or branches for them)
+#ifdef SME_EXPERIMENTS
+#define QW_STATS a.stats
+#define QW_EXPER a.exper
+#else
+#define QW_STATS ((unsigned long long *)nullptr)
+#define QW_EXPER 0
+#endif
 __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) {
   // LDS: 2.8 KB per wave + the LUT = 12 KB per workgroup, so LDS does not bound
   // the occupancy (a per-document sparse accumulator, 8 KB per wave, held it at
@@ -1493,8 +1502,8 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
       if (npos + kWNT / 64 < p_hi) NNP = ld_pos_uni(a.qpos + npos + kWNT / 64);
     }
 #ifdef SME_EXPERIMENTS  // timing switches: 4 = no sparse terms, 8 = no heavy terms
-    const uint64_t hm = (a.exper & 8) ? 0ull : (uint64_t)__ballot(D.hr >= 0);
-    const uint64_t sm = (a.exper & 4) ? 0ull : (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
+    const uint64_t hm = (QW_EXPER & 8) ? 0ull : (uint64_t)__ballot(D.hr >= 0);
+    const uint64_t sm = (QW_EXPER & 4) ? 0ull : (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
 #else
     const uint64_t hm = (uint64_t)__ballot(D.hr >= 0);
     const uint64_t sm = (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
@@ -1587,13 +1596,13 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     const int32_t bl = __popc(bm);
     const int32_t bincl = wave_incl_sum(bl);
     const int32_t nblk = __builtin_amdgcn_readlane(bincl, 63);
-    if (a.stats && lane == 0) {
-      atomicAdd(a.stats + 0, 1ull);
-      atomicAdd(a.stats + 1, (unsigned long long)total);
-      atomicAdd(a.stats + 2, (unsigned long long)nblk);
-      atomicAdd(a.stats + 3, (unsigned long long)__popcll(hm));
+    if (QW_STATS && lane == 0) {
+      atomicAdd(QW_STATS + 0, 1ull);
+      atomicAdd(QW_STATS + 1, (unsigned long long)total);
+      atomicAdd(QW_STATS + 2, (unsigned long long)nblk);
+      atomicAdd(QW_STATS + 3, (unsigned long long)__popcll(hm));
     }
-    if (nblk > 0 && !(a.exper & 1)) {
+    if (nblk > 0 && !(QW_EXPER & 1)) {
       qwave_sync();
       {
         int32_t o = bincl - bl;
@@ -1737,8 +1746,8 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
         // candidates listed in LDS, scored one per lane
         const int32_t cl = __popc(cm);
         const int32_t cincl = wave_incl_sum(cl);
-        const int32_t ncand = (a.exper & 2) ? 0 : __builtin_amdgcn_readlane(cincl, 63);
-        if (a.stats && lane == 0) atomicAdd(a.stats + 4, (unsigned long long)ncand);
+        const int32_t ncand = (QW_EXPER & 2) ? 0 : __builtin_amdgcn_readlane(cincl, 63);
+        if (QW_STATS && lane == 0) atomicAdd(QW_STATS + 4, (unsigned long long)ncand);
         for (int32_t k0 = 0; k0 < ncand; k0 += kCList) {
           const int32_t kn = min(ncand - k0, kCList);
           qwave_sync();
@@ -1822,7 +1831,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
               keep = S > th0 || (S == th0 && key <= thk);  // th0 < 0 (no seed): every touched document
             }
             const uint64_t km = (uint64_t)__ballot(keep);
-            if (a.stats && lane == 0) atomicAdd(a.stats + 5, (unsigned long long)__popcll(km));
+            if (QW_STATS && lane == 0) atomicAdd(QW_STATS + 5, (unsigned long long)__popcll(km));
             if (km) {
               unsigned int base = 0;
               if (lane == 0) base = atomicAdd(&a.ccnt[P.q], (unsigned int)__popcll(km));
