@@ -67,7 +67,8 @@ struct CpuIndex {
 
 // readUntilMatch over one split (the oracle's record reader, exported)
 std::vector<std::pair<uint64_t, uint64_t>> records(const uint8_t *b, size_t n) {
-  int cap = 1024;
+  // one pass when the records average >= 256 bytes (a second, exact-size pass otherwise)
+  int cap = (int)std::min<size_t>(n / 256 + 1024, (size_t)1 << 30);
   for (;;) {
     std::vector<uint64_t> off((size_t)cap), len((size_t)cap);
     int r = or_split_records(b, n, off.data(), len.data(), cap);
@@ -292,6 +293,7 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   }
   const auto recs = records(corpus, n);
   const int64_t nR = (int64_t)recs.size();
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "records", omp_get_wtime() - t0);
   // Three phases, no locks; every DISTINCT raw token is normalized, stop-filtered
   // and stemmed once (T13):
   //  1. per record (threads): docno; raw tokens by the byte-level TagTokenizer
