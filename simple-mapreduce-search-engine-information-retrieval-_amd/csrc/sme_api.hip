@@ -255,6 +255,9 @@ int sme_create(const sme_config *cfg, sme_ctx **out) {
     try {
       set_device(cx);
       SME_HIP(hipStreamCreateWithFlags(&cx->own_stream, hipStreamNonBlocking));
+      SME_HIP(hipStreamCreateWithFlags(&cx->aux_stream, hipStreamNonBlocking));
+      SME_HIP(hipEventCreateWithFlags(&cx->ev_fork, hipEventDisableTiming));
+      SME_HIP(hipEventCreateWithFlags(&cx->ev_join, hipEventDisableTiming));
     } catch (...) {
       delete cx;
       throw;
@@ -325,6 +328,9 @@ static void ctx_release(sme_ctx *cx) {
   (void)hipSetDevice(cx->device);
   (void)hipDeviceSynchronize();
   if (cx->own_stream) (void)hipStreamDestroy(cx->own_stream);
+  if (cx->aux_stream) (void)hipStreamDestroy(cx->aux_stream);
+  if (cx->ev_fork) (void)hipEventDestroy(cx->ev_fork);
+  if (cx->ev_join) (void)hipEventDestroy(cx->ev_join);
   for (auto &b : cx->h_stage)
     if (b) (void)hipHostFree(b);
   delete cx;

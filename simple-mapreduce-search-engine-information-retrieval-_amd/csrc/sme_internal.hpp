@@ -14,6 +14,10 @@ struct sme_ctx {
   sme_config cfg{};
   int device = 0;
   hipStream_t own_stream = nullptr;
+  // a second stream for independent kernels of one build stage (the tf-desc
+  // sort's segment classes), joined back by events
+  hipStream_t aux_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // docno mapping: {"", docids...} as UTF-16 (TrecDocnoMapping.readDocnoData)
   sme::DevBuf map_chars, map_off;
   int64_t map_n = 0;  // entries including the "" sentinel
