@@ -94,6 +94,8 @@ void sme_destroy(sme_ctx *ctx);
  *   "cand_cap"      candidate list per query of the window path, 1..2048 (default 1024; >= 1024:
  *                   at least 16 k)
  *   "win_sample"    1 (default): sample windows first, thresholds raised, then the rest
+ *   "win_stage_min" windows of the first sampled stage, at least (default 16; the stage
+ *                   count follows, at most 9)
  *   "win_slice"     queries per window-path workgroup slice (default 256)
  *   "seed_tiles"    k_query_bm: best-bound tiles scored before the sweep, 0..8 (default 4)
  *   "query_order"   1 heaviest-term query order (default), 0 batch order
@@ -112,7 +114,7 @@ void sme_destroy(sme_ctx *ctx);
  *                   corpus for the next build (no hipMalloc) only up to this
  *                   many bytes (default 16 GiB); larger copies are freed after
  *                   the build, since HBM held there also shrinks the heavy-row
- *                   budget of sme_index_prepare_queries (1/8 of free HBM)
+ *                   budget of sme_index_prepare_queries (1/4 of free HBM)
  * Unknown names and out-of-range values are SME_EINVAL. */
 int sme_set_option(sme_ctx *ctx, const char *name, int64_t value);
 
@@ -234,7 +236,10 @@ int sme_query_topk_tie(sme_index *ix, const int32_t *term_ids, const int64_t *q_
 
 /* Query-side structures of an index (the role the reference's forward index,
  * BuildIntDocVectorsForwardIndex.java:84-158, plays for rank()): heavy-term tf
- * rows and block maxima for the block-max scorer.  Built once per index; the
+ * and impact rows with their block maxima (at most a quarter of the free HBM,
+ * 64 GB), and one 4-byte window-pass word per posting of the other terms (if 4 B
+ * per posting fits a quarter of the free HBM; else the window-major scorer is
+ * not used and batches take the block-max path).  Built once per index; the
  * impact rows and their scale depend on idf, so sme_index_reweight DROPS them:
  * call this after the last reweight (sme_query_topk* rebuilds them on first
  * use otherwise, inside that call).  *ms (may be NULL) gets the device time. */
