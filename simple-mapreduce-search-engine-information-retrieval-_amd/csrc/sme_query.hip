@@ -1100,6 +1100,7 @@ constexpr int kSeedSlots = 1024;     // seed documents per query (LDS hash)
 constexpr int kCandMax = 2048;       // largest candidate list per query (final kernel LDS)
 constexpr int kWinRounds = 3;        // window passes before an overflowing query goes to k_query_bm
 constexpr int kCList = 128;          // documents over the gate listed per round of exact scoring
+constexpr int kRaiseSmall = 512;     // k_query_raise / k_query_final: lists sorted by the small-LDS instance
 constexpr int kWinLut = 128;         // k_query_win: 1 + ln(tf) for tf < 128 from LDS
 static_assert(kWDL == 64, "one lane owns 64 documents: four uint4 impact loads per heavy term");
 
@@ -1879,6 +1880,9 @@ struct QFinalArgs {
   uint64_t *th_k;
   int32_t *ovf;               // queries whose list overflowed
   unsigned int *novf;
+  const unsigned int *nlist;  // qlist's length on the device (nullptr: n)
+  int32_t *defer;             // lists longer than this instance's LDS sort -> a bigger one (nullptr: none)
+  unsigned int *ndefer;
 };
 
 // Per query: sort the candidates (score desc, key asc) and emit the best k.  A
@@ -1892,7 +1896,8 @@ __global__ __launch_bounds__(64) void k_query_final(QFinalArgs a) {
   __shared__ double bs[CM];
   __shared__ uint64_t bk[CM];
   const int lane = threadIdx.x;
-  for (int i = blockIdx.x; i < a.n; i += gridDim.x) {
+  const int nitems = a.nlist ? (int)*a.nlist : a.n;
+  for (int i = blockIdx.x; i < nitems; i += gridDim.x) {
     const int q = a.qlist ? a.qlist[i] : i;
     const unsigned int c = a.ccnt[q];
     const bool over = c > (unsigned int)a.cap || a.oflag[q] != 0u;
@@ -1903,6 +1908,10 @@ __global__ __launch_bounds__(64) void k_query_final(QFinalArgs a) {
     const int n = min((int)c, a.cap);
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
+    if (n2 > CM) {  // (a.defer is set whenever a list can outgrow CM)
+      if (lane == 0) a.defer[atomicAdd(a.ndefer, 1u)] = q;
+      continue;
+    }
     for (int j = lane; j < n2; j += 64) {
       bs[j] = j < n ? a.cs[(int64_t)q * a.cap + j] : -INFINITY;
       bk[j] = j < n ? a.ck[(int64_t)q * a.cap + j] : kNoKey;
@@ -1932,19 +1941,29 @@ __global__ __launch_bounds__(64) void k_query_final(QFinalArgs a) {
 // stored entries still bound the threshold, it is compacted like the others
 // and flagged, so the final pass sends the query to another round (with the
 // threshold the later stages raised further).
+// Two instances: a small-LDS one over every query (many workgroups per CU) that
+// hands lists longer than its CM to `defer`, and a large-LDS one over that list.
 template <int CM>
 __global__ __launch_bounds__(64) void k_query_raise(int nq, int k, int cap, unsigned int *ccnt, unsigned int *oflag,
-                                                    double *cs, uint64_t *ck, double *th_s, uint64_t *th_k) {
+                                                    double *cs, uint64_t *ck, double *th_s, uint64_t *th_k,
+                                                    const int32_t *qlist, const unsigned int *nlist, int32_t *defer,
+                                                    unsigned int *ndefer) {
   __shared__ double bs[CM];
   __shared__ uint64_t bk[CM];
   const int lane = threadIdx.x;
-  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+  const int nitems = qlist ? (int)*nlist : nq;
+  for (int i = blockIdx.x; i < nitems; i += gridDim.x) {
+    const int q = qlist ? qlist[i] : i;
     const unsigned int c = ccnt[q];
     const bool over = c > (unsigned int)cap;
     const int n = over ? cap : (int)c;
     if (n < k) continue;  // too few to bound (cap >= k here)
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
+    if (n2 > CM) {  // (defer is set whenever a list can outgrow CM)
+      if (lane == 0) defer[atomicAdd(ndefer, 1u)] = q;
+      continue;
+    }
     for (int j = lane; j < n2; j += 64) {
       bs[j] = j < n ? cs[(int64_t)q * cap + j] : -INFINITY;
       bk[j] = j < n ? ck[(int64_t)q * cap + j] : kNoKey;
@@ -2503,10 +2522,13 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     // exact ties at the k-th score), at most kCandMax
     const int cap = (int)std::min<int64_t>(std::max<int64_t>(cx->opt_cand_cap, cx->opt_cand_cap >= 1024 ? 16 * (int64_t)k : 0),
                                            kCandMax);
-    unsigned int *ccnt = W[42].as<unsigned int>(2 * (size_t)nq + 1);
+    unsigned int *ccnt = W[42].as<unsigned int>(2 * (size_t)nq + 4);
+    unsigned int *ndefer = ccnt + 2 * (size_t)nq + 2;  // count of `defer`
     double *cs = W[43].as<double>((size_t)nq * cap);
     uint64_t *ckk = W[61].as<uint64_t>((size_t)nq * cap);
-    int32_t *ovf = W[62].as<int32_t>(2 * (size_t)nq + 2);
+    int32_t *ovf = W[62].as<int32_t>(3 * (size_t)nq + 4);
+    int32_t *defer = ovf + 2 * (size_t)nq + 2;  // long lists of a raise / final pass
+
     unsigned int *novf = ccnt + nq, *oflag = ccnt + nq + 1;
     SME_HIP(hipMemsetAsync(ccnt, 0, (2 * (size_t)nq + 1) * sizeof(unsigned int), st));
     QWinArgs wa;
@@ -2600,12 +2622,18 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       if (round == 0 && cx->opt_win_sample && nwin >= 16) {
         for (int sg = 0; sg <= L; sg++) {
           if (sg > 0) {  // raise thresholds, keep each list's best k
+            // lists of <= kRaiseSmall entries in a small-LDS pass (many workgroups per
+            // CU), the longer ones deferred to the large-LDS instance
+            SME_HIP(hipMemsetAsync(ndefer, 0, sizeof(unsigned int), st));
+            const dim3 rg((unsigned)std::min(nq, 1 << 16));
+            hipLaunchKernelGGL(k_query_raise<kRaiseSmall>, rg, dim3(64), 0, st, nq, k, cap, ccnt, oflag, cs, ckk, th0,
+                               thk, nullptr, nullptr, defer, ndefer);
             if (cap <= 1024)
-              hipLaunchKernelGGL(k_query_raise<1024>, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, nq, k,
-                                 cap, ccnt, oflag, cs, ckk, th0, thk);
+              hipLaunchKernelGGL(k_query_raise<1024>, rg, dim3(64), 0, st, nq, k, cap, ccnt, oflag, cs, ckk, th0, thk,
+                                 defer, ndefer, nullptr, nullptr);
             else
-              hipLaunchKernelGGL(k_query_raise<kCandMax>, dim3((unsigned)std::min(nq, 1 << 16)), dim3(64), 0, st, nq,
-                                 k, cap, ccnt, oflag, cs, ckk, th0, thk);
+              hipLaunchKernelGGL(k_query_raise<kCandMax>, rg, dim3(64), 0, st, nq, k, cap, ccnt, oflag, cs, ckk, th0,
+                                 thk, defer, ndefer, nullptr, nullptr);
             SME_CHECK_LAUNCH();
           }
           launch_win(wl + stage_start[sg], stage_start[sg + 1] - stage_start[sg]);
@@ -2620,10 +2648,23 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       fa.qlist = round_list;
       fa.n = n_round;
       fa.ovf = out_list;
-      if (cap <= 1024)
-        hipLaunchKernelGGL(k_query_final<1024>, dim3((unsigned)std::min(n_round, 1 << 16)), dim3(64), 0, st, fa);
-      else
-        hipLaunchKernelGGL(k_query_final<kCandMax>, dim3((unsigned)std::min(n_round, 1 << 16)), dim3(64), 0, st, fa);
+      {
+        SME_HIP(hipMemsetAsync(ndefer, 0, sizeof(unsigned int), st));
+        QFinalArgs fb = fa;  // the deferred long lists
+        fa.nlist = nullptr;
+        fa.defer = defer;
+        fa.ndefer = ndefer;
+        fb.qlist = defer;
+        fb.nlist = ndefer;
+        fb.defer = nullptr;
+        fb.ndefer = nullptr;
+        const dim3 fg((unsigned)std::min(n_round, 1 << 16));
+        hipLaunchKernelGGL(k_query_final<kRaiseSmall>, fg, dim3(64), 0, st, fa);
+        if (cap <= 1024)
+          hipLaunchKernelGGL(k_query_final<1024>, fg, dim3(64), 0, st, fb);
+        else
+          hipLaunchKernelGGL(k_query_final<kCandMax>, fg, dim3(64), 0, st, fb);
+      }
       SME_CHECK_LAUNCH();
       unsigned int h_novf = 0;
       SME_HIP(hipMemcpyAsync(&h_novf, novf, sizeof h_novf, hipMemcpyDeviceToHost, st));
