@@ -331,6 +331,7 @@ static void ctx_release(sme_ctx *cx) {
   if (cx->aux_stream) (void)hipStreamDestroy(cx->aux_stream);
   if (cx->ev_fork) (void)hipEventDestroy(cx->ev_fork);
   if (cx->ev_join) (void)hipEventDestroy(cx->ev_join);
+  for (hipEvent_t e : cx->prof_events) (void)hipEventDestroy(e);
   for (auto &b : cx->h_stage)
     if (b) (void)hipHostFree(b);
   delete cx;

@@ -3021,7 +3021,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   // never calls getDocid, and records stay in file order = the map task's order)
   if (job == 0 && !cx->has_map) throw Error(SME_ENOMAP, "no docno mapping loaded (sme_load_docno_mapping)");
   DevBuf *W = cx->ws + kBuildWs;
-  Prof prof(st);
+  Prof prof(st, &cx->prof_events);
   auto cub_tmp = [&](size_t bytes) { return cx->cub_tmp.get(bytes); };
   unsigned long long *cnt = W[W_CNT].as<unsigned long long>(32);  // [20] max tf, [22..23] docno range
 

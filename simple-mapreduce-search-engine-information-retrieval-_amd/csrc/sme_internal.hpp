@@ -18,6 +18,7 @@ struct sme_ctx {
   // sort's segment classes), joined back by events
   hipStream_t aux_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  std::vector<hipEvent_t> prof_events;  // Prof's reusable stage events
   // docno mapping: {"", docids...} as UTF-16 (TrecDocnoMapping.readDocnoData)
   sme::DevBuf map_chars, map_off;
   int64_t map_n = 0;  // entries including the "" sentinel
@@ -145,14 +146,26 @@ struct sme_index {
 namespace sme {
 // per-stage device-event timer of a build
 struct Prof {
+  // stage events come from a pool kept by the context (hipEventCreate per mark
+  // cost host time between a build's launches); events of an abandoned Prof
+  // (an exception) go back to the pool in the destructor
   hipStream_t st;
+  std::vector<hipEvent_t> *pool;
   std::vector<std::pair<std::string, hipEvent_t>> ev;
-  explicit Prof(hipStream_t s) : st(s) { mark("start"); }
+  Prof(hipStream_t s, std::vector<hipEvent_t> *p) : st(s), pool(p) { mark("start"); }
+  ~Prof() {
+    for (auto &e : ev) pool->push_back(e.second);
+  }
   void mark(const char *name) {
     hipEvent_t e;
-    SME_HIP(hipEventCreate(&e));
-    SME_HIP(hipEventRecord(e, st));
+    if (!pool->empty()) {
+      e = pool->back();
+      pool->pop_back();
+    } else {
+      SME_HIP(hipEventCreate(&e));
+    }
     ev.emplace_back(name, e);
+    SME_HIP(hipEventRecord(e, st));
   }
   std::vector<std::pair<std::string, float>> finish() {
     SME_HIP(hipEventSynchronize(ev.back().second));
@@ -165,7 +178,7 @@ struct Prof {
     float tot = 0;
     SME_HIP(hipEventElapsedTime(&tot, ev.front().second, ev.back().second));
     out.emplace_back("total", tot);
-    for (auto &p : ev) (void)hipEventDestroy(p.second);
+    for (auto &p : ev) pool->push_back(p.second);
     ev.clear();
     return out;
   }
