@@ -1277,7 +1277,10 @@ struct QSeedArgs {
 
 __global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
   __shared__ int32_t hk[kSeedSlots];             // docno (INT32_MIN empty: never a docno)
-  __shared__ unsigned long long hs[kSeedSlots];  // best S' bits (non-negative doubles order as u64)
+  // best S' per seed as float bits rounded DOWN (non-negative floats order as u32):
+  // th0 only has to bound the k-th best score from below, and 4-byte entries leave
+  // the wave 8 KB of LDS (twice the workgroups per CU of 8-byte ones)
+  __shared__ unsigned int hs[kSeedSlots];
   __shared__ int s_n;
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < a.nq; q += gridDim.x) {
@@ -1288,7 +1291,7 @@ __global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
     const uint64_t hm = (uint64_t)__ballot(D.hr >= 0);
     for (int i = lane; i < kSeedSlots; i += 64) {
       hk[i] = INT32_MIN;
-      hs[i] = 0ull;
+      hs[i] = 0u;
     }
     if (lane == 0) s_n = 0;
     __syncthreads();
@@ -1318,7 +1321,7 @@ __global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
           if (old == INT32_MIN || old == d) break;
           h = (h + 1) & (kSeedSlots - 1);
         }
-        atomicMax(&hs[h], (unsigned long long)__double_as_longlong(S));
+        atomicMax(&hs[h], (unsigned int)__float_as_uint(__double2float_rd(S)));
       }
     }
     __syncthreads();
@@ -1328,7 +1331,7 @@ __global__ __launch_bounds__(64) void k_query_seed(QSeedArgs a) {
 #pragma unroll
     for (int u = 0; u < kSeedSlots / 64; u++) {
       const int i = u * 64 + lane;
-      v[u] = hk[i] != INT32_MIN ? __longlong_as_double((long long)hs[i]) : -1.0;
+      v[u] = hk[i] != INT32_MIN ? (double)__uint_as_float(hs[i]) : -1.0;
     }
     __syncthreads();
     double th = -1.0;
