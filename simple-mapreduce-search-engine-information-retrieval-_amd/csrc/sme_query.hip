@@ -1100,7 +1100,10 @@ constexpr int kSeedSlots = 1024;     // seed documents per query (LDS hash)
 constexpr int kCandMax = 2048;       // largest candidate list per query (final kernel LDS)
 constexpr int kWinRounds = 3;        // window passes before an overflowing query goes to k_query_bm
 constexpr int kCList = 128;          // documents over the gate listed per round of exact scoring
-constexpr int kRaiseSmall = 512;     // k_query_raise / k_query_final: lists sorted by the small-LDS instance
+#ifndef SME_QRAISE_SMALL
+#define SME_QRAISE_SMALL 512
+#endif
+constexpr int kRaiseSmall = SME_QRAISE_SMALL;  // k_query_raise / k_query_final: lists sorted by the small-LDS instance
 constexpr int kWinLut = 128;         // k_query_win: 1 + ln(tf) for tf < 128 from LDS
 static_assert(kWDL == 64, "one lane owns 64 documents: four uint4 impact loads per heavy term");
 
