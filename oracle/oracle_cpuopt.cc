@@ -65,20 +65,109 @@ struct CpuIndex {
   double build_s = 0;
 };
 
-// readUntilMatch over one split (the oracle's record reader, exported)
-std::vector<std::pair<uint64_t, uint64_t>> records(const uint8_t *b, size_t n) {
-  // one pass when the records average >= 256 bytes (a second, exact-size pass otherwise)
-  int cap = (int)std::min<size_t>(n / 256 + 1024, (size_t)1 << 30);
-  for (;;) {
-    std::vector<uint64_t> off((size_t)cap), len((size_t)cap);
-    int r = or_split_records(b, n, off.data(), len.data(), cap);
-    if (r <= cap) {
-      std::vector<std::pair<uint64_t, uint64_t>> out((size_t)r);
-      for (int i = 0; i < r; i++) out[(size_t)i] = {off[(size_t)i], len[(size_t)i]};
-      return out;
-    }
-    cap = r;
+// readUntilMatch over one split (XMLRecordReader, XMLInputFormat.java:173-198),
+// in parallel.  Its matcher is naive: on a mismatch the match index resets to 0
+// WITHOUT re-testing the byte ("<<DOC>" holds no start tag), so its state at any
+// byte depends on the bytes since the last state-0 point.  A byte outside the
+// tags' alphabet {< / D O C >} resets both matchers (start "<DOC>", end
+// "</DOC>"), so chunks cut just after such a byte start from state 0; every
+// thread records where each matcher, run from its chunk start, completes a tag
+// (both tags leave the other matcher at state 0 too, so at every mode switch the
+// whole-file reader and these independent scans agree), and one serial pass
+// alternates start / end detections exactly as the reader does.  Bytes between
+// '<'s are skipped by memchr: a state > 0 needs a '<' since the last reset.
+// (or_cpuopt_split_records exports it; the tests hold it to or_split_records.)
+struct TagHits {
+  std::vector<uint64_t> st, en;  // start-tag first bytes; end-tag byte after '>'
+};
+static inline bool tag_byte(uint8_t c) {
+  return c == '<' || c == '/' || c == 'D' || c == 'O' || c == 'C' || c == '>';
+}
+static void scan_tags(const uint8_t *b, size_t n, size_t a, size_t e, TagHits *h) {
+  static const char S[] = "<DOC>", E[] = "</DOC>";
+  size_t p = a;
+  while (p < n) {
+    const uint8_t *q = (const uint8_t *)memchr(b + p, '<', n - p);
+    if (!q) break;
+    p = (size_t)(q - b);
+    if (p >= e) break;  // a tag starting at or past e belongs to the next chunk
+    // both matchers from state 0 at this '<' until both are back at 0
+    int is = 0, ie = 0;
+    size_t x = p;
+    do {
+      const uint8_t c = b[x];
+      if (c == (uint8_t)S[is]) {
+        if (++is == 5) {
+          h->st.push_back(x + 1 - 5);
+          is = 0;
+        }
+      } else {
+        is = 0;
+      }
+      if (c == (uint8_t)E[ie]) {
+        if (++ie == 6) {
+          h->en.push_back(x + 1);
+          ie = 0;
+        }
+      } else {
+        ie = 0;
+      }
+      x++;
+    } while (x < n && (is | ie));
+    p = x;
   }
+}
+std::vector<std::pair<uint64_t, uint64_t>> records(const uint8_t *b, size_t n) {
+  const int T = std::max(1, std::min(omp_get_max_threads(), (int)(n >> 20) + 1));
+  std::vector<size_t> cut((size_t)T + 1, n);
+  cut[0] = 0;
+  for (int t = 1; t < T; t++) {
+    size_t c = n / (size_t)T * (size_t)t;
+    while (c < n && (c == 0 || tag_byte(b[c - 1]))) c++;  // just after a byte that resets both matchers
+    cut[(size_t)t] = std::max(c, cut[(size_t)t - 1]);
+  }
+  std::vector<TagHits> hits((size_t)T);
+#pragma omp parallel for schedule(static, 1)
+  for (int t = 0; t < T; t++) scan_tags(b, n, cut[(size_t)t], cut[(size_t)t + 1], &hits[(size_t)t]);
+  // the reader: a start tag, then the first end tag completed after it, ...
+  std::vector<std::pair<uint64_t, uint64_t>> out;
+  size_t ti = 0, si = 0, tj = 0, ej = 0;
+  uint64_t pos = 0;
+  for (;;) {
+    // first start tag beginning at or after pos
+    uint64_t rs = UINT64_MAX;
+    while (ti < (size_t)T) {
+      if (si < hits[ti].st.size()) {
+        if (hits[ti].st[si] >= pos) {
+          rs = hits[ti].st[si];
+          break;
+        }
+        si++;
+      } else {
+        ti++;
+        si = 0;
+      }
+    }
+    if (rs == UINT64_MAX) break;
+    // first end tag whose first byte follows the start tag
+    uint64_t re = UINT64_MAX;
+    while (tj < (size_t)T) {
+      if (ej < hits[tj].en.size()) {
+        if (hits[tj].en[ej] - 6 >= rs + 5) {
+          re = hits[tj].en[ej];
+          break;
+        }
+        ej++;
+      } else {
+        tj++;
+        ej = 0;
+      }
+    }
+    if (re == UINT64_MAX) break;  // unterminated: the reader drops it
+    out.emplace_back(rs, re - rs);
+    pos = re;
+  }
+  return out;
 }
 
 int jcmp(const u16s &a, const u16s &b) {
@@ -252,6 +341,16 @@ struct RawTab {
 }  // namespace
 
 extern "C" {
+
+/* The parallel record split (tests: equal to or_split_records). */
+int or_cpuopt_split_records(const uint8_t *b, size_t n, uint64_t *off, uint64_t *len, int cap) {
+  const auto r = records(b, n);
+  for (size_t i = 0; i < r.size() && i < (size_t)cap; i++) {
+    off[i] = r[i].first;
+    len[i] = r[i].second;
+  }
+  return (int)r.size();
+}
 
 /* Build from a host corpus; mapping = TrecDocnoMapping file bytes.  threads <= 0:
  * omp default.  Returns NULL on a record the reference rejects (no </DOCNO>). */

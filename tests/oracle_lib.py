@@ -45,6 +45,7 @@ def lib():
         L.or_count_distinct_terms.restype = C.c_int64
         L.or_count_distinct_terms.argtypes = [C.c_char_p, C.c_void_p, C.c_int64]
         L.or_split_records.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]
+        L.or_cpuopt_split_records.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]
         L.or_chargram.restype = C.c_void_p
         L.or_chargram.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int]
         L.or_chargram_ngrams.argtypes = [C.c_void_p]
@@ -118,11 +119,14 @@ def is_stopword(word):
     return bool(lib().or_is_stopword_utf8(b, len(b)))
 
 
-def split_records(corpus):
+def split_records(corpus, cpuopt=False):
+    """XMLRecordReader's records: the oracle's serial reader, or (cpuopt) the cpu-opt
+    baseline's parallel split that must equal it."""
     cap = corpus.count(b"<DOC>") + 1
     off = (C.c_uint64 * cap)()
     ln = (C.c_uint64 * cap)()
-    n = lib().or_split_records(corpus, len(corpus), off, ln, cap)
+    f = lib().or_cpuopt_split_records if cpuopt else lib().or_split_records
+    n = f(corpus, len(corpus), off, ln, cap)
     return [(off[i], ln[i]) for i in range(n)]
 
 

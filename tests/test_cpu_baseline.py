@@ -70,3 +70,23 @@ def test_cpuopt_from_csr_matches_built_index():
     d1, s1, _ = built.query(tq, qo, 10, 0, 2)
     d2, s2, _ = wrapped.query(tq, qo, 10, 0, 2)
     assert np.array_equal(d1, d2) and np.array_equal(s1, s2)
+
+
+def test_cpuopt_parallel_record_split():
+    """cpu-opt's parallel record split (chunks cut after bytes outside the tags'
+    alphabet, memchr between '<'s, one serial pass over the tag hits) equals the
+    oracle's serial XMLRecordReader: naive-matcher quirks ("<<DOC>" holds no start
+    tag, "<<<DOC>" does), "<D<DOC>", nested and unterminated records, tags at
+    chunk cuts of a corpus split over many threads."""
+    import random
+    rng = random.Random(5)
+    parts = [b"<DOC>", b"</DOC>", b"<<DOC>", b"<<<DOC>", b"<D<DOC>", b"</D</DOC>", b"<DOC", b"</DO", b"<", b"/",
+             b"D", b"O", b"C", b">", b"x", b" ", b"<DOCNO>a</DOCNO>", b"text words ", b"<<", b"</DOC></DOC>"]
+    cases = [b"", b"<DOC>", b"<DOC></DOC>", b"<<DOC></DOC>", b"<<<DOC>a</DOC>", b"<D<DOC>a</DOC>", b"<DOC>a</D</DOC>",
+             b"<DOC><DOC>a</DOC></DOC>", b"<DOC>a</DOC><DOC>b"]
+    for _ in range(300):
+        cases.append(b"".join(rng.choice(parts) for _ in range(rng.randint(1, 60))))
+    for _ in range(20):  # big enough for many chunks (1 MiB each)
+        cases.append(b"".join(rng.choice(parts) * rng.randint(1, 3) for _ in range(rng.randint(200000, 400000))))
+    for c in cases:
+        assert O.split_records(c, cpuopt=True) == O.split_records(c), c[:80]
