@@ -600,9 +600,10 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   struct TK {
     uint64_t k0, k1;
     const u16s *s;
+    int32_t slot;  // the output's place in gterm (-1: a complex record's term)
   };
   auto tkey = [](const u16s *w) {
-    TK t{0, 0, w};
+    TK t{0, 0, w, -1};
     for (size_t i = 0; i < 8; i++) {
       const uint64_t u = i < w->size() ? (uint64_t)(uint16_t)(*w)[i] : 0ull;
       if (i < 4) t.k0 = (t.k0 << 16) | u;
@@ -619,34 +620,49 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   auto teq = [](const TK &x, const TK &y) {
     return x.k0 == y.k0 && x.k1 == y.k1 && (x.s->size() <= 8 && y.s->size() <= 8 ? x.s->size() == y.s->size() : *x.s == *y.s);
   };
-  std::vector<TK> keyed;
-  for (auto &v : gout)
-    for (auto &w : v) keyed.push_back(tkey(&w));
-  for (auto &v : rterm)
-    for (auto &w : v) keyed.push_back(tkey(&w));
-  __gnu_parallel::sort(keyed.begin(), keyed.end(), tless);
-  std::vector<u16s> vocab;
-  std::vector<TK> vk;
-  for (size_t i = 0; i < keyed.size(); i++)
-    if (i == 0 || !teq(keyed[i], keyed[i - 1])) {
-      vocab.push_back(*keyed[i].s);
-      vk.push_back(keyed[i]);
+  // every distinct raw token's outputs keyed in parallel (slot = its place in
+  // gterm), the complex records' terms after them; after the sort each output's
+  // term id is its run's rank (no search per output)
+  std::vector<int32_t> go0((size_t)G + 1, 0);
+  for (int64_t g = 0; g < G; g++) go0[(size_t)g + 1] = go0[(size_t)g] + (int32_t)gout[(size_t)g].size();
+  const size_t nout = (size_t)go0[(size_t)G];
+  size_t nrt = 0;
+  for (auto &v : rterm) nrt += v.size();
+  std::vector<TK> keyed(nout + nrt);
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (int64_t g = 0; g < G; g++)
+    for (size_t k = 0; k < gout[(size_t)g].size(); k++) {
+      TK t = tkey(&gout[(size_t)g][k]);
+      t.slot = go0[(size_t)g] + (int32_t)k;
+      keyed[(size_t)t.slot] = t;
     }
+  {
+    size_t i = nout;
+    for (auto &v : rterm)
+      for (auto &w : v) keyed[i++] = tkey(&w);
+  }
+  __gnu_parallel::sort(keyed.begin(), keyed.end(), tless);
+  std::vector<int32_t> gterm(nout);
+  std::vector<size_t> first;  // first sorted entry of each distinct term
+  for (size_t i = 0; i < keyed.size(); i++) {
+    if (i == 0 || !teq(keyed[i], keyed[i - 1])) first.push_back(i);
+    if (keyed[i].slot >= 0) gterm[(size_t)keyed[i].slot] = (int32_t)(first.size() - 1);
+  }
+  const int64_t V = (int64_t)first.size();
+  std::vector<u16s> vocab((size_t)V);
+  std::vector<TK> vk((size_t)V);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < V; i++) {
+    vocab[(size_t)i] = *keyed[first[(size_t)i]].s;
+    vk[(size_t)i] = keyed[first[(size_t)i]];
+  }
   keyed.clear();
   keyed.shrink_to_fit();
-  const int64_t V = (int64_t)vocab.size();
   for (int64_t i = 0; i < V; i++) vk[(size_t)i].s = &vocab[(size_t)i];
-  auto term_of = [&](const u16s &w) {
+  auto term_of = [&](const u16s &w) {  // (complex records' terms)
     const TK k = tkey(&w);
     return (int32_t)(std::lower_bound(vk.begin(), vk.end(), k, tless) - vk.begin());
   };
-  // term ids of every distinct raw token's outputs
-  std::vector<int32_t> go0((size_t)G + 1, 0);
-  for (int64_t g = 0; g < G; g++) go0[(size_t)g + 1] = go0[(size_t)g] + (int32_t)gout[(size_t)g].size();
-  std::vector<int32_t> gterm((size_t)go0[(size_t)G]);
-#pragma omp parallel for schedule(dynamic, 1024)
-  for (int64_t g = 0; g < G; g++)
-    for (size_t k = 0; k < gout[(size_t)g].size(); k++) gterm[(size_t)go0[(size_t)g] + k] = term_of(gout[(size_t)g][k]);
   // per thread: local raw id -> its single term id (>= 0), no term (-1) or the
   // first of several at gterm[-v - 2] (one random access per token below)
   std::vector<std::vector<int32_t>> ltm((size_t)nthr);
