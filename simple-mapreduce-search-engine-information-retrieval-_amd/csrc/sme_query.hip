@@ -2353,8 +2353,9 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       }
       {  // (a single query's tables are always built: <= 64 rows)
         row_of = rowo;
-        uint8_t *ql = W[44].as<uint8_t>(std::max<int64_t>(nrows, 1) * 256);
-        qlut = ql;
+        // impact scale: the index's (prepare_queries), shared by every batch
+        SME_HIP(hipMemcpyAsync(wmax, &ix->q_wmax_bits, sizeof(uint64_t), hipMemcpyHostToDevice, st));
+        if (!winp) qlut = W[44].as<uint8_t>(std::max<int64_t>(nrows, 1) * 256);
         if (nrows > 0) {
           int32_t *tor = W[57].as<int32_t>(nrows + 1);
           int64_t *rdf = W[58].as<int64_t>(nrows + 1), *rpre = W[59].as<int64_t>(nrows + 1);
@@ -2362,9 +2363,14 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           hipLaunchKernelGGL(k_term_rows, dim3(gV), dim3(256), 0, st, mark, rowo, V, off, tor, rdf);
           SME_HIP(hipMemsetAsync(rdf + nrows, 0, sizeof(int64_t), st));
           excl_scan(rdf, rpre, (int64_t)(nrows + 1), cx->ws[23], st);
-          // tile skip table (k_query_bm); the window path builds its window
-          // table directly and the tile table only if a query falls back
-          build_sk = [=, &W, &sk]() {
+          // tile skip table and impact tables (k_query_bm); the window path
+          // builds its window table directly (its postings carry their impacts)
+          // and these only if a query falls back
+          build_sk = [=, &W, &sk, &qlut]() {
+            uint8_t *ql = W[44].as<uint8_t>(nrows * 256);
+            qlut = ql;
+            hipLaunchKernelGGL(k_row_qlut, dim3((unsigned)std::min<int64_t>(nrows, 16384)), dim3(256), 0, st, tor,
+                               nrows, lut, ix->max_tf, idf, (const unsigned long long *)wmax, ql);
             int32_t *skw = W[60].as<int32_t>(std::max<int64_t>(nrows, 1) * (T + 1));  // allocated on first use
             sk = skw;
             SME_HIP(hipMemsetAsync(skw, 0x7F, (size_t)nrows * (T + 1) * sizeof(int32_t), st));
@@ -2397,10 +2403,6 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
           } else {
             build_sk();
           }
-          // impact scale: the index's (prepare_queries), shared by every batch
-          SME_HIP(hipMemcpyAsync(wmax, &ix->q_wmax_bits, sizeof(uint64_t), hipMemcpyHostToDevice, st));
-          hipLaunchKernelGGL(k_row_qlut, dim3((unsigned)std::min<int64_t>(nrows, 16384)), dim3(256), 0, st, tor, nrows,
-                             lut, ix->max_tf, idf, (const unsigned long long *)wmax, ql);
           SME_CHECK_LAUNCH();
         }
         if (!sk && !winp) {  // no valid term in the batch: an empty (all 'none') table row for k_query_bm
@@ -2689,6 +2691,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
         if (build_sk) build_sk();
         QBmArgs ob = qa;
         ob.sk = sk;
+        ob.qlut = qlut;
         ob.qorder = round_list;
         ob.nq = n_round;
         launch_bm(ob);
