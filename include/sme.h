@@ -94,8 +94,9 @@ void sme_destroy(sme_ctx *ctx);
  *   "cand_cap"      candidate list per query of the window path, 1..2048 (default 1024; >= 1024:
  *                   at least 16 k)
  *   "win_sample"    1 (default): sample windows first, thresholds raised, then the rest
- *   "win_stage_min" windows of the first sampled stage, at least (default 16; the stage
- *                   count follows, at most 9)
+ *   "win_stage_min" windows of the first sampled stage, at least (default 0 = auto: 16, or 8
+ *                   for indexes of >= 1024 windows of 4096 documents; the stage count
+ *                   follows, at most 9)
  *   "win_slice"     queries per window-path workgroup slice (default 256)
  *   "seed_tiles"    k_query_bm: best-bound tiles scored before the sweep, 0..8 (default 4)
  *   "query_order"   1 heaviest-term query order (default), 0 batch order

@@ -298,7 +298,7 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
       range(0, 1);
       cx->opt_win_sample = v;
     } else if (n == "win_stage_min") {
-      range(1, int64_t(1) << 20);
+      range(0, int64_t(1) << 20);
       cx->opt_win_stage_min = v;
     } else if (n == "kgram_rank") {
       range(0, 1);

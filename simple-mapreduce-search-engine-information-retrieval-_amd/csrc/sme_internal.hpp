@@ -57,7 +57,7 @@ struct sme_ctx {
   int64_t opt_kgram_rank = 0;     // "kgram_rank": 1 = K >= 2 gram keys by iterated ranking even when packed ids fit
   int64_t opt_win_slice = 256;    // "win_slice": queries per k_query_win workgroup slice (>= 1)
   int64_t opt_win_sample = 1;     // "win_sample": 1 = every 8th window first, thresholds raised, then the rest
-  int64_t opt_win_stage_min = 16;  // "win_stage_min": windows of the first stage (at least; the stage count follows)
+  int64_t opt_win_stage_min = 0;   // "win_stage_min": windows of the first stage (at least; the stage count follows; 0 = auto)
   int64_t opt_query_budget = 0;  // "query_table_budget": per-batch skip-table bytes (0: a quarter of free HBM)
   int64_t opt_corpus_keep = int64_t(16) << 30;  // "corpus_keep_bytes": host-corpus builds keep their device copy
                                                 // (no hipMalloc next build) only up to this size

@@ -2584,8 +2584,13 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     // windows seen, so it appends about k documents over the raised threshold;
     // only the first one runs on the seed threshold, and L makes it small (about
     // 16 windows, 1/8 .. 1/256 of the index).
+    // (auto: at least 16 windows, 8 from 1024 windows on -- a large index's first
+    // stage on the seed threshold costs ~3.5x a last-stage window, and the extra raise
+    // pass is cheap next to it: c5 (2,160 windows) -0.75 % per batch and 1,119 -> 72
+    // overflowed lists, while c2's 245 windows lose 3 % to a ninth stage)
+    const int64_t smin = cx->opt_win_stage_min > 0 ? cx->opt_win_stage_min : (nwin >= 1024 ? 8 : 16);
     int L = 3;
-    while (L < 8 && (nwin >> (L + 1)) >= cx->opt_win_stage_min) L++;
+    while (L < 8 && (nwin >> (L + 1)) >= smin) L++;
     int64_t n_samp = 0, stage_start[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     {
       std::vector<int32_t> &h = cx->h_wlist;  // outlives the async copy
