@@ -1233,6 +1233,21 @@ __device__ __forceinline__ QDesc ld_desc_nt(const QDesc *d, int64_t q0, int nt, 
   }
   return QDesc{0, 0, 0, -1, 0, 0.0};
 }
+// a wave-uniform pointer pinned to SGPRs (opaque to reassociation, so a load at
+// p + 32-bit lane offset uses the scalar-base address mode: no 64-bit VALU math)
+typedef const __attribute__((address_space(1))) uint8_t gbyte;
+__device__ __forceinline__ gbyte *uni_ptr(const uint8_t *p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return reinterpret_cast<gbyte *>(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t ld_g4(gbyte *base, uint32_t off) {
+  return *reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(base + off);
+}
+__device__ __forceinline__ uint4 ld_g16(gbyte *base, uint32_t off) {
+  const qu32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) qu32x4 *>(base + off);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 // wave-uniform records through the scalar cache (read-only here: written by
 // earlier launches), so the pipelined next-query records hold no VGPRs
 template <typename T>
@@ -1437,6 +1452,13 @@ struct QWinArgs {
 #ifndef SME_QWIN_SPARSE_NT
 #define SME_QWIN_SPARSE_NT 0
 #endif
+// SME_QW_HV2 = 1: heavy impact / bound rows and skip entries loaded at a scalar row
+// base + 32-bit lane offset, every lane loading (no exec-masked loads, no zeroed
+// registers; 64 -> 61 VGPRs, 69 -> 64 spilled SGPRs): measured slower (c3 kernel
+// 22.57 -> 22.81 ms, c5 1 M top-100 1972 -> 1982 ms, digests equal), so off
+#ifndef SME_QW_HV2
+#define SME_QW_HV2 0
+#endif
 // the experiment build's counters and timing switches; constants in the product
 // (so the product kernel holds no registers or branches for them)
 #ifdef SME_EXPERIMENTS
@@ -1519,6 +1541,27 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     // heavy terms' block maxima: one dword per term = the impact bound of this
     // lane's four 16-document blocks (index-resident bmq rows), all loads in flight
     uint32_t ub0 = 0, ub1 = 0;  // blocks 4 lane + {0, 1} | {2, 3} as u16 pairs
+#if SME_QW_HV2
+    {
+      // two rows per step, scalar row base + 32-bit lane offset (as the impact loads)
+      uint32_t bo = (uint32_t)((x << (kWinB - 4)) + 4 * lane);
+      asm volatile("" : "+v"(bo));
+      const int64_t bstr = a.hstride >> 4;
+      for (uint64_t mh = hm; mh;) {
+        const int j0 = (int)__builtin_ctzll(mh);
+        mh &= mh - 1;
+        const uint32_t w0 = ld_g4(uni_ptr(a.bmq + (int64_t)__builtin_amdgcn_readlane(D.hr, j0) * bstr), bo);
+        uint32_t w1 = 0;
+        if (mh) {
+          const int j1 = (int)__builtin_ctzll(mh);
+          mh &= mh - 1;
+          w1 = ld_g4(uni_ptr(a.bmq + (int64_t)__builtin_amdgcn_readlane(D.hr, j1) * bstr), bo);
+        }
+        ub0 += __builtin_amdgcn_perm(0u, w0, 0x0C010C00u) + __builtin_amdgcn_perm(0u, w1, 0x0C010C00u);
+        ub1 += __builtin_amdgcn_perm(0u, w0, 0x0C030C02u) + __builtin_amdgcn_perm(0u, w1, 0x0C030C02u);
+      }
+    }
+#else
     {
       const int64_t boff = (x << (kWinB - 4)) + 4 * lane;
       for (uint64_t mh = hm; mh;) {
@@ -1540,6 +1583,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
         }
       }
     }
+#endif
     // sparse terms: the window's postings into LDS -- impact sums per block, and
     // the (document, impact, tf) list (per term docno-ascending) for the exact
     // sums of passing blocks and the candidates' tf lookups
@@ -1583,8 +1627,14 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     // the next query's skip entries (its records arrived during the sparse pass)
     int32_t nmc = 0, nme = 0;
     if (ND.mdf > 0 && ND.hr < 0) {
+#if SME_QW_HV2
+      gbyte *s0 = uni_ptr(reinterpret_cast<const uint8_t *>(a.skt + x * a.nrows));
+      nmc = (int32_t)ld_g4(s0, (uint32_t)ND.brow << 2);
+      nme = (int32_t)ld_g4(s0 + (a.nrows << 2), (uint32_t)ND.brow << 2);
+#else
       nmc = a.skt[x * a.nrows + ND.brow];
       nme = a.skt[(x + 1) * a.nrows + ND.brow];
+#endif
     }
     // blocks over the gate: heavy maxima + the block's sparse impact sum
     uint32_t ub[4] = {ub0 & 0xFFFFu, ub0 >> 16, ub1 & 0xFFFFu, ub1 >> 16};
@@ -1719,6 +1769,38 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
             }
           }
         }
+#if SME_QW_HV2
+        // two heavy rows per step, every lane loading (a lane without a block reads
+        // block 0's bytes, a valid address, and its gate bits are dropped below), so
+        // no exec-masked loads and no zeroed registers; the row base is scalar and
+        // the window offset a 32-bit lane offset (one VALU-free address per load)
+        {
+          uint32_t wo = (uint32_t)((x << kWinB) + r0);
+          asm volatile("" : "+v"(wo));
+          auto addimp = [&](const uint4 v) {
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+              acc[2 * u] += __builtin_amdgcn_perm(0u, w4[u], 0x0C010C00u);
+              acc[2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
+            }
+          };
+          for (uint64_t mh = hm; mh;) {
+            const int j0 = (int)__builtin_ctzll(mh);
+            mh &= mh - 1;
+            const uint4 v0 = ld_g16(uni_ptr(a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j0) * a.hstride), wo);
+            if (mh) {
+              const int j1 = (int)__builtin_ctzll(mh);
+              mh &= mh - 1;
+              const uint4 v1 = ld_g16(uni_ptr(a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j1) * a.hstride), wo);
+              addimp(v0);
+              addimp(v1);
+            } else {
+              addimp(v0);
+            }
+          }
+        }
+#else
         for (uint64_t mh = hm; mh;) {
           uint4 v[SME_QIMPG];
 #pragma unroll
@@ -1742,6 +1824,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
             }
           }
         }
+#endif
         uint32_t cm = 0;  // documents of the block over the gate
         if (hb) {
           // biased accumulators: bit 15 of a half is set exactly when A(d) >= gate
