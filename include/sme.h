@@ -97,7 +97,8 @@ void sme_destroy(sme_ctx *ctx);
  *   "win_stage_min" windows of the first sampled stage, at least (default 0 = auto: 16, or 8
  *                   for indexes of >= 1024 windows of 4096 documents; the stage count
  *                   follows, at most 9)
- *   "win_slice"     queries per window-path workgroup slice (default 256)
+ *   "win_slice"     queries per window-path workgroup slice (default 0 = auto: 128, or 256 for
+ *                   indexes of >= 1024 windows)
  *   "seed_tiles"    k_query_bm: best-bound tiles scored before the sweep, 0..8 (default 4)
  *   "query_order"   1 heaviest-term query order (default), 0 batch order
  *   "agg_two_pass"  1 count + emit aggregation passes (default 0: single pass)

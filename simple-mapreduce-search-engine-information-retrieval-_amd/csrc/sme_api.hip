@@ -304,7 +304,7 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
       range(0, 1);
       cx->opt_kgram_rank = v;
     } else if (n == "win_slice") {
-      range(1, int64_t(1) << 30);
+      range(0, int64_t(1) << 30);
       cx->opt_win_slice = v;
     } else if (n == "seed_m") {
       range(0, 4096);

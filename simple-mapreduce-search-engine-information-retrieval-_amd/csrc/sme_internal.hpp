@@ -55,7 +55,7 @@ struct sme_ctx {
   int64_t opt_cand_cap = 1024;    // "cand_cap": candidate list per query of k_query_win (1..2048; >= 1024: at least 16 k)
   int64_t opt_seed_m = 64;        // "seed_m": seed postings per term (k_query_seed; 0 = no seed)
   int64_t opt_kgram_rank = 0;     // "kgram_rank": 1 = K >= 2 gram keys by iterated ranking even when packed ids fit
-  int64_t opt_win_slice = 256;    // "win_slice": queries per k_query_win workgroup slice (>= 1)
+  int64_t opt_win_slice = 0;      // "win_slice": queries per k_query_win workgroup slice (0 = auto: 128, 256 from 1024 windows)
   int64_t opt_win_sample = 1;     // "win_sample": 1 = every 8th window first, thresholds raised, then the rest
   int64_t opt_win_stage_min = 0;   // "win_stage_min": windows of the first stage (at least; the stage count follows; 0 = auto)
   int64_t opt_query_budget = 0;  // "query_table_budget": per-batch skip-table bytes (0: a quarter of free HBM)

@@ -2714,7 +2714,11 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
                            round_list, d_qoff, n_round, tbase, qpos);
       }
       wa.nq = n_round;
-      wa.nslices = (int)std::max<int64_t>(1, std::min<int64_t>(n_round / cx->opt_win_slice, 4096));
+      // (auto: 128 queries per slice below 1024 windows -- c2's 245 windows: c3 kernel
+      // 22.59 -> 22.34 ms, twice the workgroups per window --, 256 from 1024 on, where
+      // the launch is large anyway and c5 does not gain)
+      const int64_t qps = cx->opt_win_slice > 0 ? cx->opt_win_slice : (nwin >= 1024 ? 256 : 128);
+      wa.nslices = (int)std::max<int64_t>(1, std::min<int64_t>(n_round / qps, 4096));
       if (round == 0 && cx->opt_win_sample && nwin >= 16) {
         for (int sg = 0; sg <= L; sg++) {
           if (sg > 0) {  // raise thresholds, keep each list's best k

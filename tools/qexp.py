@@ -90,7 +90,7 @@ def main():
                                                              "query_total") if x in prof}}), flush=True)
         for n in opts:  # restore defaults
             ctx.set_option(n.strip(), {"heavy_div": 128, "seed_tiles": 4, "query_order": 1, "query_kernel": 0,
-                                       "cand_cap": 1024, "seed_m": 64, "win_slice": 256, "win_sample": 1, "win_stage_min": 0,
+                                       "cand_cap": 1024, "seed_m": 64, "win_slice": 0, "win_sample": 1, "win_stage_min": 0,
                                        }[n.strip()])
     ix.close()
     ctx.close()
