@@ -15,6 +15,11 @@ seed 9, strong scaling: the passages are split over the ranks) + 1M-query top-10
 --config c4shard: one GPU's shard of c4 (6.25M docs of ~280 tokens, V_w=2^22,
 seed 44, weak scaling).  These are profiling lines (profiles/), not the driver's.
 
+Beside `value`, timed the same way: value_with_records (+ the I9 serialization),
+value_query_ready (+ the once-per-index query preparation) and value_true_df
+(build in true-df idf mode + the global df exchange by owner rank over RCCL and
+the re-weight: the north star's "global df is an RCCL all-reduce" step).
+
 After the timed regions (untimed): full-size property checks of the built index
 (sum tf = tokens + docid tokens, V = distinct terms of the vocabulary + N, CSR
 offsets monotone, docnos ascending per term), a cross-kernel check of a query
@@ -80,6 +85,9 @@ def parse():
     p.add_argument("--cpu-opt-queries", type=int, default=20000, help="queries timed with the cpu-opt rank()")
     p.add_argument("--no-query", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the untimed host-to-host end-to-end stage")
+    p.add_argument("--true-df-steps", type=int, default=None,
+                   help="timed steps of the true-df leg (build + global df exchange + reweight; default --steps, "
+                        "0 = skip)")
     a = p.parse_args()
     cfg = dict(CONFIGS[a.config])
     for key in ("docs", "vocab", "queries"):
@@ -87,13 +95,18 @@ def parse():
             cfg[key] = getattr(a, key)
     a.cfg = cfg
     a.docs, a.vocab, a.queries = cfg["docs"], cfg["vocab"], cfg["queries"]
+    if a.true_df_steps is None:
+        a.true_df_steps = a.steps
     return a
 
 
 def spawn_ranks(n):
     """--gpus N > 1 without a launcher: start N rank processes of this script
     (one per GPU) and return rank 0's exit status (any failing rank fails the
-    run).  Nothing here touches the GPU: the children initialise their own."""
+    run).  The children are polled together: when one exits non-zero the others
+    (which would wait in a collective until the backend timeout) are terminated
+    at once and its status returned.  Nothing here touches the GPU: the children
+    initialise their own."""
     import socket
     import subprocess
     with socket.socket() as s:
@@ -104,6 +117,26 @@ def spawn_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        for p in procs:
+            c = p.poll()
+            if c is not None and c != 0:
+                failed = c
+                break
+        else:
+            time.sleep(0.2)
+    if failed is not None:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        return failed
     codes = [p.wait() for p in procs]
     bad = [c for c in codes if c != 0]
     return codes[0] if codes[0] != 0 else (bad[0] if bad else 0)
@@ -222,21 +255,24 @@ def main():
     barrier()
     dt_rec = (time.perf_counter() - t0) / a.steps
     gc.enable()
+    # a drop-in that serves queries right after its build also pays the
+    # once-per-index query preparation (the reference's own post-build step is
+    # the forward-index job, BuildIntDocVectorsForwardIndex.java:84-158): the same
+    # steps with sme_index_prepare_queries inside the clock -> value_query_ready
+    barrier()
+    gc.disable()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ix.close()
+        ix = step()
+        ix.prepare_queries(stream)
+    barrier()
+    dt_qr = (time.perf_counter() - t0) / a.steps
+    gc.enable()
     t_max = dt
     tot_bytes = nbytes
-    df_ex = None
     if dist is not None:
-        # true-df exchange, once per index, untimed: fingerprint
-        # all_gather + unique + df all_reduce over RCCL (dist.global_df_index)
-        D2 = importlib.import_module(PKG + ".dist")
-        df_ex = {}
-        barrier()
-        t_ex = time.perf_counter()
-        D2.global_df_index(ix, timings=df_ex)
-        barrier()
-        df_ex["total_ms"] = round((time.perf_counter() - t_ex) * 1e3, 3)
-        df_ex = {k2: (round(v, 3) if isinstance(v, float) else v) for k2, v in df_ex.items()}
-        tt = torch.tensor([dt, float(nbytes), float(N), float(V), float(P), dt_rec], dtype=torch.float64,
+        tt = torch.tensor([dt, float(nbytes), float(N), float(V), float(P), dt_rec, dt_qr], dtype=torch.float64,
                           device="cpu" if rehearse else "cuda")
         ts = [torch.zeros_like(tt) for _ in range(world)]
         dist.all_gather(ts, tt)
@@ -244,6 +280,7 @@ def main():
         t_max = float(ts[:, 0].max())
         tot_bytes = float(ts[:, 1].sum())
         dt_rec = float(ts[:, 5].max())
+        dt_qr = float(ts[:, 6].max())
     gbs = tot_bytes / t_max / 1e9
     alg_bytes = nbytes + 8 * P + 8 * (V + 1)  # A_build = B + 8P + 8(V+1) per GPU
     # dominant kernel: the stream tokenizer (k_tok_fast).  Algorithmic bytes per
@@ -288,6 +325,12 @@ def main():
                                        "(sme_index_serialize) per step, max over ranks; the records stay in HBM"
                                        + ("" if world == 1 else "; per-shard records (the reference layout "
                                           "needs dist.reference_partitions' exchange, not timed)")},
+        "value_query_ready": {"value": round(tot_bytes / dt_qr / 1e9, 4), "unit": "GB/s",
+                              "ms_per_step": round(dt_qr * 1e3, 3),
+                              "what": "build + TF-IDF + the once-per-index query preparation "
+                                      "(sme_index_prepare_queries: heavy tf / impact rows and their block "
+                                      "bounds, sparse posting words) per step, max over ranks: the index "
+                                      "ready to answer queries"},
         "build_roofline": {"achieved": round(achieved_build, 2), "unit": "GB/s",
                            "frac": round(achieved_build / HBM_PEAK_GBS, 5),
                            "what": "whole build step: A_build = B + 8P + 8(V+1) per GPU / step time"},
@@ -306,8 +349,6 @@ def main():
         result["roofline"]["frac_of_measured"] = (round(tok_gbs / cal.value, 5) if tok_gbs else None)
         result["hbm_copy_GBps"] = {"value": round(cal.value, 1), "what": "sme_hbm_copy_bench: 4 GiB device copy, "
                                    "16-byte nontemporal loads/stores, read + write bytes / kernel time (x10)"}
-    if df_ex is not None:
-        result["df_exchange_untimed"] = df_ex
     qinternal = None
     if query is not None:
         qinternal = (query.pop("_terms"), query.pop("_qoff"), query.pop("_out"))
@@ -323,6 +364,15 @@ def main():
         ix = None
         gc.collect()
         result["end_to_end_ms"] = end_to_end_stage(sme, ctx, d_corpus.value, nbytes, torch)
+    if ix is not None:
+        ix.close()
+        ix = None
+    ctx.close()
+    if a.true_df_steps > 0:
+        result["value_true_df"] = true_df_leg(a, sme, ctx_args=dict(k=1, num_partitions=1, device=local),
+                                              mapping=mapping, d_corpus=d_corpus.value, nbytes=nbytes,
+                                              stream=stream, D=D, barrier=barrier, world=world, torch=torch,
+                                              rehearse=rehearse)
     if rank == 0 and a.cpu_docs > 0:
         result["cpu_baseline"] = cpu_baseline(synth, a)
         if a.config == "c2":
@@ -331,12 +381,67 @@ def main():
             result["cpu_baseline"]["cpu_opt"].update(cpu_full)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if ix is not None:
-        ix.close()
-    ctx.close()
     L.sme_synth_free(d_corpus)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def true_df_leg(a, sme, ctx_args, mapping, d_corpus, nbytes, stream, D, barrier, world, torch, rehearse):
+    """The north star's collective in a timed leg: "global df is an RCCL
+    all-reduce over xGMI".  Each step builds the shard in true-df idf mode
+    (log10(N / df)) and, on N > 1 ranks, exchanges the df of every local term
+    with its owner rank (dist.global_df_index: device fingerprints, owner
+    all_to_all, owner sums in libsme, all_to_all back) plus the all-reduce of N,
+    then re-weights the shard with the global statistics (sme_index_reweight) --
+    the reducer's df over all map outputs, TermKGramDocIndexer.java:175-183.
+    Timed like `value` (barrier + synchronize on both sides, max over ranks).
+    Runs after the main legs with their context closed (one build workspace in
+    HBM at a time)."""
+    ctx = sme.Context(idf_mode=sme.SME_IDF_TRUE_DF, **ctx_args)
+    ctx.load_docno_mapping(mapping)
+    ex = {}
+
+    def step(timings=None):
+        ix = ctx.build_device(d_corpus, nbytes, stream)
+        if D is not None:
+            gdf = D.global_df_index(ix, timings=timings)
+            ix.reweight(D.global_count(ix.N), gdf.data_ptr(), stream)
+        return ix
+
+    ix = None
+    for _ in range(max(1, a.warmup)):
+        if ix is not None:
+            ix.close()
+        ix = step()
+    barrier()
+    gc.disable()
+    t0 = time.perf_counter()
+    for i in range(a.true_df_steps):
+        ix.close()
+        ix = step(ex if i == a.true_df_steps - 1 else None)
+    barrier()
+    dt = (time.perf_counter() - t0) / a.true_df_steps
+    gc.enable()
+    tot = float(nbytes)
+    if D is not None:
+        import torch.distributed as tdist
+        tt = torch.tensor([dt, float(nbytes)], dtype=torch.float64, device="cpu" if rehearse else "cuda")
+        ts = [torch.zeros_like(tt) for _ in range(world)]
+        tdist.all_gather(ts, tt)
+        ts = torch.stack(ts).cpu().numpy()
+        dt, tot = float(ts[:, 0].max()), float(ts[:, 1].sum())
+    prof = ctx.last_build_profile()
+    ix.close()
+    ctx.close()
+    out = {"value": round(tot / dt / 1e9, 4), "unit": "GB/s", "ms_per_step": round(dt * 1e3, 3),
+           "steps": a.true_df_steps, "build_ms_last_step": prof.get("total"),
+           "what": "build in true-df idf mode + (N > 1) the global df exchange by owner rank and the all-reduce of N "
+                   "over %s + sme_index_reweight with the global N / df, per step, max over ranks"
+                   % ("RCCL" if D is not None and not rehearse else "gloo" if D is not None else "no collective "
+                      "(one rank: the local df is the global df)")}
+    if ex:
+        out["df_exchange_ms_last_step"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in ex.items()}
+    return out
 
 
 def run_queries(a, sme, synth, ix, torch, dist, world, rank, barrier):

@@ -285,6 +285,26 @@ int sme_df_owner_sum(sme_ctx *ctx, const uint64_t *d_fp, const int64_t *d_df, in
 int sme_df_owner_unpack(sme_ctx *ctx, const int64_t *d_ret, const int64_t *d_pos, int64_t n, int64_t *d_out,
                         void *stream);
 
+/* Query-owner merge (dist.merge_topk_owner): rows x m candidates
+ * (d_score / d_docno / optional d_tie, row-major, any order, docno -1 pads, e.g.
+ * the W shards' top-k lists of the queries this rank owns) -> per row the best k
+ * in (score desc, tie asc, docno asc) order, docno -1 / score 0 / tie ~0 pads.
+ * The tie word is sme_query_topk_tie's (0 in the north-star docno order), so the
+ * merged rows equal one index's top-k (IntDocVectorsForwardIndex.java:215-222:
+ * Collections.sort over the candidates, first k).  k <= 2048.  Device memory;
+ * synchronized on return. */
+int sme_topk_merge_rows(sme_ctx *ctx, const double *d_score, const int32_t *d_docno, const uint32_t *d_tie,
+                        int64_t rows, int m, int k, int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie,
+                        void *stream);
+
+/* Owner side of the cross-shard duplicate-docid check (dist.docno_duplicates):
+ * d_rows = n (key, source rank) pairs (u64, keys zero-extended 32-bit docnos)
+ * received by the keys' owner rank (grouped with sme_df_owner_pack); *count =
+ * distinct keys that arrive from two or more source ranks.  A docid held by two
+ * shards is one posting with summed tf in the reference's single reducer
+ * (TermKGramDocIndexer.java:202-210), so per-shard scoring must refuse it. */
+int sme_count_shared_keys(sme_ctx *ctx, const uint64_t *d_rows, int64_t n, int64_t *count, void *stream);
+
 /* Recompute the fp64 TF-IDF weights of a doc-sharded index with global
  * statistics: n_global = records over all shards (all-reduced doc counter),
  * d_df_global = per local term the all-reduced df (device int64[V]) or NULL to

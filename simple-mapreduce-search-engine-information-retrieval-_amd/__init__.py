@@ -50,6 +50,7 @@ EXPORTS = [
     "sme_split_points", "sme_split_points_device", "sme_index_term_fingerprints", "sme_set_option",
     "sme_index_prepare_queries", "sme_hbm_copy_bench", "sme_index_pack_pieces", "sme_merge_pieces",
     "sme_index_record_docnos", "sme_df_owner_pack", "sme_df_owner_sum", "sme_df_owner_unpack",
+    "sme_topk_merge_rows", "sme_count_shared_keys",
 ]
 
 
@@ -113,6 +114,8 @@ def lib():
     L.sme_df_owner_pack.argtypes = [vp, vp, vp, C.c_int64, C.c_int, vp, vp, vp, i64p, vp]
     L.sme_df_owner_sum.argtypes = [vp, vp, vp, C.c_int64, vp, i64p, vp]
     L.sme_df_owner_unpack.argtypes = [vp, vp, vp, C.c_int64, vp, vp]
+    L.sme_topk_merge_rows.argtypes = [vp, vp, vp, vp, C.c_int64, C.c_int, C.c_int, vp, vp, vp, vp]
+    L.sme_count_shared_keys.argtypes = [vp, vp, C.c_int64, i64p, vp]
     _lib = L
     return L
 
@@ -244,6 +247,20 @@ class Context:
         """sme_df_owner_unpack: out[i] = ret[pos[i]]."""
         _check(lib().sme_df_owner_unpack(self._h, C.c_void_p(d_ret), C.c_void_p(d_pos), n, C.c_void_p(d_out),
                                          C.c_void_p(stream or 0)))
+
+    def topk_merge_rows(self, d_score, d_docno, d_tie, rows, m, k, d_out_docno, d_out_score, d_out_tie, stream=None):
+        """sme_topk_merge_rows: rows x m candidates (device; d_tie may be 0) -> per
+        row the best k by (score desc, tie asc, docno asc), docno -1 pads."""
+        _check(lib().sme_topk_merge_rows(self._h, C.c_void_p(d_score), C.c_void_p(d_docno), C.c_void_p(d_tie or 0),
+                                         rows, m, k, C.c_void_p(d_out_docno), C.c_void_p(d_out_score),
+                                         C.c_void_p(d_out_tie or 0), C.c_void_p(stream or 0)))
+
+    def count_shared_keys(self, d_rows, n, stream=None):
+        """sme_count_shared_keys: (key, source rank) u64 pairs -> distinct keys
+        that arrive from two or more sources."""
+        cnt = C.c_int64()
+        _check(lib().sme_count_shared_keys(self._h, C.c_void_p(d_rows), n, C.byref(cnt), C.c_void_p(stream or 0)))
+        return cnt.value
 
     def merge_pieces(self, d_blobs, sizes):
         """sme_merge_pieces: the blobs one rank received from every shard (device

@@ -762,6 +762,27 @@ int sme_df_owner_unpack(sme_ctx *ctx, const int64_t *d_ret, const int64_t *d_pos
   });
 }
 
+int sme_topk_merge_rows(sme_ctx *ctx, const double *d_score, const int32_t *d_docno, const uint32_t *d_tie,
+                        int64_t rows, int m, int k, int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie,
+                        void *stream) {
+  return guard([&] {
+    if (!ctx || rows < 0 || m < 0 || k < 1 || (rows > 0 && (!d_out_docno || !d_out_score || (m > 0 && (!d_score || !d_docno)))))
+      throw sme::Error(SME_EINVAL, "bad argument");
+    set_device(ctx);
+    hipStream_t st = stream_of(ctx, stream);
+    sme::merge_rows(d_score, d_docno, d_tie, rows, m, k, d_out_docno, d_out_score, d_out_tie, st);
+    SME_HIP(hipStreamSynchronize(st));
+  });
+}
+
+int sme_count_shared_keys(sme_ctx *ctx, const uint64_t *d_rows, int64_t n, int64_t *count, void *stream) {
+  return guard([&] {
+    if (!ctx || !count || n < 0 || (n > 0 && !d_rows)) throw sme::Error(SME_EINVAL, "bad argument");
+    set_device(ctx);
+    *count = sme::count_shared_keys(ctx, d_rows, n, stream_of(ctx, stream));
+  });
+}
+
 int sme_index_reweight(sme_index *ix, int64_t n_global, const int64_t *d_df_global, void *stream) {
   return guard([&] {
     if (!ix || n_global < 0) throw sme::Error(SME_EINVAL, "bad argument");

@@ -3813,6 +3813,17 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     hipStream_t s2 = cx->aux_stream;
     SME_HIP(hipEventRecord(cx->ev_fork, st));
     SME_HIP(hipStreamWaitEvent(s2, cx->ev_fork, 0));
+    // every exit from this block -- a throw between the fork and the join
+    // included -- makes st wait for the auxiliary stream's kernels, so they never
+    // write docno_o / tf_o after the build's workspace is released or reused
+    struct AuxJoin {
+      hipStream_t st, s2;
+      hipEvent_t ev;
+      ~AuxJoin() {
+        (void)hipEventRecord(ev, s2);
+        (void)hipStreamWaitEvent(st, ev, 0);
+      }
+    } aux_join{st, s2, cx->ev_join};
     hipLaunchKernelGGL(k_tfsort_small, dim3(grid_for(Vi * 64, 256, 8192)), dim3(256), 0, s2, off, seg_small, nseg + 2,
                        docno_d, tf_d, docno_o, tf_o);
     const size_t lds4 = (size_t)(max_tf + 1) * 4 * sizeof(int32_t);
@@ -3821,7 +3832,6 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
     hipLaunchKernelGGL(k_tfsort_block<1>, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(Vi, 1), 32768)),
                        dim3(64), lds4 / 4, s2, off, Vi, docno_d, tf_d, docno_o, tf_o, seg_wave, nseg + 3, max_tf);
     SME_CHECK_LAUNCH();
-    SME_HIP(hipEventRecord(cx->ev_join, s2));
     // large segments: tiles spread over the whole chip
     hipLaunchKernelGGL(k_tf_ntiles, dim3(grid_for(Vi + 1)), dim3(256), 0, st, off, seg_large, nseg + 1, Vi, ntl);
     size_t tbb = 0;
@@ -3839,8 +3849,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
                          nseg + 1, toff, ntiles, docno_d, tf_d, max_tf, tcnt, docno_o, tf_o);
     }
     SME_CHECK_LAUNCH();
-    SME_HIP(hipStreamWaitEvent(st, cx->ev_join, 0));
-  } else if (PP > 0) {
+  } else if (PP > 0) {  // (aux_join: st waits for the auxiliary stream here)
     const int tfb = bits_for((uint64_t)max_tf);
     if (tbits + tfb <= 32) {  // u32 composite (term, tf desc)
       const uint32_t tfmask = (uint32_t)((1ull << tfb) - 1);

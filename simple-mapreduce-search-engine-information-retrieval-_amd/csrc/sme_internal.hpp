@@ -121,8 +121,10 @@ struct sme_index {
   // query-side heavy rows (prepare_queries, sme_query.hip): tf byte rows, 16-doc
   // and 1024-doc block maxima of the terms covering >= 1/div of the docno span
   sme::DevBuf d_hrow_of;  // int32 [V] heavy row or -1
-  sme::DevBuf d_heavy;    // u8 [H][T * 1024] tf | [H][T * 64] bm16 | [H][T] bm1k
-  const uint8_t *q_tfrow = nullptr, *q_bm16 = nullptr, *q_bm1k = nullptr, *q_imp = nullptr, *q_bmq = nullptr;
+  // u8 [H][T * 1024] tf | imp | [H][T * 64] bm16 | [H][T] bm1k | [H][T * 256] sbq
+  sme::DevBuf d_heavy;
+  const uint8_t *q_tfrow = nullptr, *q_bm16 = nullptr, *q_bm1k = nullptr, *q_imp = nullptr;
+  const uint8_t *q_sbq = nullptr;  // impact maxima of 4-document sub-blocks (k_query_win's second level)
   // k_query_win's sparse postings, one word per docno-order posting of a term
   // without a heavy row: (docno - dmin) mod 4096 | q(tf) << 12 | min(tf, 4095) << 20
   sme::DevBuf d_spk;
@@ -241,8 +243,12 @@ void pack_pieces(sme_index *ix, int world, uint8_t *d_out, uint64_t *sizes, hipS
 sme_index *merge_pieces(sme_ctx *cx, const uint8_t *d_blobs, const uint64_t *sizes, int np, hipStream_t st);
 void reweight_index(sme_index *ix, int64_t N, const int64_t *d_gdf, hipStream_t st);
 void prepare_queries(sme_index *ix, hipStream_t st);
+// tie_bits: the reference tie word's tf width (24, or 22 when a query of the
+// batch has > 256 terms); 0 = decided by this batch.  Only the nested calls of
+// one batch (query-range splits, overflow subsets) pass it, so every query of a
+// batch -- on every doc shard answering it -- gets the same tie words.
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k,
-                int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie, hipStream_t st);
+                int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie, hipStream_t st, int tie_bits = 0);
 void tokenize_string(sme_ctx *cx, const uint8_t *h_utf8, size_t n, std::vector<std::vector<uint16_t>> &out,
                      hipStream_t st);
 void term_fingerprints(sme_index *ix, uint64_t *d_out, hipStream_t st);
@@ -252,6 +258,11 @@ void dfx_pack(sme_ctx *cx, const uint64_t *fp, const int64_t *df, int64_t n, int
 void dfx_sum(sme_ctx *cx, const uint64_t *fp, const int64_t *df, int64_t n, int64_t *out, int64_t *h_distinct,
              hipStream_t st);
 void dfx_unpack(const int64_t *ret, const int64_t *pos, int64_t n, int64_t *out, hipStream_t st);
+// owner-side steps of the N > 1 query path (sme_owner.hip): merge of the shards'
+// top-k rows, and the count of keys that arrive from two or more ranks
+void merge_rows(const double *s, const int32_t *d, const uint32_t *t, int64_t rows, int m, int k, int32_t *od,
+                double *os, uint32_t *ot, hipStream_t st);
+int64_t count_shared_keys(sme_ctx *cx, const uint64_t *rows, int64_t n, hipStream_t st);
 void lookup_terms(sme_index *ix, const std::vector<std::vector<uint16_t>> &terms, int32_t *ids,
                   hipStream_t st);
 }  // namespace sme

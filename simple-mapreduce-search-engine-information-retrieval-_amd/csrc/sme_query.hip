@@ -486,6 +486,14 @@ __global__ void k_heavy_bm16(const uint4 *tfrow, int64_t n, uint8_t *bm16) {
     bm16[i] = (uint8_t)max(max(max_u8x4(v.x), max_u8x4(v.y)), max(max_u8x4(v.z), max_u8x4(v.w)));
   }
 }
+// sbq[i] = largest impact byte of the 4-document sub-block i of the impact rows
+// (flat over all rows, like bm16): k_query_win's second-level bound
+__global__ void k_heavy_sbq(const uint4 *imp, int64_t n, uint32_t *sbq) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 v = imp[i];
+    sbq[i] = max_u8x4(v.x) | (max_u8x4(v.y) << 8) | (max_u8x4(v.z) << 16) | (max_u8x4(v.w) << 24);
+  }
+}
 // bm1k[i] = largest of the 64 block maxima of tile i
 __global__ void k_heavy_bm1k(const uint4 *bm16, int64_t n, uint8_t *bm1k) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1420,7 +1428,7 @@ struct QWinArgs {
   int64_t nrows;
   const uint8_t *qlut;         // impact tables [rows][256]
   const uint8_t *imp, *tfrow;  // [H][hstride] impact / tf bytes
-  const uint8_t *bmq;          // [H][hstride / 16] impact bound of every 16-document block
+  const uint8_t *sbq;          // [H][hstride / 4] impact bound of every 4-document sub-block
   int64_t hstride, dmin, T, nwin;
   const int32_t *wlist;        // windows of this launch (nullptr: 0 .. nwin - 1), nw of them
   int64_t nw;
@@ -1447,17 +1455,14 @@ struct QWinArgs {
 #define SME_QIMPG 2
 #endif
 #ifndef SME_QFB
-#define SME_QFB 8
+#define SME_QFB 4
+#endif
+// heavy sub-block bound rows (uint4 per lane) in flight per step of the first level
+#ifndef SME_QSBG
+#define SME_QSBG 2
 #endif
 #ifndef SME_QWIN_SPARSE_NT
 #define SME_QWIN_SPARSE_NT 0
-#endif
-// SME_QW_HV2 = 1: heavy impact / bound rows and skip entries loaded at a scalar row
-// base + 32-bit lane offset, every lane loading (no exec-masked loads, no zeroed
-// registers; 64 -> 61 VGPRs, 69 -> 64 spilled SGPRs): measured slower (c3 kernel
-// 22.57 -> 22.81 ms, c5 1 M top-100 1972 -> 1982 ms, digests equal), so off
-#ifndef SME_QW_HV2
-#define SME_QW_HV2 0
 #endif
 // the experiment build's counters and timing switches; constants in the product
 // (so the product kernel holds no registers or branches for them)
@@ -1477,10 +1482,11 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
   // per block: sparse postings << 16 | their impact sum (<= 256 x 254 < 2^16), and
   // the first two postings inline ((r & 15) | q << 4), so a passing block reads its
   // documents' sparse impacts without searching the list
-  __shared__ uint32_t bsum_all[kWNT / 64][kWin / 16];
-  __shared__ uint16_t bent_all[kWNT / 64][2 * (kWin / 16)];
-  __shared__ uint32_t slist_all[kWNT / 64][kSList];   // the window's sparse postings: r | q << 12 | tf << 20
-  __shared__ uint16_t blist_all[kWNT / 64][kWin / 16];  // blocks over the gate
+  // (16-byte aligned: read as uint4, and bent / slist hold 32-byte slots)
+  __shared__ alignas(16) uint32_t bsum_all[kWNT / 64][kWin / 16];
+  __shared__ alignas(16) uint16_t bent_all[kWNT / 64][2 * (kWin / 16)];
+  __shared__ alignas(16) uint32_t slist_all[kWNT / 64][kSList];  // the window's sparse postings: r | q << 12 | tf << 20
+  __shared__ uint16_t blist_all[kWNT / 64][kWin / 16];  // sub-blocks over the gate (chunks of 256)
   __shared__ uint16_t clist_all[kWNT / 64][kCList];     // documents over the gate
   __shared__ double s_lut[kWinLut];                    // 1 + ln(tf) for tf < 128
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1538,52 +1544,43 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     const uint64_t sm = (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
 #endif
     const uint32_t gate = (uint32_t)__builtin_amdgcn_readfirstlane((int)gate_of(th0, a.alpha));
-    // heavy terms' block maxima: one dword per term = the impact bound of this
-    // lane's four 16-document blocks (index-resident bmq rows), all loads in flight
-    uint32_t ub0 = 0, ub1 = 0;  // blocks 4 lane + {0, 1} | {2, 3} as u16 pairs
-#if SME_QW_HV2
-    {
-      // two rows per step, scalar row base + 32-bit lane offset (as the impact loads)
-      uint32_t bo = (uint32_t)((x << (kWinB - 4)) + 4 * lane);
-      asm volatile("" : "+v"(bo));
-      const int64_t bstr = a.hstride >> 4;
-      for (uint64_t mh = hm; mh;) {
-        const int j0 = (int)__builtin_ctzll(mh);
-        mh &= mh - 1;
-        const uint32_t w0 = ld_g4(uni_ptr(a.bmq + (int64_t)__builtin_amdgcn_readlane(D.hr, j0) * bstr), bo);
-        uint32_t w1 = 0;
-        if (mh) {
-          const int j1 = (int)__builtin_ctzll(mh);
-          mh &= mh - 1;
-          w1 = ld_g4(uni_ptr(a.bmq + (int64_t)__builtin_amdgcn_readlane(D.hr, j1) * bstr), bo);
-        }
-        ub0 += __builtin_amdgcn_perm(0u, w0, 0x0C010C00u) + __builtin_amdgcn_perm(0u, w1, 0x0C010C00u);
-        ub1 += __builtin_amdgcn_perm(0u, w0, 0x0C030C02u) + __builtin_amdgcn_perm(0u, w1, 0x0C030C02u);
-      }
-    }
-#else
-    {
-      const int64_t boff = (x << (kWinB - 4)) + 4 * lane;
-      for (uint64_t mh = hm; mh;) {
-        uint32_t wq[4];
+    // every u16 accumulator below starts at 2^15 - gate, so a bound or an A(d)
+    // reaching the gate is its bit 15 (A(d) < 2^14 and gate <= 2^14 + 1 leave no
+    // carry between halves; a gate past 2^15 - 1 takes no bias, and nothing
+    // reaches bit 15)
+    const uint32_t bias = gate > 0x7FFFu ? 0u : 0x8000u - gate;
+    const uint32_t bias2 = bias | (bias << 16);
+    // heavy terms' sub-block maxima: one uint4 per term = the impact bounds of the
+    // 16 four-document sub-blocks of this lane's 64 documents (index-resident sbq
+    // rows), two loads in flight; sb[i] holds sub-blocks 2i (low u16) and 2i + 1
+    uint32_t sb[8];
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
-          wq[g] = 0;
+    for (int i = 0; i < 8; i++) sb[i] = bias2;
+    {
+      const int64_t soff = (x << (kWinB - 2)) + 16 * lane;
+      const int64_t hstr4 = a.hstride >> 2;
+      for (uint64_t mh = hm; mh;) {
+        uint4 v[SME_QSBG];
+#pragma unroll
+        for (int g = 0; g < SME_QSBG; g++) {
+          v[g] = make_uint4(0, 0, 0, 0);
           if (mh) {
             const int j = (int)__builtin_ctzll(mh);
             mh &= mh - 1;
-            wq[g] = *reinterpret_cast<const uint32_t *>(
-                a.bmq + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * (a.hstride >> 4) + boff);
+            v[g] = *reinterpret_cast<const uint4 *>(a.sbq + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * hstr4 + soff);
           }
         }
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
-          ub0 += __builtin_amdgcn_perm(0u, wq[g], 0x0C010C00u);
-          ub1 += __builtin_amdgcn_perm(0u, wq[g], 0x0C030C02u);
+        for (int g = 0; g < SME_QSBG; g++) {
+          const uint32_t w4[4] = {v[g].x, v[g].y, v[g].z, v[g].w};
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            sb[2 * u] += __builtin_amdgcn_perm(0u, w4[u], 0x0C010C00u);
+            sb[2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
+          }
         }
       }
     }
-#endif
     // sparse terms: the window's postings into LDS -- impact sums per block, and
     // the (document, impact, tf) list (per term docno-ascending) for the exact
     // sums of passing blocks and the candidates' tf lookups
@@ -1627,61 +1624,68 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     // the next query's skip entries (its records arrived during the sparse pass)
     int32_t nmc = 0, nme = 0;
     if (ND.mdf > 0 && ND.hr < 0) {
-#if SME_QW_HV2
-      gbyte *s0 = uni_ptr(reinterpret_cast<const uint8_t *>(a.skt + x * a.nrows));
-      nmc = (int32_t)ld_g4(s0, (uint32_t)ND.brow << 2);
-      nme = (int32_t)ld_g4(s0 + (a.nrows << 2), (uint32_t)ND.brow << 2);
-#else
       nmc = a.skt[x * a.nrows + ND.brow];
       nme = a.skt[(x + 1) * a.nrows + ND.brow];
-#endif
     }
-    // blocks over the gate: heavy maxima + the block's sparse impact sum
-    uint32_t ub[4] = {ub0 & 0xFFFFu, ub0 >> 16, ub1 & 0xFFFFu, ub1 >> 16};
+    // sub-blocks over the gate: heavy maxima + their block's sparse impact sum
     if (total > 0) {
-      // + the block's sparse impact sum (>= the sparse sum of any of its documents)
+      // + the block's sparse impact sum (>= the sparse sum of any of its documents;
+      // clamped: any sum >= 2^14 passes every gate, A(d) <= 64 x 254 < 2^14)
       int li = lane;
       asm volatile("" : "+v"(li));  // (an address recomputed here, not a hoisted register that spills)
       const uint4 b4 = reinterpret_cast<const uint4 *>(bsum)[li];
       const uint32_t bws[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-      for (int m = 0; m < 4; m++) ub[m] += wide_nl ? (bws[m] ? 0x10000u : 0u) : (bws[m] & 0xFFFFu);
+      for (int m = 0; m < 4; m++) {
+        const uint32_t c = wide_nl ? (bws[m] ? 0x4000u : 0u) : min(bws[m] & 0xFFFFu, 0x4000u);
+        sb[2 * m] += c | (c << 16);
+        sb[2 * m + 1] += c | (c << 16);
+      }
     }
-    uint32_t bm = 0;
+    uint32_t smk = 0;  // bit i: sub-block 16 lane + i reaches the gate
+    {
+      uint32_t hi = 0;
 #pragma unroll
-    for (int m = 0; m < 4; m++) bm |= (ub[m] >= gate ? 1u : 0u) << m;
-    const int32_t bl = __popc(bm);
-    const int32_t bincl = wave_incl_sum(bl);
-    const int32_t nblk = __builtin_amdgcn_readlane(bincl, 63);
+      for (int i = 0; i < 8; i++) hi |= (sb[i] & 0x80008000u) >> (15 - 2 * i);
+      smk = (hi & 0x5555u) | ((hi >> 15) & 0xAAAAu);
+    }
+    const int32_t sl = __popc(smk);
+    const int32_t sincl = wave_incl_sum(sl);
+    const int32_t nsub = __builtin_amdgcn_readlane(sincl, 63);
     if (QW_STATS && lane == 0) {
       atomicAdd(QW_STATS + 0, 1ull);
       atomicAdd(QW_STATS + 1, (unsigned long long)total);
-      atomicAdd(QW_STATS + 2, (unsigned long long)nblk);
+      atomicAdd(QW_STATS + 2, (unsigned long long)nsub);
       atomicAdd(QW_STATS + 3, (unsigned long long)__popcll(hm));
     }
-    if (nblk > 0 && !(QW_EXPER & 1)) {
-      qwave_sync();
-      {
-        int32_t o = bincl - bl;
-        for (uint32_t m = bm; m; m &= m - 1) blist[o++] = (uint16_t)(4 * lane + __builtin_ctz(m));
-      }
-      qwave_sync();
+    if (nsub > 0 && !(QW_EXPER & 1)) {
       const uint64_t amask = hm | sm;
-      // every u16 accumulator starts at 2^15 - gate, so A(d) >= gate is
-      // its bit 15 (A(d) < 2^14 and gate <= 2^14 + 1 leave no carry between halves;
-      // a gate past 2^15 - 1 takes no bias, and no document reaches bit 15)
-      const uint32_t bias = gate > 0x7FFFu ? 0u : 0x8000u - gate;
-      const uint32_t bias2 = bias | (bias << 16);
       const bool unl = !listed && total > 0;  // (wave-uniform)
-      // slots: the first 64 passing blocks, 32 bytes each, the first 32 in slist, the rest in bent
+      // slots: the first 64 blocks holding a passing sub-block, 32 bytes each, the
+      // first 32 in slist, the rest in bent
       uint32_t *const slot0 = slist, *const slot32 = reinterpret_cast<uint32_t *>(bent);
+      auto slot_of = [&](int i) { return i < 32 ? slot0 + 8 * i : slot32 + 8 * (i - 32); };
       if (unl) {
-        // a window whose sparse postings are too many to list: its first 64 passing
-        // blocks take slots (bit 31 | slot over their block sums: the bounds are
-        // done), and a second pass over the postings sums each slot's documents
-        // exactly into a u16 table in the list's LDS, which this pair leaves unused
-        if (lane < nblk) bsum[blist[lane]] = 0x80000000u | (uint32_t)lane;
-        uint32_t *my = lane < 32 ? slot0 + 8 * lane : slot32 + 8 * (lane - 32);
+        // a window whose sparse postings are too many to list: its first 64 blocks
+        // with a passing sub-block take slots (bit 31 | slot over their block sums:
+        // the bounds are done), and a second pass over the postings sums each slot's
+        // documents exactly into a u16 table in the list's LDS, which this pair
+        // leaves unused
+        uint32_t bm = 0;
+#pragma unroll
+        for (int m = 0; m < 4; m++) bm |= ((smk >> (4 * m)) & 0xFu) ? (1u << m) : 0u;
+        const int32_t bl = __popc(bm);
+        const int32_t bincl = wave_incl_sum(bl);
+        const int32_t nblk = __builtin_amdgcn_readlane(bincl, 63);
+        qwave_sync();
+        {
+          int32_t o = bincl - bl;
+          for (uint32_t m = bm; m; m &= m - 1, o++)
+            if (o < 64) clist[o] = (uint16_t)(4 * lane + __builtin_ctz(m));
+        }
+        qwave_sync();
+        if (lane < nblk) bsum[clist[lane]] = 0x80000000u | (uint32_t)lane;
+        uint32_t *my = slot_of(lane);
         *reinterpret_cast<uint4 *>(my) = make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4 *>(my + 4) = make_uint4(0, 0, 0, 0);
         qwave_sync();
@@ -1699,238 +1703,201 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
             const int r = (int)(pw & 0xFFFu);
             const uint32_t sw = bsum[r >> 4];
             if (sw >> 31) {
-              const int sl = (int)(sw & 0xFFu);
-              uint32_t *t = sl < 32 ? slot0 + 8 * sl : slot32 + 8 * (sl - 32);
+              uint32_t *t = slot_of((int)(sw & 0xFFu));
               atomicAdd(t + ((r & 15) >> 1), ((pw >> 12) & 0xFFu) << ((r & 1) << 4));  // A(d) < 2^14: no carry
             }
           }
         }
         qwave_sync();
       }
-      // one passing block per lane: exact A(d) of its 16 documents
-      for (int32_t b0 = 0; b0 < nblk; b0 += 64) {
-        const bool hb = b0 + lane < nblk;
-        const int blk = hb ? (int)blist[b0 + lane] : 0;
-        const int r0 = blk << 4;  // first document of the block in the window
-        uint32_t acc[8];          // documents r0 + 2m (low u16), + 1 (high)
-#pragma unroll
-        for (int i = 0; i < 8; i++) acc[i] = bias2;
-        if (unl && hb) {
-          if (b0 == 0) {  // a slot: exact sums
-            const uint32_t *my = lane < 32 ? slot0 + 8 * lane : slot32 + 8 * (lane - 32);
-            const uint4 u0 = *reinterpret_cast<const uint4 *>(my), u1 = *reinterpret_cast<const uint4 *>(my + 4);
-            acc[0] += u0.x;
-            acc[1] += u0.y;
-            acc[2] += u0.z;
-            acc[3] += u0.w;
-            acc[4] += u1.x;
-            acc[5] += u1.y;
-            acc[6] += u1.z;
-            acc[7] += u1.w;
-          } else {  // past 64 passing blocks: the block's sum bounds each document
-            // (clamped: any sum >= 2^14 passes every gate, A(d) <= 64 x 254 < 2^14)
-            const uint32_t bsc = wide_nl ? 0x4000u : min(bsum[blk] & 0xFFFFu, 0x4000u);
-#pragma unroll
-            for (int i = 0; i < 8; i++) acc[i] += bsc | (bsc << 16);
-          }
-        }
-        const uint32_t bw = (listed && total > 0 && hb) ? bsum[blk] : 0u;
-        const uint32_t bs = bw & 0xFFFFu, bn = bw >> 16;
-        if (bs != 0 && bn <= 2) {  // the common case: the block's inline entries
-          for (uint32_t k2 = 0; k2 < bn; k2++) {
-            const uint32_t ent = bent[2 * blk + k2];
-            const int dr = (int)(ent & 15u);
-            const uint32_t add = (ent >> 4) << ((dr & 1) << 4);
-#pragma unroll
-            for (int i = 0; i < 8; i++) acc[i] += (dr >> 1) == i ? add : 0u;
-          }
-        } else if (bs != 0) {  // (most passing blocks hold no sparse posting)
-          {
-            // the block's sparse postings: per sparse term, its listed entries
-            // from the first with r >= r0 while r < r0 + 16
-            for (uint64_t m = sm; m; m &= m - 1) {
-              const int j = (int)__builtin_ctzll(m);
-              int lo = __builtin_amdgcn_readlane(prej, j);
-              const int hi0 = lo + __builtin_amdgcn_readlane(cj, j);
-              int hi = hi0;
-              while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if ((int)(slist[mid] & 0xFFFu) < r0) lo = mid + 1;
-                else hi = mid;
-              }
-              for (; lo < hi0; lo++) {
-                const uint32_t ent = slist[lo];
-                const int dr = (int)(ent & 0xFFFu) - r0;
-                if (dr >= 16) break;
-                const uint32_t add = ((ent >> 12) & 0xFFu) << ((dr & 1) << 4);
-#pragma unroll
-                for (int i = 0; i < 8; i++) acc[i] += (dr >> 1) == i ? add : 0u;
-              }
-            }
-          }
-        }
-#if SME_QW_HV2
-        // two heavy rows per step, every lane loading (a lane without a block reads
-        // block 0's bytes, a valid address, and its gate bits are dropped below), so
-        // no exec-masked loads and no zeroed registers; the row base is scalar and
-        // the window offset a 32-bit lane offset (one VALU-free address per load)
+      // one passing sub-block per lane: exact A(d) of its 4 documents (one impact
+      // dword per heavy term + its sparse impacts), then the candidates.  The
+      // sub-blocks are listed in chunks of 256 (blist)
+      for (int32_t s0 = 0; s0 < nsub; s0 += kWin / 16) {
+        const int32_t sn = min(nsub - s0, kWin / 16);
+        qwave_sync();
         {
-          uint32_t wo = (uint32_t)((x << kWinB) + r0);
-          asm volatile("" : "+v"(wo));
-          auto addimp = [&](const uint4 v) {
-            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-              acc[2 * u] += __builtin_amdgcn_perm(0u, w4[u], 0x0C010C00u);
-              acc[2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
-            }
-          };
-          for (uint64_t mh = hm; mh;) {
-            const int j0 = (int)__builtin_ctzll(mh);
-            mh &= mh - 1;
-            const uint4 v0 = ld_g16(uni_ptr(a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j0) * a.hstride), wo);
-            if (mh) {
-              const int j1 = (int)__builtin_ctzll(mh);
-              mh &= mh - 1;
-              const uint4 v1 = ld_g16(uni_ptr(a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j1) * a.hstride), wo);
-              addimp(v0);
-              addimp(v1);
+          int32_t o = sincl - sl - s0;
+          for (uint32_t m = smk; m; m &= m - 1, o++)
+            if (o >= 0 && o < sn) blist[o] = (uint16_t)(16 * lane + __builtin_ctz(m));
+        }
+        qwave_sync();
+        for (int32_t e0 = 0; e0 < sn; e0 += 64) {
+          const bool hs = e0 + lane < sn;
+          const int sid = hs ? (int)blist[e0 + lane] : 0;  // sub-block in the window
+          const int bk = sid >> 2, sj = sid & 3;
+          const int r0 = sid << 2;  // its first document in the window
+          uint32_t acc0 = bias2, acc1 = bias2;  // documents r0, r0 + 1 | r0 + 2, r0 + 3
+          if (hs && total > 0) {
+            const uint32_t bw = bsum[bk];
+            if (unl) {
+              if (bw >> 31) {  // its block's slot: exact sums
+                const uint32_t *my = slot_of((int)(bw & 0xFFu)) + 2 * sj;
+                acc0 += my[0];
+                acc1 += my[1];
+              } else {  // past 64 blocks: the block's sum bounds each document
+                const uint32_t bsc = wide_nl ? 0x4000u : min(bw & 0xFFFFu, 0x4000u);
+                acc0 += bsc | (bsc << 16);
+                acc1 += bsc | (bsc << 16);
+              }
             } else {
-              addimp(v0);
-            }
-          }
-        }
-#else
-        for (uint64_t mh = hm; mh;) {
-          uint4 v[SME_QIMPG];
-#pragma unroll
-          for (int g = 0; g < SME_QIMPG; g++) {
-            v[g] = make_uint4(0, 0, 0, 0);
-            if (mh) {
-              const int j = (int)__builtin_ctzll(mh);
-              mh &= mh - 1;
-              if (hb)
-                v[g] = *reinterpret_cast<const uint4 *>(a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride +
-                                                       (x << kWinB) + r0);
-            }
-          }
-#pragma unroll
-          for (int g = 0; g < SME_QIMPG; g++) {
-            const uint32_t w4[4] = {v[g].x, v[g].y, v[g].z, v[g].w};
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-              acc[2 * u] += __builtin_amdgcn_perm(0u, w4[u], 0x0C010C00u);
-              acc[2 * u + 1] += __builtin_amdgcn_perm(0u, w4[u], 0x0C030C02u);
-            }
-          }
-        }
-#endif
-        uint32_t cm = 0;  // documents of the block over the gate
-        if (hb) {
-          // biased accumulators: bit 15 of a half is set exactly when A(d) >= gate
-          uint32_t hi = 0;
-#pragma unroll
-          for (int i = 0; i < 8; i++) hi |= (acc[i] & 0x80008000u) >> (15 - 2 * i);
-          cm = (hi & 0x5555u) | ((hi >> 15) & 0xAAAAu);
-        }
-        // candidates listed in LDS, scored one per lane
-        const int32_t cl = __popc(cm);
-        const int32_t cincl = wave_incl_sum(cl);
-        const int32_t ncand = (QW_EXPER & 2) ? 0 : __builtin_amdgcn_readlane(cincl, 63);
-        if (QW_STATS && lane == 0) atomicAdd(QW_STATS + 4, (unsigned long long)ncand);
-        for (int32_t k0 = 0; k0 < ncand; k0 += kCList) {
-          const int32_t kn = min(ncand - k0, kCList);
-          qwave_sync();
-          {
-            int32_t o = cincl - cl - k0;
-            for (uint32_t m = cm; m; m &= m - 1, o++)
-              if (o >= 0 && o < kn) clist[o] = (uint16_t)(r0 + __builtin_ctz(m));
-          }
-          qwave_sync();
-          for (int32_t c0 = 0; c0 < kn; c0 += 64) {
-            double S = 0.0;
-            uint64_t key = kNoKey;
-            bool keep = false;
-            if (c0 + lane < kn) {
-              const int r = (int)clist[c0 + lane];
-              const int32_t d = (int32_t)(wbase + r);
-              uint32_t tie = 0xFFFFFFFFu;
-              // the first 8 heavy terms' tf bytes first, their loads in flight
-              // together (the ordered sum below would wait on each in turn)
-              uint64_t hb = 0;
-              {
-                uint64_t mh = hm;
-                uint32_t fb[8];
-#pragma unroll
-                for (int c = 0; c < SME_QFB; c++) {
-                  fb[c] = 0;
-                  if (mh) {
-                    const int j = (int)__builtin_ctzll(mh);
-                    mh &= mh - 1;
-                    fb[c] = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
-                  }
+              const uint32_t bs = bw & 0xFFFFu, bn = bw >> 16;
+              if (bs != 0 && bn <= 2) {  // the block's inline entries in this sub-block
+                for (uint32_t k2 = 0; k2 < bn; k2++) {
+                  const uint32_t ent = bent[2 * bk + k2];
+                  const int dr = (int)(ent & 15u) - (sj << 2);
+                  const uint32_t add = (ent >> 4) << ((dr & 1) << 4);
+                  acc0 += (dr == 0 || dr == 1) ? add : 0u;
+                  acc1 += (dr == 2 || dr == 3) ? add : 0u;
                 }
-#pragma unroll
-                for (int c = 0; c < SME_QFB; c++) hb |= (uint64_t)fb[c] << (8 * c);
-              }
-              int hseen = 0;
-              for (uint64_t m = amask; m; m &= m - 1) {
-                const int j = (int)__builtin_ctzll(m);
-                int f = 0;
-                if ((hm >> j) & 1) {
-                  if (hseen < SME_QFB) {
-                    f = (int)(hb & 0xFFu);
-                    hb >>= 8;
-                  } else {
-                    f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
-                  }
-                  hseen++;
-                } else if (listed) {
-                  const int lo0 = __builtin_amdgcn_readlane(prej, j), hi0 = lo0 + __builtin_amdgcn_readlane(cj, j);
-                  int lo = lo0, hi = hi0;
-                  while (lo < hi) {  // the term's entries are docno-ascending
-                    const int mid = (lo + hi) >> 1;
-                    if ((int)(slist[mid] & 0xFFFu) < r) lo = mid + 1;
-                    else hi = mid;
-                  }
-                  if (lo < hi0 && (int)(slist[lo] & 0xFFFu) == r) {
-                    f = (int)(slist[lo] >> 20);
-                    if (f == 0xFFF) f = -1;  // tf >= 4095: read it from the postings
-                  }
-                } else {
-                  f = -1;
-                }
-                if (f < 0) {  // global binary search over the term's postings in the window
-                  const int64_t base = rl64(D.mb, j);
-                  int64_t lo = base + __builtin_amdgcn_readlane(mc, j);
-                  const int64_t e = base + __builtin_amdgcn_readlane(me, j);
-                  int64_t hi = e;
+              } else if (bs != 0) {
+                // per sparse term, its listed entries from the first with r >= r0 while r < r0 + 4
+                for (uint64_t m = sm; m; m &= m - 1) {
+                  const int j = (int)__builtin_ctzll(m);
+                  int lo = __builtin_amdgcn_readlane(prej, j);
+                  const int hi0 = lo + __builtin_amdgcn_readlane(cj, j);
+                  int hi = hi0;
                   while (lo < hi) {
-                    const int64_t mid = (lo + hi) >> 1;
-                    if (a.docno[mid] < d) lo = mid + 1;
+                    const int mid = (lo + hi) >> 1;
+                    if ((int)(slist[mid] & 0xFFFu) < r0) lo = mid + 1;
                     else hi = mid;
                   }
-                  f = (lo < e && a.docno[lo] == d) ? a.tf[lo] : 0;
-                }
-                if (f != 0) {
-                  S = __dadd_rn(S, __dmul_rn(f < kWinLut ? s_lut[f] : a.lut[f], rld(D.idf, j)));
-                  if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f, a.reftie);
+                  for (; lo < hi0; lo++) {
+                    const uint32_t ent = slist[lo];
+                    const int dr = (int)(ent & 0xFFFu) - r0;
+                    if (dr >= 4) break;
+                    const uint32_t add = ((ent >> 12) & 0xFFu) << ((dr & 1) << 4);
+                    acc0 += dr < 2 ? add : 0u;
+                    acc1 += dr < 2 ? 0u : add;
+                  }
                 }
               }
-              key = doc_key(a.reftie ? tie : 0u, d);
-              keep = S > th0 || (S == th0 && key <= thk);  // th0 < 0 (no seed): every touched document
             }
-            const uint64_t km = (uint64_t)__ballot(keep);
-            if (QW_STATS && lane == 0) atomicAdd(QW_STATS + 5, (unsigned long long)__popcll(km));
-            if (km) {
-              unsigned int base = 0;
-              if (lane == 0) base = atomicAdd(&a.ccnt[P.q], (unsigned int)__popcll(km));
-              base = (unsigned int)__shfl((int)base, 0, 64);
-              if (keep) {
-                const unsigned int idx = base + lane_prefix(km);
-                if (idx < (unsigned int)a.cap) {
-                  a.cs[(int64_t)P.q * a.cap + idx] = S;
-                  a.ck[(int64_t)P.q * a.cap + idx] = key;
+          }
+          {  // heavy impacts: one dword (four documents) per term, four loads in flight
+            const int64_t io = (x << kWinB) + r0;
+            for (uint64_t mh = hm; mh;) {
+              uint32_t wq[4];
+#pragma unroll
+              for (int g = 0; g < 4; g++) {
+                wq[g] = 0;
+                if (mh) {
+                  const int j = (int)__builtin_ctzll(mh);
+                  mh &= mh - 1;
+                  if (hs)
+                    wq[g] = *reinterpret_cast<const uint32_t *>(
+                        a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + io);
+                }
+              }
+#pragma unroll
+              for (int g = 0; g < 4; g++) {
+                acc0 += __builtin_amdgcn_perm(0u, wq[g], 0x0C010C00u);
+                acc1 += __builtin_amdgcn_perm(0u, wq[g], 0x0C030C02u);
+              }
+            }
+          }
+          // documents of the sub-block over the gate (bit 15 of each biased half)
+          const uint32_t cm = hs ? (((acc0 >> 15) & 1u) | ((acc0 >> 30) & 2u) | ((acc1 >> 13) & 4u) | ((acc1 >> 28) & 8u))
+                                 : 0u;
+          // candidates listed in LDS, scored one per lane
+          const int32_t cl = __popc(cm);
+          const int32_t cincl = wave_incl_sum(cl);
+          const int32_t ncand = (QW_EXPER & 2) ? 0 : __builtin_amdgcn_readlane(cincl, 63);
+          if (QW_STATS && lane == 0) atomicAdd(QW_STATS + 4, (unsigned long long)ncand);
+          for (int32_t k0 = 0; k0 < ncand; k0 += kCList) {
+            const int32_t kn = min(ncand - k0, kCList);
+            qwave_sync();
+            {
+              int32_t o = cincl - cl - k0;
+              for (uint32_t m = cm; m; m &= m - 1, o++)
+                if (o >= 0 && o < kn) clist[o] = (uint16_t)(r0 + __builtin_ctz(m));
+            }
+            qwave_sync();
+            for (int32_t c0 = 0; c0 < kn; c0 += 64) {
+              double S = 0.0;
+              uint64_t key = kNoKey;
+              bool keep = false;
+              if (c0 + lane < kn) {
+                const int r = (int)clist[c0 + lane];
+                const int32_t d = (int32_t)(wbase + r);
+                uint32_t tie = 0xFFFFFFFFu;
+                // the first 8 heavy terms' tf bytes first, their loads in flight
+                // together (the ordered sum below would wait on each in turn)
+                uint64_t hb8 = 0;
+                {
+                  uint64_t mh = hm;
+                  uint32_t fb[8];
+#pragma unroll
+                  for (int c = 0; c < SME_QFB; c++) {
+                    fb[c] = 0;
+                    if (mh) {
+                      const int j = (int)__builtin_ctzll(mh);
+                      mh &= mh - 1;
+                      fb[c] = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
+                    }
+                  }
+#pragma unroll
+                  for (int c = 0; c < SME_QFB; c++) hb8 |= (uint64_t)fb[c] << (8 * c);
+                }
+                int hseen = 0;
+                for (uint64_t m = amask; m; m &= m - 1) {
+                  const int j = (int)__builtin_ctzll(m);
+                  int f = 0;
+                  if ((hm >> j) & 1) {
+                    if (hseen < SME_QFB) {
+                      f = (int)(hb8 & 0xFFu);
+                      hb8 >>= 8;
+                    } else {
+                      f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
+                    }
+                    hseen++;
+                  } else if (listed) {
+                    const int lo0 = __builtin_amdgcn_readlane(prej, j), hi0 = lo0 + __builtin_amdgcn_readlane(cj, j);
+                    int lo = lo0, hi = hi0;
+                    while (lo < hi) {  // the term's entries are docno-ascending
+                      const int mid = (lo + hi) >> 1;
+                      if ((int)(slist[mid] & 0xFFFu) < r) lo = mid + 1;
+                      else hi = mid;
+                    }
+                    if (lo < hi0 && (int)(slist[lo] & 0xFFFu) == r) {
+                      f = (int)(slist[lo] >> 20);
+                      if (f == 0xFFF) f = -1;  // tf >= 4095: read it from the postings
+                    }
+                  } else {
+                    f = -1;
+                  }
+                  if (f < 0) {  // global binary search over the term's postings in the window
+                    const int64_t base = rl64(D.mb, j);
+                    int64_t lo = base + __builtin_amdgcn_readlane(mc, j);
+                    const int64_t e = base + __builtin_amdgcn_readlane(me, j);
+                    int64_t hi = e;
+                    while (lo < hi) {
+                      const int64_t mid = (lo + hi) >> 1;
+                      if (a.docno[mid] < d) lo = mid + 1;
+                      else hi = mid;
+                    }
+                    f = (lo < e && a.docno[lo] == d) ? a.tf[lo] : 0;
+                  }
+                  if (f != 0) {
+                    S = __dadd_rn(S, __dmul_rn(f < kWinLut ? s_lut[f] : a.lut[f], rld(D.idf, j)));
+                    if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f, a.reftie);
+                  }
+                }
+                key = doc_key(a.reftie ? tie : 0u, d);
+                keep = S > th0 || (S == th0 && key <= thk);  // th0 < 0 (no seed): every touched document
+              }
+              const uint64_t km = (uint64_t)__ballot(keep);
+              if (QW_STATS && lane == 0) atomicAdd(QW_STATS + 5, (unsigned long long)__popcll(km));
+              if (km) {
+                unsigned int base = 0;
+                if (lane == 0) base = atomicAdd(&a.ccnt[P.q], (unsigned int)__popcll(km));
+                base = (unsigned int)__shfl((int)base, 0, 64);
+                if (keep) {
+                  const unsigned int idx = base + lane_prefix(km);
+                  if (idx < (unsigned int)a.cap) {
+                    a.cs[(int64_t)P.q * a.cap + idx] = S;
+                    a.ck[(int64_t)P.q * a.cap + idx] = key;
+                  }
                 }
               }
             }
@@ -2109,32 +2076,6 @@ __global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const i
     dst[threadIdx.x] = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
-// impact bound rows of the 16-document blocks: q(block's largest tf) (q is
-// monotone in tf, so this is the largest impact in the block); one workgroup per row
-__global__ __launch_bounds__(256) void k_heavy_bmq(const uint8_t *bm16, const int32_t *hterm, int64_t H, int64_t stride,
-                                                   const double *lut, int max_tf, const double *idf, double alpha,
-                                                   uint8_t *bmq) {
-  __shared__ uint8_t ql[256];
-  for (int64_t row = blockIdx.x; row < H; row += gridDim.x) {
-    const double wi = idf[hterm[row]];
-    __syncthreads();
-    const int f = threadIdx.x;
-    ql[f] = (uint8_t)(f == 0 ? 0u : f <= max_tf ? impact(lut[f], wi, alpha) : 255u);
-    __syncthreads();
-    const uint4 *src = reinterpret_cast<const uint4 *>(bm16 + row * stride);
-    uint4 *dst = reinterpret_cast<uint4 *>(bmq + row * stride);
-    for (int64_t i = threadIdx.x; i < (stride >> 4); i += blockDim.x) {
-      const uint4 v = src[i];
-      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-      uint32_t o[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++)
-        o[u] = (uint32_t)ql[w4[u] & 0xFF] | ((uint32_t)ql[(w4[u] >> 8) & 0xFF] << 8) |
-               ((uint32_t)ql[(w4[u] >> 16) & 0xFF] << 16) | ((uint32_t)ql[w4[u] >> 24] << 24);
-      dst[i] = make_uint4(o[0], o[1], o[2], o[3]);
-    }
-  }
-}
 // k_query_win's sparse posting words (index-resident, like the impact rows):
 // (docno - dmin) mod 4096 = the posting's place in its 4096-document window, its
 // impact q(tf) at the index's scale and its tf (4095 = "4095 or more"), so the
@@ -2228,7 +2169,7 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     // list; the c4 shard's ~2,300 heavy terms need ~30 GB of rows)
     size_t fr = 0, tot = 0;
     SME_HIP(hipMemGetInfo(&fr, &tot));
-    const double per_row = 2.0 * (double)stride + 2.0 * (double)(T << 6) + (double)T;
+    const double per_row = 2.0 * (double)stride + (double)(T << 6) + (double)T + (double)(T << 8);
     const int64_t cap = (int64_t)(std::min<double>((double)fr / 4.0, 64e9) / per_row);
     const int64_t H = std::min<int64_t>(nh, cap);
     int32_t *hrow_of = ix->d_hrow_of.as<int32_t>(V);
@@ -2241,7 +2182,7 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
       excl_scan(hdf, hpre, (int64_t)(H + 1), cx->ws[23], st);
       uint8_t *buf = ix->d_heavy.as<uint8_t>((size_t)H * (size_t)per_row + 128);
       uint8_t *tfrow = buf, *imp = buf + H * stride, *bm16 = imp + H * stride, *bm1k = bm16 + H * (T << 6);
-      uint8_t *bmq = bm1k + H * T + 64 - ((H * T) & 15);  // 16-byte aligned
+      uint8_t *sbq = bm1k + H * T + 64 - ((H * T) & 15);  // 16-byte aligned
       SME_HIP(hipMemsetAsync(tfrow, 0, (size_t)(H * stride), st));
       hipLaunchKernelGGL(k_heavy_fill, dim3(16384), dim3(256), 0, st, hpre, H, hterm, off,
                          (const int32_t *)ix->d_docno_d.p, (const int32_t *)ix->d_tf_d.p, ix->dmin, stride, tfrow);
@@ -2253,11 +2194,11 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
       hipLaunchKernelGGL(k_heavy_imp, dim3((unsigned)std::min<int64_t>(H * (stride >> 12), 1 << 16)), dim3(256), 0, st,
                          tfrow, hterm, H, stride, (const double *)ix->d_lut.p, ix->max_tf,
                          (const double *)ix->d_idf.p, ix->q_alpha, imp);
-      hipLaunchKernelGGL(k_heavy_bmq, dim3((unsigned)std::min<int64_t>(H, 1 << 16)), dim3(256), 0, st, bm16, hterm, H,
-                         T << 6, (const double *)ix->d_lut.p, ix->max_tf, (const double *)ix->d_idf.p, ix->q_alpha, bmq);
+      hipLaunchKernelGGL(k_heavy_sbq, dim3((unsigned)std::min<int64_t>((n16 + 255) / 256, 1 << 16)), dim3(256), 0, st,
+                         (const uint4 *)imp, n16, reinterpret_cast<uint32_t *>(sbq));
       SME_CHECK_LAUNCH();
       ix->q_imp = imp;
-      ix->q_bmq = bmq;
+      ix->q_sbq = sbq;
       ix->q_tfrow = tfrow;
       ix->q_bm16 = bm16;
       ix->q_bm1k = bm1k;
@@ -2337,10 +2278,10 @@ struct QTimes {  // the per-call query timings of the context, summed over sub-b
 // are few, so its own tables fit (a single query of <= 64 terms always does).
 static void query_subset(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, const int32_t *h_qlist,
                          int n, int k, int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie,
-                         hipStream_t st);
+                         hipStream_t st, int tie_bits);
 
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k, int32_t *d_out_docno,
-                double *d_out_score, uint32_t *d_out_tie, hipStream_t st) {
+                double *d_out_score, uint32_t *d_out_tie, hipStream_t st, int tie_bits) {
   if (k < 1) throw Error(SME_EINVAL, "k must be >= 1");
   // k <= 448 on the window / block-max kernels; larger k up to 1792 on the streaming
   // kernel's LDS candidate list
@@ -2353,14 +2294,19 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   SME_HIP(hipMemsetAsync(err, 0, 4 * sizeof(int), st));
   int h_mx = 0;  // the batch's longest query (terms)
   // reference tie order: ref_tie keys hold the token index above tb tf bits, 24
-  // for queries of <= 256 terms, 22 for longer ones (the batch decides, so doc
-  // shards answering one batch build the same keys)
+  // for queries of <= 256 terms, 22 for longer ones (the top-level batch decides
+  // and its nested calls inherit it, so doc shards answering one batch build the
+  // same keys whatever the splits each shard's memory makes)
   int reftie = 0;
   if (cx->cfg.tiebreak == SME_TIE_REFERENCE) {
-    hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
-    SME_HIP(hipMemcpyAsync(&h_mx, err + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-    SME_HIP(hipStreamSynchronize(st));
-    reftie = h_mx > 256 ? 22 : 24;
+    if (tie_bits > 0) {
+      reftie = tie_bits;
+    } else {
+      hipLaunchKernelGGL(k_max_qlen, dim3(std::min((nq + 255) / 256, 1024)), dim3(256), 0, st, d_qoff, nq, err + 1);
+      SME_HIP(hipMemcpyAsync(&h_mx, err + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+      SME_HIP(hipStreamSynchronize(st));
+      reftie = h_mx > 256 ? 22 : 24;
+    }
     if ((int64_t)ix->max_tf >= (int64_t(1) << reftie))
       throw Error(SME_ELIMIT, reftie == 24 ? "reference tie order with a term frequency >= 2^24"
                                            : "reference tie order, a query of > 256 terms and a term frequency >= 2^22");
@@ -2425,10 +2371,10 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
         SME_HIP(hipEventDestroy(ep));
         QTimes acc;
         const int h = nq / 2;
-        query_topk(ix, d_terms, d_qoff, h, k, d_out_docno, d_out_score, d_out_tie, st);
+        query_topk(ix, d_terms, d_qoff, h, k, d_out_docno, d_out_score, d_out_tie, st, reftie);
         acc.add(cx);
         query_topk(ix, d_terms, d_qoff + h, nq - h, k, d_out_docno + (int64_t)h * k, d_out_score + (int64_t)h * k,
-                   d_out_tie ? d_out_tie + (int64_t)h * k : nullptr, st);
+                   d_out_tie ? d_out_tie + (int64_t)h * k : nullptr, st, reftie);
         acc.add(cx);
         acc.store(cx);
         cx->last_query_split = true;
@@ -2634,7 +2580,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     wa.nrows = nrows_b;
     wa.qlut = qlut;
     wa.imp = ix->q_imp;
-    wa.bmq = ix->q_bmq;
+    wa.sbq = ix->q_sbq;
     wa.tfrow = ix->q_tfrow;
     wa.hstride = T << kQB;
     wa.dmin = ix->dmin;
@@ -2797,14 +2743,14 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
         // here and added to this call's below (with the split flag)
         subset_ran = true;
         if (n_round < nq) {
-          query_subset(ix, d_terms, d_qoff, nq, hl.data(), n_round, k, d_out_docno, d_out_score, d_out_tie, st);
+          query_subset(ix, d_terms, d_qoff, nq, hl.data(), n_round, k, d_out_docno, d_out_score, d_out_tie, st, reftie);
           sub_times.add(cx);
         } else {  // every query of the batch: two compact halves (each recursion has fewer queries)
           const int h = n_round / 2;
-          query_subset(ix, d_terms, d_qoff, nq, hl.data(), h, k, d_out_docno, d_out_score, d_out_tie, st);
+          query_subset(ix, d_terms, d_qoff, nq, hl.data(), h, k, d_out_docno, d_out_score, d_out_tie, st, reftie);
           sub_times.add(cx);
           query_subset(ix, d_terms, d_qoff, nq, hl.data() + h, n_round - h, k, d_out_docno, d_out_score, d_out_tie,
-                       st);
+                       st, reftie);
           sub_times.add(cx);
         }
       }
@@ -2871,7 +2817,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     uint64_t h[8];
     SME_HIP(hipMemcpy(h, qstats, sizeof h, hipMemcpyDeviceToHost));
     if (win)
-      fprintf(stderr, "SME_QSTATS pairs=%llu sparse_postings=%llu blocks_over_gate=%llu heavy_terms=%llu "
+      fprintf(stderr, "SME_QSTATS pairs=%llu sparse_postings=%llu subblocks_over_gate=%llu heavy_terms=%llu "
               "docs_over_gate=%llu kept=%llu\n", (unsigned long long)h[0], (unsigned long long)h[1],
               (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[4], (unsigned long long)h[5]);
     else
@@ -2883,7 +2829,7 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
 
 static void query_subset(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, const int32_t *h_qlist,
                          int n, int k, int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie,
-                         hipStream_t st) {
+                         hipStream_t st, int tie_bits) {
   const std::vector<int32_t> ql(h_qlist, h_qlist + n);
   std::vector<int64_t> qo((size_t)nq + 1);
   SME_HIP(hipMemcpyAsync(qo.data(), d_qoff, (nq + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -2909,7 +2855,7 @@ static void query_subset(sme_index *ix, const int32_t *d_terms, const int64_t *d
     SME_HIP(hipMemcpyAsync(dt, sterms.data(), sterms.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
   SME_HIP(hipMemcpyAsync(doff, soff.data(), soff.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
   SME_HIP(hipMemcpyAsync(dl, ql.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st));
-  query_topk(ix, dt, doff, n, k, od, os, ot, st);  // splits by itself until a subset's tables fit
+  query_topk(ix, dt, doff, n, k, od, os, ot, st, tie_bits);  // splits by itself until a subset's tables fit
   hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)std::min<int64_t>(((int64_t)n * k + 255) / 256, 4096)), dim3(256),
                      0, st, dl, n, k, od, os, ot, d_out_docno, d_out_score, d_out_tie);
   SME_CHECK_LAUNCH();

@@ -22,8 +22,17 @@ the small global statistics and the query results:
                    shards: all_to_all of per-owner term/postings blobs, per-term
                    reducer merge on the owner (sme_merge_pieces)
   merge_topk_owner per-shard top-k -> global top-k of the queries a rank owns
-                   (query-owner all_to_all of Q x k x (4 + 8) B, score desc,
-                   docno asc); merge_topk also all_gathers the merged slices
+                   (query-owner all_to_all of Q x k x (4 + 8) B, then the W lists
+                   of each owned query merged by score desc, tie word asc, docno
+                   asc in libsme, sme_topk_merge_rows); merge_topk also
+                   all_gathers the merged slices
+  docno_duplicates docids held by two shards (owner all_to_all of (docno, rank)
+                   rows grouped by sme_df_owner_pack, counted by
+                   sme_count_shared_keys)
+
+No torch sort / unique runs on these product paths: the grouping, sums, merges
+and counts are libsme kernels (DeviceDfOps); the CPU tests pass a numpy / torch
+restatement of the same local steps (tests/test_dist.py HostDfOps).
 
 Exactness: with docids unique across shards (every synthetic corpus), the sharded
 result equals the single-index result bit for bit: a document's score only uses its
@@ -142,14 +151,30 @@ def global_df(local_df, l2g, n_global_terms, group=None):
     return g[torch.from_numpy(l2g).to(dev)] if len(l2g) else g[:0]
 
 
-class DeviceDfOps:
-    """The df exchange's local steps on the device, in libsme (sme_dfx.hip):
-    owner grouping (counting scatter), owner sums (fingerprint hash table) and
-    the return gather.  Tensors are CUDA tensors; libsme runs them on the
-    context's own stream, synchronized before torch reads the results."""
+_OWNER_CTX = {}
 
-    def __init__(self, ctx):
-        self.ctx = ctx
+
+def _owner_ctx():
+    """A libsme context on the current device for the owner-side kernels of
+    callers that hold no index (merge_topk_owner, docno_duplicates)."""
+    sme = importlib.import_module(__package__)
+    d = torch.cuda.current_device()
+    if d not in _OWNER_CTX:
+        _OWNER_CTX[d] = sme.Context(device=d)
+    return _OWNER_CTX[d]
+
+
+class DeviceDfOps:
+    """The multi-GPU path's local steps on the device, in libsme: the df
+    exchange's owner grouping (counting scatter), owner sums (fingerprint hash
+    table) and return gather (sme_dfx.hip), and the query owner's merge of the
+    shards' top-k rows and the shared-docid count (sme_owner.hip).  Tensors are
+    CUDA tensors (merge_rows / count_shared move theirs there and back); libsme
+    runs them on the context's own stream, synchronized before torch reads the
+    results."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx if ctx is not None else _owner_ctx()
 
     def pack(self, fp, df, world):
         n = int(fp.shape[0])
@@ -178,6 +203,33 @@ class DeviceDfOps:
         if n:
             self.ctx.df_owner_unpack(ret.data_ptr(), pos.data_ptr(), n, out.data_ptr())
         return out[:n]
+
+    def merge_rows(self, s, d, k, t=None):
+        """rows of candidates (score f64, docno i32, tie u32 as int64 or None)
+        -> (docno int32, score f64, tie int64) [rows, k] (sme_topk_merge_rows),
+        on the inputs' device."""
+        src = s.device
+        dev = torch.device("cuda", torch.cuda.current_device())
+        rows, m = int(s.shape[0]), int(s.shape[1])
+        s_ = s.to(dev, torch.float64).contiguous()
+        d_ = d.to(dev, torch.int32).contiguous()
+        t_ = t.to(dev, torch.int64).to(torch.int32).contiguous() if t is not None else None  # (low 32 bits)
+        od = torch.empty((max(rows, 1), k), dtype=torch.int32, device=dev)
+        os_ = torch.empty((max(rows, 1), k), dtype=torch.float64, device=dev)
+        ot = torch.empty((max(rows, 1), k), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        if rows:
+            self.ctx.topk_merge_rows(s_.data_ptr(), d_.data_ptr(), t_.data_ptr() if t_ is not None else 0, rows, m, k,
+                                     od.data_ptr(), os_.data_ptr(), ot.data_ptr())
+        return od[:rows].to(src), os_[:rows].to(src), (ot[:rows].to(torch.int64) & 0xFFFFFFFF).to(src)
+
+    def count_shared(self, rows):
+        """(key, source rank) int64 [n, 2] rows -> distinct keys from two or more
+        ranks (sme_count_shared_keys)."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        r = rows.to(dev).contiguous()
+        torch.cuda.synchronize()
+        return self.ctx.count_shared_keys(r.data_ptr(), int(r.shape[0])) if r.shape[0] else 0
 
 
 def df_exchange(fp, df, group=None, timings=None, ops=None):
@@ -306,38 +358,42 @@ def reference_partitions(ix, group=None, timings=None):
     return merged, [p for p in range(R) if p % world == rank]
 
 
-def docno_duplicates(docnos, group=None):
+def docno_duplicates(docnos, group=None, ops=None):
     """Number of distinct docnos that more than one shard holds (docnos: this
-    shard's record docnos, an int64 tensor on the collective's device).  Disjoint
-    [min, max] ranges answer 0 at once (all_gather of 16 B); otherwise each rank
-    sends its distinct docnos to owner docno mod W, and owners count the values
-    that arrive from more than one shard.  A docid duplicated across shards is
-    one posting with summed tf in the reference's single reducer
-    (TermKGramDocIndexer.java:202-210); per-shard scoring would keep two."""
-    world = dist.get_world_size(group)
-    dev = docnos.device
+    shard's record docnos, an int64 tensor).  Disjoint [min, max] ranges answer
+    0 at once (all_gather of 16 B); otherwise every (docno, rank) row goes to the
+    docno's owner rank (grouped by `ops.pack`, one all_to_all) and each owner
+    counts the docnos that arrive from two or more ranks (`ops.count_shared`),
+    summed over the owners.  A docid duplicated across shards is one posting
+    with summed tf in the reference's single reducer
+    (TermKGramDocIndexer.java:202-210); per-shard scoring would keep two.
+    `ops`: DeviceDfOps (libsme, the default) or the CPU tests' restatement."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    cdev = _dev(group)
     n = int(docnos.shape[0])
     big = 1 << 62
-    mm = torch.tensor([int(docnos.min()) if n else big, int(docnos.max()) if n else -big], dtype=torch.int64, device=dev)
+    mm = torch.tensor([int(docnos.min()) if n else big, int(docnos.max()) if n else -big], dtype=torch.int64, device=cdev)
     alls = [torch.empty_like(mm) for _ in range(world)]
     dist.all_gather(alls, mm, group=group)
     rng = sorted((int(a[0]), int(a[1])) for a in alls if int(a[0]) <= int(a[1]))
     if all(rng[i][1] < rng[i + 1][0] for i in range(len(rng) - 1)):
         return 0
-    u = torch.unique(docnos) if n else docnos
-    owner = torch.remainder(u, world)
-    order = torch.argsort(owner, stable=True)
-    u = u[order].contiguous()
-    cnt = torch.bincount(owner, minlength=world).to(torch.int64)
-    rcnt = torch.empty_like(cnt)
-    dist.all_to_all_single(rcnt, cnt, group=group)
-    recv = torch.empty(int(rcnt.sum()), dtype=torch.int64, device=dev)
-    dist.all_to_all_single(recv, u, rcnt.tolist(), cnt.tolist(), group=group)
-    if recv.numel():
-        _, c = torch.unique(recv, return_counts=True)
-        dup = torch.tensor([int((c > 1).sum())], dtype=torch.int64, device=dev)
-    else:
-        dup = torch.zeros(1, dtype=torch.int64, device=dev)
+    if ops is None:
+        ops = DeviceDfOps()
+    # keys: docnos as zero-extended 32-bit values (never the table's empty marker)
+    dd = docnos.to(torch.int64) & 0xFFFFFFFF
+    rows = torch.stack([dd, torch.full_like(dd, rank)], 1).contiguous()
+    if hasattr(ops, "ctx"):
+        rows = rows.to("cuda")
+    send, _, _, cs = ops.pack(rows, torch.zeros_like(dd).to(rows.device), world)
+    counts = torch.tensor(cs, dtype=torch.int64, device=cdev)
+    rcounts = torch.empty_like(counts)
+    dist.all_to_all_single(rcounts, counts, group=group)
+    rc = rcounts.tolist()
+    recv = torch.empty((int(sum(rc)), 2), dtype=torch.int64, device=cdev)
+    dist.all_to_all_single(recv.view(-1), send.to(cdev).contiguous().view(-1), [2 * c for c in rc],
+                           [2 * c for c in cs], group=group)
+    dup = torch.tensor([int(ops.count_shared(recv))], dtype=torch.int64, device=cdev)
     dist.all_reduce(dup, group=group)
     return int(dup.item())
 
@@ -358,36 +414,17 @@ def owner_bounds(nq, world):
     return [nq * r // world for r in range(world + 1)]
 
 
-def _merge_rows(s, d, k, t=None):
+def _merge_rows(s, d, k, t=None, ops=None):
     """rows of candidate (score, docno[, tie]) lists -> the best k per row, (score
     desc, tie asc, docno asc); docno -1 pads.  The tie word (sme_query_topk_tie)
     is 0 under SME_TIE_DOCNO and the first-encounter rank under SME_TIE_REFERENCE,
     a property of the document and the query alone, so shards merge into the
-    single index's order."""
-    d = d.to(torch.int64)
-    # docno -1 is padding; other negative docnos are real results (docids missing
-    # from the mapping: binarySearch's -(insertion point) - 1 <= -2, T14)
-    valid = d != -1
-    s = torch.where(valid, s, torch.full_like(s, -float("inf")))
-    # one int64 key: tie (32 bits) above the docno (+2^31, 32 bits); pads last
-    key = d + (1 << 31)
-    if t is not None:
-        key = key + (t.to(torch.int64) & 0xFFFFFFFF) * (1 << 32)
-    key = torch.where(valid, key, torch.full_like(key, (1 << 63) - 1))
-    # stable sort by key, then stable sort by -score
-    i1 = torch.argsort(key, dim=1, stable=True)
-    s1, k1 = torch.gather(s, 1, i1), torch.gather(key, 1, i1)
-    i2 = torch.argsort(-s1, dim=1, stable=True)[:, :k]
-    out_k, out_s = torch.gather(k1, 1, i2), torch.gather(s1, 1, i2)
-    pad = out_k == (1 << 63) - 1
-    out_d = (out_k & 0xFFFFFFFF) - (1 << 31)
-    out_t = (out_k >> 32) & 0xFFFFFFFF
-    return (torch.where(pad, torch.full_like(out_d, -1), out_d).to(torch.int32),
-            torch.where(pad, torch.zeros_like(out_s), out_s),
-            torch.where(pad, torch.full_like(out_t, 0xFFFFFFFF), out_t))
+    single index's order.  libsme's merge kernel (sme_topk_merge_rows) unless
+    `ops` restates it (CPU tests)."""
+    return (ops if ops is not None else DeviceDfOps()).merge_rows(s, d, k, t)
 
 
-def merge_topk_owner(docno, score, k, group=None, tie=None):
+def merge_topk_owner(docno, score, k, group=None, tie=None, ops=None):
     """Query-owner merge: docno int32 [Q, k] (-1 pads), score float64
     [Q, k] of this shard -> (q0, q1, docno [q1-q0, k], score [q1-q0, k]), the global
     top-k of the queries this rank owns.  One all_to_all moves every shard's lists
@@ -409,16 +446,16 @@ def merge_topk_owner(docno, score, k, group=None, tie=None):
         rt = torch.empty(world * my * k, dtype=torch.int64, device=docno.device)
         dist.all_to_all_single(rt, tie.to(torch.int64).contiguous().reshape(-1), [my * k] * world, ins, group=group)
         t = rt.reshape(world, my, k).permute(1, 0, 2).reshape(my, world * k)
-    md, ms, _ = _merge_rows(s, d, k, t)
+    md, ms, _ = _merge_rows(s, d, k, t, ops)
     return b[r], b[r + 1], md, ms
 
 
-def merge_topk(docno, score, k, group=None, tie=None):
+def merge_topk(docno, score, k, group=None, tie=None, ops=None):
     """Global (docno, score) [Q, k] on every rank: the query-owner merge, then an
     all_gather of the merged slices (Q x k x 12 B, not W x Q x k)."""
     world = dist.get_world_size(group)
     nq = docno.shape[0]
-    q0, q1, md, ms = merge_topk_owner(docno, score, k, group, tie)
+    q0, q1, md, ms = merge_topk_owner(docno, score, k, group, tie, ops)
     b = owner_bounds(nq, world)
     m = max(b[i + 1] - b[i] for i in range(world))
     pd = torch.full((m, k), -1, dtype=md.dtype, device=md.device)

@@ -774,6 +774,41 @@ def test_queries_table_budget(sme, synth, budget, cap):
         assert (dn[q, len(rd):] == -1).all()
 
 
+@pytest.mark.parametrize("long_query", [False, True])
+def test_queries_tie_width_split(sme, synth, long_query):
+    """SME_TIE_REFERENCE under a forced split (query_table_budget 1: down to one
+    query per nested call, then overflow subsets with cand_cap 4): the tie
+    words' tf width is the TOP-LEVEL batch's (22 bits when one of its queries
+    has more than 256 terms, else 24) and the nested calls inherit it, so every
+    tie word equals the unsplit run's -- doc shards merging tie words
+    (dist.merge_topk_owner) never see two widths for one query."""
+    n = 4000
+    c = synth.gen_corpus(n, V=1500, seed=17, len_lo=10, len_hi=40)
+    ix, ref = _check_build(sme, c, synth.docids(n), R=1, tiebreak=1)
+    _, _, _, df = ix.csr()
+    terms, qoff = synth.queries_by_df(df, 40, seed=3, qlen_lo=1, qlen_hi=8)
+    if long_query:
+        rng = np.random.default_rng(2)
+        terms = np.concatenate([terms, rng.integers(0, ix.V, size=300).astype(np.int32)])
+        qoff = np.concatenate([qoff, [qoff[-1] + 300]]).astype(np.int64)
+    k = 10
+    dn0, sc0, t0 = ix.query_topk(terms, qoff, k, with_tie=True)
+    try:
+        ix.ctx.set_option("query_table_budget", 1)
+        ix.ctx.set_option("cand_cap", 4)
+        dn, sc, t = ix.query_topk(terms, qoff, k, with_tie=True)
+    finally:
+        ix.ctx.set_option("query_table_budget", 0)
+        ix.ctx.set_option("cand_cap", 1024)
+    assert np.array_equal(dn, dn0) and np.array_equal(sc.view(np.int64), sc0.view(np.int64))
+    assert np.array_equal(t, t0)
+    # the width is visible in the words: token index j above tb bits of 2^tb - 1 - tf
+    hit = dn0 >= 0
+    tb = 22 if long_query else 24
+    f = ((1 << tb) - 1) - (t0[hit].astype(np.int64) & ((1 << tb) - 1))
+    assert hit.any() and ((f >= 1) & (f < 256)).all()
+
+
 def test_c1_sample_on_device(sme, tmp_path):
     """c1 on the device: the committed 1,000-document sample through
     libsme (R = 10 reducers) -> partition records byte-equal to the oracle's ->
