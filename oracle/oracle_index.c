@@ -675,6 +675,368 @@ static void legacy_merge_sort(docscore *src, docscore *dest, int low, int high, 
   }
 }
 
+/*
+ * JDK 7 Collections.sort over the same comparator: java.util.ComparableTimSort
+ * (OpenJDK 7 GA, the default since Java 7 unless -Djava.util.Arrays.
+ * useLegacyMergeSort=true; not vendored in the reference -- restated from the
+ * published source).  Collections.sort(List) -> Arrays.sort(Object[]) ->
+ * ComparableTimSort.sort: runs (countRunAndMakeAscending, reversed when strictly
+ * descending by compareTo < 0), binary insertion to minRun, the JDK 7 GA
+ * mergeCollapse invariant (before the JDK-8072909 fix), gallopLeft /
+ * gallopRight and mergeLo / mergeHi with MIN_GALLOP 7.  Every test is `< 0`,
+ * `<= 0`, `> 0` or `>= 0` on compareTo exactly as the Java source asks it, so
+ * the broken DocScore comparator (T5) is applied the way the JVM applies it.
+ * A merge that finds the contract violated throws IllegalArgumentException
+ * ("Comparison method violates its general contract!") in Java: returned here
+ * as -1 (the reference's rank() would fail).
+ */
+enum { TS_MIN_MERGE = 32, TS_MIN_GALLOP = 7 };
+typedef struct {
+  docscore *a, *tmp;
+  int tmplen, min_gallop, stack;
+  int base[85], len[85];
+  int err;
+} tsort;
+
+static int ts_cmp(const docscore *x, const docscore *y) { return ds_cmp_ref(x, y); } /* x.compareTo(y) */
+
+static void ts_reverse(docscore *a, int lo, int hi) {
+  hi--;
+  while (lo < hi) {
+    docscore t = a[lo];
+    a[lo++] = a[hi];
+    a[hi--] = t;
+  }
+}
+
+static int ts_count_run(docscore *a, int lo, int hi) {
+  int runHi = lo + 1;
+  if (runHi == hi) return 1;
+  if (ts_cmp(&a[runHi++], &a[lo]) < 0) {
+    while (runHi < hi && ts_cmp(&a[runHi], &a[runHi - 1]) < 0) runHi++;
+    ts_reverse(a, lo, runHi);
+  } else {
+    while (runHi < hi && ts_cmp(&a[runHi], &a[runHi - 1]) >= 0) runHi++;
+  }
+  return runHi - lo;
+}
+
+static void ts_binary_sort(docscore *a, int lo, int hi, int start) {
+  if (start == lo) start++;
+  for (; start < hi; start++) {
+    docscore pivot = a[start];
+    int left = lo, right = start;
+    while (left < right) {
+      int mid = (int)(((unsigned)left + (unsigned)right) >> 1);
+      if (ts_cmp(&pivot, &a[mid]) < 0) right = mid;
+      else left = mid + 1;
+    }
+    memmove(&a[left + 1], &a[left], (size_t)(start - left) * sizeof(docscore));
+    a[left] = pivot;
+  }
+}
+
+static int ts_min_run(int n) {
+  int r = 0;
+  while (n >= TS_MIN_MERGE) {
+    r |= (n & 1);
+    n >>= 1;
+  }
+  return n + r;
+}
+
+static int ts_gallop_left(const docscore *key, const docscore *a, int base, int len, int hint) {
+  int lastOfs = 0, ofs = 1;
+  if (ts_cmp(key, &a[base + hint]) > 0) {
+    int maxOfs = len - hint;
+    while (ofs < maxOfs && ts_cmp(key, &a[base + hint + ofs]) > 0) {
+      lastOfs = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxOfs;
+    }
+    if (ofs > maxOfs) ofs = maxOfs;
+    lastOfs += hint;
+    ofs += hint;
+  } else {
+    int maxOfs = hint + 1;
+    while (ofs < maxOfs && ts_cmp(key, &a[base + hint - ofs]) <= 0) {
+      lastOfs = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxOfs;
+    }
+    if (ofs > maxOfs) ofs = maxOfs;
+    int tmp = lastOfs;
+    lastOfs = hint - ofs;
+    ofs = hint - tmp;
+  }
+  lastOfs++;
+  while (lastOfs < ofs) {
+    int m = lastOfs + (int)((unsigned)(ofs - lastOfs) >> 1);
+    if (ts_cmp(key, &a[base + m]) > 0) lastOfs = m + 1;
+    else ofs = m;
+  }
+  return ofs;
+}
+
+static int ts_gallop_right(const docscore *key, const docscore *a, int base, int len, int hint) {
+  int ofs = 1, lastOfs = 0;
+  if (ts_cmp(key, &a[base + hint]) < 0) {
+    int maxOfs = hint + 1;
+    while (ofs < maxOfs && ts_cmp(key, &a[base + hint - ofs]) < 0) {
+      lastOfs = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxOfs;
+    }
+    if (ofs > maxOfs) ofs = maxOfs;
+    int tmp = lastOfs;
+    lastOfs = hint - ofs;
+    ofs = hint - tmp;
+  } else {
+    int maxOfs = len - hint;
+    while (ofs < maxOfs && ts_cmp(key, &a[base + hint + ofs]) >= 0) {
+      lastOfs = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxOfs;
+    }
+    if (ofs > maxOfs) ofs = maxOfs;
+    lastOfs += hint;
+    ofs += hint;
+  }
+  lastOfs++;
+  while (lastOfs < ofs) {
+    int m = lastOfs + (int)((unsigned)(ofs - lastOfs) >> 1);
+    if (ts_cmp(key, &a[base + m]) < 0) ofs = m;
+    else lastOfs = m + 1;
+  }
+  return ofs;
+}
+
+static docscore *ts_tmp(tsort *t, int n) {
+  if (t->tmplen < n) {
+    free(t->tmp);
+    t->tmplen = n;
+    t->tmp = (docscore *)malloc(sizeof(docscore) * (size_t)n);
+  }
+  return t->tmp;
+}
+
+static void ts_merge_lo(tsort *t, int base1, int len1, int base2, int len2) {
+  docscore *a = t->a, *tmp = ts_tmp(t, len1);
+  memcpy(tmp, a + base1, (size_t)len1 * sizeof(docscore));
+  int cursor1 = 0, cursor2 = base2, dest = base1;
+  a[dest++] = a[cursor2++];
+  if (--len2 == 0) {
+    memcpy(a + dest, tmp + cursor1, (size_t)len1 * sizeof(docscore));
+    return;
+  }
+  if (len1 == 1) {
+    memmove(a + dest, a + cursor2, (size_t)len2 * sizeof(docscore));
+    a[dest + len2] = tmp[cursor1];
+    return;
+  }
+  int minGallop = t->min_gallop;
+  for (;;) {
+    int count1 = 0, count2 = 0;
+    int brk = 0;
+    do {
+      if (ts_cmp(&a[cursor2], &tmp[cursor1]) < 0) {
+        a[dest++] = a[cursor2++];
+        count2++;
+        count1 = 0;
+        if (--len2 == 0) { brk = 1; break; }
+      } else {
+        a[dest++] = tmp[cursor1++];
+        count1++;
+        count2 = 0;
+        if (--len1 == 1) { brk = 1; break; }
+      }
+    } while ((count1 | count2) < minGallop);
+    if (brk) break;
+    do {
+      count1 = ts_gallop_right(&a[cursor2], tmp, cursor1, len1, 0);
+      if (count1 != 0) {
+        memcpy(a + dest, tmp + cursor1, (size_t)count1 * sizeof(docscore));
+        dest += count1;
+        cursor1 += count1;
+        len1 -= count1;
+        if (len1 <= 1) { brk = 1; break; }
+      }
+      a[dest++] = a[cursor2++];
+      if (--len2 == 0) { brk = 1; break; }
+      count2 = ts_gallop_left(&tmp[cursor1], a, cursor2, len2, 0);
+      if (count2 != 0) {
+        memmove(a + dest, a + cursor2, (size_t)count2 * sizeof(docscore));
+        dest += count2;
+        cursor2 += count2;
+        len2 -= count2;
+        if (len2 == 0) { brk = 1; break; }
+      }
+      a[dest++] = tmp[cursor1++];
+      if (--len1 == 1) { brk = 1; break; }
+      minGallop--;
+    } while (count1 >= TS_MIN_GALLOP || count2 >= TS_MIN_GALLOP);
+    if (brk) break;
+    if (minGallop < 0) minGallop = 0;
+    minGallop += 2;
+  }
+  t->min_gallop = minGallop < 1 ? 1 : minGallop;
+  if (len1 == 1) {
+    memmove(a + dest, a + cursor2, (size_t)len2 * sizeof(docscore));
+    a[dest + len2] = tmp[cursor1];
+  } else if (len1 == 0) {
+    t->err = 1; /* IllegalArgumentException: Comparison method violates its general contract! */
+  } else {
+    memcpy(a + dest, tmp + cursor1, (size_t)len1 * sizeof(docscore));
+  }
+}
+
+static void ts_merge_hi(tsort *t, int base1, int len1, int base2, int len2) {
+  docscore *a = t->a, *tmp = ts_tmp(t, len2);
+  memcpy(tmp, a + base2, (size_t)len2 * sizeof(docscore));
+  int cursor1 = base1 + len1 - 1, cursor2 = len2 - 1, dest = base2 + len2 - 1;
+  a[dest--] = a[cursor1--];
+  if (--len1 == 0) {
+    memcpy(a + dest - (len2 - 1), tmp, (size_t)len2 * sizeof(docscore));
+    return;
+  }
+  if (len2 == 1) {
+    dest -= len1;
+    cursor1 -= len1;
+    memmove(a + dest + 1, a + cursor1 + 1, (size_t)len1 * sizeof(docscore));
+    a[dest] = tmp[cursor2];
+    return;
+  }
+  int minGallop = t->min_gallop;
+  for (;;) {
+    int count1 = 0, count2 = 0;
+    int brk = 0;
+    do {
+      if (ts_cmp(&tmp[cursor2], &a[cursor1]) < 0) {
+        a[dest--] = a[cursor1--];
+        count1++;
+        count2 = 0;
+        if (--len1 == 0) { brk = 1; break; }
+      } else {
+        a[dest--] = tmp[cursor2--];
+        count2++;
+        count1 = 0;
+        if (--len2 == 1) { brk = 1; break; }
+      }
+    } while ((count1 | count2) < minGallop);
+    if (brk) break;
+    do {
+      count1 = len1 - ts_gallop_right(&tmp[cursor2], a, base1, len1, len1 - 1);
+      if (count1 != 0) {
+        dest -= count1;
+        cursor1 -= count1;
+        len1 -= count1;
+        memmove(a + dest + 1, a + cursor1 + 1, (size_t)count1 * sizeof(docscore));
+        if (len1 == 0) { brk = 1; break; }
+      }
+      a[dest--] = tmp[cursor2--];
+      if (--len2 == 1) { brk = 1; break; }
+      count2 = len2 - ts_gallop_left(&a[cursor1], tmp, 0, len2, len2 - 1);
+      if (count2 != 0) {
+        dest -= count2;
+        cursor2 -= count2;
+        len2 -= count2;
+        memcpy(a + dest + 1, tmp + cursor2 + 1, (size_t)count2 * sizeof(docscore));
+        if (len2 <= 1) { brk = 1; break; }
+      }
+      a[dest--] = a[cursor1--];
+      if (--len1 == 0) { brk = 1; break; }
+      minGallop--;
+    } while (count1 >= TS_MIN_GALLOP || count2 >= TS_MIN_GALLOP);
+    if (brk) break;
+    if (minGallop < 0) minGallop = 0;
+    minGallop += 2;
+  }
+  t->min_gallop = minGallop < 1 ? 1 : minGallop;
+  if (len2 == 1) {
+    dest -= len1;
+    cursor1 -= len1;
+    memmove(a + dest + 1, a + cursor1 + 1, (size_t)len1 * sizeof(docscore));
+    a[dest] = tmp[cursor2];
+  } else if (len2 == 0) {
+    t->err = 1; /* IllegalArgumentException */
+  } else {
+    memcpy(a + dest - (len2 - 1), tmp, (size_t)len2 * sizeof(docscore));
+  }
+}
+
+static void ts_merge_at(tsort *t, int i) {
+  int base1 = t->base[i], len1 = t->len[i], base2 = t->base[i + 1], len2 = t->len[i + 1];
+  t->len[i] = len1 + len2;
+  if (i == t->stack - 3) {
+    t->base[i + 1] = t->base[i + 2];
+    t->len[i + 1] = t->len[i + 2];
+  }
+  t->stack--;
+  int k = ts_gallop_right(&t->a[base2], t->a, base1, len1, 0);
+  base1 += k;
+  len1 -= k;
+  if (len1 == 0) return;
+  len2 = ts_gallop_left(&t->a[base1 + len1 - 1], t->a, base2, len2, len2 - 1);
+  if (len2 == 0) return;
+  if (len1 <= len2) ts_merge_lo(t, base1, len1, base2, len2);
+  else ts_merge_hi(t, base1, len1, base2, len2);
+}
+
+static void ts_merge_collapse(tsort *t) { /* JDK 7 GA */
+  while (t->stack > 1 && !t->err) {
+    int n = t->stack - 2;
+    if (n > 0 && t->len[n - 1] <= t->len[n] + t->len[n + 1]) {
+      if (t->len[n - 1] < t->len[n + 1]) n--;
+      ts_merge_at(t, n);
+    } else if (t->len[n] <= t->len[n + 1]) {
+      ts_merge_at(t, n);
+    } else {
+      break;
+    }
+  }
+}
+
+static void ts_merge_force_collapse(tsort *t) {
+  while (t->stack > 1 && !t->err) {
+    int n = t->stack - 2;
+    if (n > 0 && t->len[n - 1] < t->len[n + 1]) n--;
+    ts_merge_at(t, n);
+  }
+}
+
+/* ComparableTimSort.sort(a, 0, n): 0, or -1 where Java throws */
+static int timsort7(docscore *a, int n) {
+  if (n < 2) return 0;
+  int lo = 0, rem = n;
+  if (rem < TS_MIN_MERGE) {
+    int initRunLen = ts_count_run(a, lo, n);
+    ts_binary_sort(a, lo, n, lo + initRunLen);
+    return 0;
+  }
+  tsort t;
+  memset(&t, 0, sizeof t);
+  t.a = a;
+  t.min_gallop = TS_MIN_GALLOP;
+  int minRun = ts_min_run(rem);
+  do {
+    int runLen = ts_count_run(a, lo, n);
+    if (runLen < minRun) {
+      int force = rem <= minRun ? rem : minRun;
+      ts_binary_sort(a, lo, lo + force, lo + runLen);
+      runLen = force;
+    }
+    t.base[t.stack] = lo;
+    t.len[t.stack] = runLen;
+    t.stack++;
+    ts_merge_collapse(&t);
+    lo += runLen;
+    rem -= runLen;
+  } while (rem != 0 && !t.err);
+  ts_merge_force_collapse(&t);
+  free(t.tmp);
+  return t.err ? -1 : 0;
+}
+
 static int ds_cmp_docno(const void *x, const void *y) {
   const docscore *a = (const docscore *)x, *b = (const docscore *)y;
   if (a->score > b->score) return -1;
@@ -693,8 +1055,10 @@ static int ds_cmp_first(const void *x, const void *y) {
  * idf_mode: 0 = reference (stored key df, T1/T2), 1 = true df (postings length), int division both.
  * order: 0 = score desc / docno asc (north-star tie-break),
  *        1 = Java 6 Collections.sort with the reference DocScore comparator,
- *        2 = score desc / first-encounter (stable exact ties).
- * Returns number of results written (<= k); scores/docnos out.
+ *        2 = score desc / first-encounter (stable exact ties),
+ *        3 = Java 7 Collections.sort (ComparableTimSort) with the DocScore comparator.
+ * Returns number of results written (<= k); scores/docnos out; -1 in order 3
+ * where Java 7's TimSort throws IllegalArgumentException (contract violation).
  */
 /* ref-faithful timing mode (bench.py cpu_baseline): the accumulator lookup is
  * the reference's linear scores.indexOf scan (T6) instead of the docno table;
@@ -764,6 +1128,11 @@ int or_query(const or_index *ix, const uint16_t *const *terms, const int *lens, 
     memcpy(aux, sc, sizeof(docscore) * n);
     legacy_merge_sort(aux, sc, 0, n, 0);
     free(aux);
+  } else if (order == 3) {
+    if (timsort7(sc, n) != 0) { /* Collections.sort throws: rank() has no result */
+      free(sc);
+      return -1;
+    }
   } else {
     qsort(sc, (size_t)n, sizeof(docscore), order == 2 ? ds_cmp_first : ds_cmp_docno);
   }
@@ -772,6 +1141,34 @@ int or_query(const or_index *ix, const uint16_t *const *terms, const int *lens, 
     out_docno[i] = sc[i].docId;
     out_score[i] = sc[i].score;
   }
+  free(sc);
+  return r;
+}
+
+/* rank()'s sort alone, for the sort tests: candidates (score[i], first-encounter
+ * index i, docId i) in list order -> perm[r] = the index at rank r under `order`
+ * (1 Java 6 legacy merge sort, 3 Java 7 ComparableTimSort, 0 / 2 exact orders);
+ * returns n, or -1 where Java 7 throws */
+int or_sort_docscores(const double *score, int n, int order, int32_t *perm) {
+  docscore *sc = (docscore *)malloc(sizeof(docscore) * (size_t)(n ? n : 1));
+  for (int i = 0; i < n; i++) {
+    sc[i].docId = i;
+    sc[i].score = score[i];
+    sc[i].first = i;
+  }
+  int r = n;
+  if (order == 1) {
+    docscore *aux = (docscore *)malloc(sizeof(docscore) * (size_t)(n ? n : 1));
+    memcpy(aux, sc, sizeof(docscore) * (size_t)n);
+    legacy_merge_sort(aux, sc, 0, n, 0);
+    free(aux);
+  } else if (order == 3) {
+    if (timsort7(sc, n) != 0) r = -1;
+  } else {
+    qsort(sc, (size_t)n, sizeof(docscore), order == 2 ? ds_cmp_first : ds_cmp_docno);
+  }
+  if (r >= 0)
+    for (int i = 0; i < n; i++) perm[i] = sc[i].docId;
   free(sc);
   return r;
 }

@@ -61,6 +61,12 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise SmeError(-2, "libsme.so not built (run __graft_entry__.build() or make -C %s)" % _HERE)
+    # a process that also drives the device through torch lets torch's HIP runtime
+    # open it first (torch's lazy init fails once libsme's runtime holds the device)
+    import sys
+    t = sys.modules.get("torch")
+    if t is not None and t.cuda.is_available():
+        t.cuda.init()
     L = C.CDLL(LIB_PATH)
     vp, sz, i64p, i32p = C.c_void_p, C.c_size_t, C.POINTER(C.c_int64), C.POINTER(C.c_int32)
     L.sme_last_error.restype = C.c_char_p

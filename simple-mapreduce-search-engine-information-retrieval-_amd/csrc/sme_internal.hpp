@@ -29,6 +29,7 @@ struct sme_ctx {
   // build workspace, reused across builds (see DevBuf)
   sme::DevBuf ws[128];  // 48..63 query / serializer / tokenizer / reweight, 64..127 build
   sme::DevBuf cub_tmp;
+  sme::DevBuf q_gates;  // k_query_win: per-query gate of the current thresholds (k_gates)
   uint64_t vocab_long_cap = 0, vocab_ovf_cap = 0, raw_cap_hint = 0, lt_cap_hint = 0;  // learned across builds
   std::string profile_json;
   std::vector<std::pair<std::string, float>> last_profile;

@@ -1121,6 +1121,13 @@ __device__ __forceinline__ uint32_t gate_of(double th0, double alpha) {
   return g >= 0.0 ? (uint32_t)g + 1u : 1u;
 }
 
+// the window pass's per-query gates, computed once per launch from the current
+// thresholds (the kernel then holds one scalar per query instead of the fp64
+// threshold, and loads th0 / thk only for its candidates)
+__global__ void k_gates(const double *th0, int n, double alpha, uint32_t *gate) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) gate[q] = gate_of(th0[q], alpha);
+}
+
 // Per-batch query tables for the window path: one 32-byte record per query
 // term (postings base, df, batch row, heavy row, idf) and one per position of
 // the query order (query, first term, term count), so a wave reaches a query's
@@ -1436,6 +1443,7 @@ struct QWinArgs {
   double alpha;
   const double *th0;           // per query threshold: keep (S, key) not worse than (th0, thk)
   const uint64_t *thk;
+  const uint32_t *gate;        // per query gate_of(th0): the impact sum a document must reach (k_gates)
   unsigned int *ccnt;          // candidates per query
   double *cs;                  // [nq][cap] scores
   uint64_t *ck;                // [nq][cap] doc keys
@@ -1513,8 +1521,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
   // record, term records, threshold and skip entries load while this one runs
   QPos P = ld_pos_uni(a.qpos + pos);
   QDesc D = ld_desc_nt(a.desc, P.q0, P.nt, lane);
-  double th0 = ld_uni(a.th0 + P.q);
-  uint64_t thk = ld_uni(a.thk + P.q);
+  uint32_t gate = ld_uni(a.gate + P.q);
   int32_t mc = 0, me = 0;
   if (D.mdf > 0 && D.hr < 0) {
     mc = a.skt[x * a.nrows + D.brow];
@@ -1525,15 +1532,13 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
   for (;;) {
     const int npos = pos + kWNT / 64;
     const bool hasn = npos < p_hi;
-    // the next query's term records and threshold, and the position record after it
+    // the next query's term records and gate, and the position record after it
     QDesc ND{0, 0, 0, -1, 0, 0.0};
-    double nth0 = 0.0;
-    uint64_t nthk = kNoKey;
+    uint32_t ngate = 0;
     QPos NNP{0, 0, 0};
     if (hasn) {
       ND = ld_desc_nt(a.desc, NP.q0, NP.nt, lane);
-      nth0 = ld_uni(a.th0 + NP.q);
-      nthk = ld_uni(a.thk + NP.q);
+      ngate = ld_uni(a.gate + NP.q);
       if (npos + kWNT / 64 < p_hi) NNP = ld_pos_uni(a.qpos + npos + kWNT / 64);
     }
 #ifdef SME_EXPERIMENTS  // timing switches: 4 = no sparse terms, 8 = no heavy terms
@@ -1543,7 +1548,6 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     const uint64_t hm = (uint64_t)__ballot(D.hr >= 0);
     const uint64_t sm = (uint64_t)__ballot(D.mdf > 0 && D.hr < 0);
 #endif
-    const uint32_t gate = (uint32_t)__builtin_amdgcn_readfirstlane((int)gate_of(th0, a.alpha));
     // every u16 accumulator below starts at 2^15 - gate, so a bound or an A(d)
     // reaching the gate is its bit 15 (A(d) < 2^14 and gate <= 2^14 + 1 leave no
     // carry between halves; a gate past 2^15 - 1 takes no bias, and nothing
@@ -1804,6 +1808,9 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
           const int32_t cincl = wave_incl_sum(cl);
           const int32_t ncand = (QW_EXPER & 2) ? 0 : __builtin_amdgcn_readlane(cincl, 63);
           if (QW_STATS && lane == 0) atomicAdd(QW_STATS + 4, (unsigned long long)ncand);
+          // the threshold itself (score, key) only where documents reached the gate
+          const double th0 = ncand > 0 ? ld_uni(a.th0 + P.q) : 0.0;
+          const uint64_t thk = ncand > 0 ? ld_uni(a.thk + P.q) : kNoKey;
           for (int32_t k0 = 0; k0 < ncand; k0 += kCList) {
             const int32_t kn = min(ncand - k0, kCList);
             qwave_sync();
@@ -1915,8 +1922,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     P = NP;
     NP = NNP;
     D = ND;
-    th0 = nth0;
-    thk = nthk;
+    gate = ngate;
     mc = nmc;
     me = nme;
   }
@@ -2591,6 +2597,8 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
     wa.alpha = ix->q_alpha;
     wa.th0 = th0;
     wa.thk = thk;
+    uint32_t *gates = cx->q_gates.as<uint32_t>((size_t)nq);
+    wa.gate = gates;
     wa.ccnt = ccnt;
     wa.cs = cs;
     wa.ck = ckk;
@@ -2649,7 +2657,11 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
       // workgroups per CU without changing the kernel's code
       if (const char *ql = getenv("SME_QLDS")) dyn_lds = (size_t)atoi(ql);
 #endif
-      if (wg > 0) hipLaunchKernelGGL(k_query_win, dim3((unsigned)wg), dim3(kWNT), dyn_lds, st, wa);
+      if (wg > 0) {
+        hipLaunchKernelGGL(k_gates, dim3((unsigned)std::min((nq + 255) / 256, 4096)), dim3(256), 0, st, th0, nq,
+                           wa.alpha, gates);
+        hipLaunchKernelGGL(k_query_win, dim3((unsigned)wg), dim3(kWNT), dyn_lds, st, wa);
+      }
       SME_CHECK_LAUNCH();
     };
     for (int round = 0; round < kWinRounds && n_round > 0; round++) {

@@ -42,6 +42,7 @@ def lib():
         L.or_last_error.restype = C.c_char_p
         L.or_lookup_selfcheck.argtypes = [C.c_void_p]
         L.or_set_ref_scan.argtypes = [C.c_int]
+        L.or_sort_docscores.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         L.or_count_distinct_terms.restype = C.c_int64
         L.or_count_distinct_terms.argtypes = [C.c_char_p, C.c_void_p, C.c_int64]
         L.or_split_records.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]
@@ -182,7 +183,9 @@ class OracleIndex:
 
     def query(self, terms, k=10, idf_mode=0, order=0):
         """rank() over already-processed query terms; order 0 docno tie-break,
-        1 Java-6 Collections.sort with DocScore comparator, 2 first-encounter."""
+        1 Java-6 Collections.sort with DocScore comparator, 2 first-encounter,
+        3 Java-7 Collections.sort (ComparableTimSort) with the DocScore comparator
+        (None, None where Java 7 throws IllegalArgumentException)."""
         bs = [t.encode("utf-8") for t in terms]
         blob = b"".join(bs)
         offs = [0]
@@ -192,6 +195,8 @@ class OracleIndex:
         dn = (C.c_int32 * max(k, 1))()
         sc = (C.c_double * max(k, 1))()
         r = lib().or_query_utf8(self._h, blob, o, len(terms), k, idf_mode, order, dn, sc)
+        if r < 0:  # order 3: Java 7's TimSort throws IllegalArgumentException here
+            return None, None
         return [dn[i] for i in range(r)], [sc[i] for i in range(r)]
 
 
@@ -300,3 +305,15 @@ class CpuOptIndex:
         if getattr(self, "_h", None):
             lib().or_cpuopt_free(self._h)
             self._h = None
+
+
+def sort_docscores(scores, order):
+    """rank()'s Collections.sort alone (oracle or_sort_docscores): candidates in
+    list order with these scores -> their list indices in sorted order (order 1
+    Java 6 legacy merge sort, 3 Java 7 ComparableTimSort, both over the DocScore
+    comparator), or None where Java 7 throws IllegalArgumentException."""
+    import numpy as np
+    sc = np.ascontiguousarray(scores, dtype=np.float64)
+    perm = np.zeros(max(len(sc), 1), np.int32)
+    r = lib().or_sort_docscores(sc.ctypes.data, len(sc), order, perm.ctypes.data)
+    return None if r < 0 else perm[:len(sc)].tolist()

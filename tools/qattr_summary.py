@@ -10,12 +10,12 @@ import json
 import os
 import sys
 
-PARTS = [(0, "full kernel"), (2, "- exact candidate scoring"), (3, "- passing-block impact sums"),
-         (7, "- sparse postings"), (15, "- heavy block bounds (records / skip entries / pipeline left)")]
+PARTS = [(0, "full kernel"), (2, "- exact candidate scoring"), (3, "- passing sub-block sums"),
+         (7, "- sparse postings"), (15, "- heavy sub-block bounds (records / skip entries / pipeline left)")]
 WHAT = {0: "candidates: tf bytes, LDS / global tf search, list appends",
-        2: "passing blocks: heavy impact rows (+ inline sparse entries)",
-        3: "sparse postings of the window: docno / tf loads, LDS block sums and list",
-        7: "heavy block bounds: bmq rows",
+        2: "passing sub-blocks: listing + exact A(d) from one heavy impact dword per term (+ sparse entries)",
+        3: "sparse postings of the window: posting words, LDS block sums and list",
+        7: "heavy sub-block bounds: sbq rows (one uint4 per heavy term and lane)",
         15: "per-pair overhead: position / term records, thresholds, skip entries"}
 
 

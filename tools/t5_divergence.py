@@ -15,8 +15,15 @@ the fraction of queries whose top-k docno LISTS differ, whose top-k SETS differ,
 and the mean number of positions that differ -- and checks that order 1 equals
 order 2 (score desc, first-encounter index asc): the merge sort only ever asks
 compareTo(a, b) <= 0 / > 0, which is b.score <= a.score / b.score > a.score
-for finite scores, so the legacy merge sort is a STABLE sort by score desc.  CPU only; writes
-profiles/t5_divergence.json.
+for finite scores, so the legacy merge sort is a STABLE sort by score desc.
+
+Round 6 adds order 3: JDK 7's Collections.sort (ComparableTimSort, the default
+from Java 7 on; run 0196 is dated three days after Java 7 shipped, so the JVM is
+unpinned).  TimSort asks compareTo < 0 / >= 0 and gallops, so the broken
+comparator DOES bite: per group, how many queries' printed top-k differ between
+the Java 7 and Java 6 orders, and in how many Java 7 throws
+IllegalArgumentException ("Comparison method violates its general contract!")
+instead of printing anything.  CPU only; writes profiles/t5_divergence.json.
     python tools/t5_divergence.py
 """
 import importlib
@@ -46,12 +53,20 @@ def main():
     for grp in gold["queries"]:
         k, mode = grp["k"], grp["idf_mode"]
         n_list = n_set = n_pos = n_multi = n_12 = 0
+        n7_throw = n7_list = n7_set = n7_vs0 = 0
         for tl, d_gold, _ in grp["q"]:
             d0, s0 = ix.query(tl, k, mode, 0)
             assert d0 == d_gold
             d1, s1 = ix.query(tl, k, mode, 1)
             d2, s2 = ix.query(tl, k, mode, 2)
+            d3, s3 = ix.query(tl, k, mode, 3)
             n_12 += (d1 != d2) or (s1 != s2)
+            if d3 is None:
+                n7_throw += 1
+            else:
+                n7_list += d3 != d1
+                n7_set += set(d3) != set(d1)
+                n7_vs0 += d3 != d0
             n_multi += len(set(tl)) > 1
             if d0 != d1:
                 n_list += 1
@@ -63,7 +78,10 @@ def main():
              "multi_term": n_multi, "list_differs": n_list, "list_differs_frac": round(n_list / nq, 4),
              "set_differs": n_set, "set_differs_frac": round(n_set / nq, 4),
              "mean_positions_differing": round(n_pos / max(n_list, 1), 2),
-             "java6_sort_vs_first_encounter_differs": n_12}
+             "java6_sort_vs_first_encounter_differs": n_12,
+             "java7_timsort_throws": n7_throw, "java7_timsort_throws_frac": round(n7_throw / nq, 4),
+             "java7_vs_java6_list_differs": n7_list, "java7_vs_java6_set_differs": n7_set,
+             "java7_vs_docno_order_list_differs": n7_vs0}
         print(g, flush=True)
         out["groups"].append(g)
     path = os.path.join(ROOT, "profiles", "t5_divergence.json")
