@@ -106,6 +106,10 @@ void sme_destroy(sme_ctx *ctx);
  *                   even when the packed term ids fit 64 bits (default 0: automatic)
  *   "tok_grid"      tokenizer workgroups, >= 1 (default 4096)
  *   "raw_load_pct"  raw-vocabulary table load of the next build, 10..90 (default 40)
+ *   "docid_terms"   1 (default): a record's DOCNO token that is its own term (ASCII letters and
+ *                   digits ending in a digit, unchanged by the stemmer) skips the per-distinct
+ *                   vocabulary work and is ranked by a merge with the sorted word terms when the
+ *                   docids ascend in file order; 0: every raw token through the general path
  *   "query_table_budget"  bytes a batch's skip table may take (default 0 =
  *                   a quarter of the free HBM); a batch over it is split by
  *                   query range, and queries still overflowing their

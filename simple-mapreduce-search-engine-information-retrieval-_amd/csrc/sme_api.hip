@@ -318,6 +318,9 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
     } else if (n == "raw_load_pct") {
       range(10, 90);
       cx->opt_raw_load_pct = v;
+    } else if (n == "docid_terms") {
+      range(0, 1);
+      cx->opt_docid_terms = v;
     } else {
       throw sme::Error(SME_EINVAL, "unknown option " + n);
     }

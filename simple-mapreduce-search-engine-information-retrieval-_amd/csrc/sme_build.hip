@@ -444,7 +444,7 @@ constexpr int kDocWin = 96;
 __global__ __launch_bounds__(256) void k_docno(const uint8_t *t, int64_t n, const uint64_t *rs, const uint64_t *re,
                                                int64_t nR, const uint16_t *mchars, const int64_t *moff, int64_t mn,
                                                const uint32_t *mslots, uint64_t mmask, int32_t *docno,
-                                               unsigned long long *err) {
+                                               unsigned long long *err, uint64_t *dspan) {
   __shared__ uint4 win[256][kDocWin / 16];
   uint8_t *w = reinterpret_cast<uint8_t *>(win[threadIdx.x]);
   const int64_t mis = (int64_t)((uintptr_t)t & 15);
@@ -484,11 +484,13 @@ __global__ __launch_bounds__(256) void k_docno(const uint8_t *t, int64_t n, cons
       if (!docid_span(t, s, e, &ib, &ie)) {  // getDocid throws: the map task fails
         atomicAdd(err, 1ull);
         docno[r] = 0;
+        dspan[r] = 0;
         continue;
       }
       db = t + ib;
     }
     const int64_t dl = ie - ib;
+    dspan[r] = dl <= 255 ? (((uint64_t)ib << 8) | (uint64_t)dl) : 0;  // the docid's bytes (K4b)
     if (mslots) {
       uint64_t h = 0xCBF29CE484222325ull;
       for (int64_t p = 0; p < dl;) {
@@ -1764,7 +1766,7 @@ __global__ void k_raw_term(const int32_t *rlist, int64_t nraw, const uint32_t *c
                            const int32_t *raw_nout, int32_t *raw_term) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nraw; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t slot = rlist[i];
-    if (raw_nout[slot] == 1) raw_term[slot] = rank_of_slot[cand_final[i]];
+    if (raw_nout[slot] == 1 && cand_final[i] != 0xFFFFFFFFu) raw_term[slot] = rank_of_slot[cand_final[i]];
   }
 }
 __global__ void k_raw_multi(const uint64_t *okey_s, const uint32_t *oidx_s, int64_t novf, int64_t nraw,
@@ -1778,6 +1780,330 @@ __global__ void k_raw_multi(const uint64_t *okey_s, const uint32_t *oidx_s, int6
 
 // ============================================================================
 // K5: per-record aggregation (combiner) and emission
+// ============================================================================
+// K4b: docid terms (T7) beside the word vocabulary
+// ============================================================================
+// Every record's DOCNO text is indexed like the rest of the record
+// (TrecDocument.getContent is the whole record, TrecDocument.java:94-96;
+// TermKGramDocIndexer.java:129): on c5 / the c4 shard most of the vocabulary
+// is docid terms, one document each.  A raw token that is a record's whole
+// trimmed <DOCNO> span and whose term is provably its own lowercase form --
+// ASCII letters and digits ending in a digit, at most kDocTermMax bytes, no
+// stopword, and Porter2 leaves it unchanged (the stemmer is run to check) --
+// skips the per-distinct normalize / dedup / sort of the word vocabulary: in
+// file order such docid terms are usually ascending already (checked), so
+// their ranks come from a merge with the sorted word terms.  A failed check
+// (unsorted or equal docid terms, a docid term equal to a word term) keeps
+// the build on the general path; the result is the same either way.
+constexpr int kDocTermMax = 48;
+constexpr uint32_t kNoRec = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint8_t lower_ascii(uint8_t c) { return (c >= 'A' && c <= 'Z') ? (uint8_t)(c + 32) : c; }
+
+// per record: the raw slot of its docid token when it qualifies, else -1; such
+// slots marked in dmark (0; kNoRec: no docid term's).
+// The docid's bytes come from k_docno (getDocid's trimmed span).  No stopword
+// ends in a digit, and every rule of the 2010 Porter2 (englishStemmer.java:
+// Step_0 .. Step_5, exception1 / exception2) matches a letter suffix or a whole
+// letter word, so a word of [a-z0-9] ending in a digit stems to itself -- pinned
+// by tests/test_docid_terms.py against the oracle's stemmer and stopword list.
+// the <= 16 bytes of text[ib, ib + len) as little-endian words, by two aligned
+// 16-byte loads (false: not inside the buffer, take the bytes one by one)
+__device__ __forceinline__ bool span16(const uint8_t *t, int64_t n, int64_t ib, int64_t len, uint64_t &w0,
+                                       uint64_t &w1) {
+  const int64_t a0 = (int64_t)(((uintptr_t)(t + ib)) & 15);
+  if (len > 16 || ib < a0 || ib - a0 + 32 > n) return false;
+  const uint4 *q = reinterpret_cast<const uint4 *>(t + ib - a0);
+  const uint4 x = q[0], y = q[1];
+  const uint32_t wd[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  w0 = w1 = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int p = (int)a0 + k;
+    const uint64_t c = k < len ? (wd[p >> 2] >> (8 * (p & 3))) & 0xFFu : 0u;
+    if (k < 8) w0 |= c << (8 * k);
+    else w1 |= c << (8 * (k - 8));
+  }
+  return true;
+}
+__device__ __forceinline__ bool alnum_byte(uint32_t c) {
+  const uint32_t l = c | 0x20u;
+  return (c >= '0' && c <= '9') || (l >= 'a' && l <= 'z');
+}
+__global__ __launch_bounds__(256) void k_docid_slots(const uint8_t *t, int64_t n, const uint64_t *dspan, int64_t nR,
+                                                     const RawTable tb, int32_t *dslot, uint32_t *dmark) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nR; r += (int64_t)gridDim.x * blockDim.x) {
+    int32_t out = -1;
+    const uint64_t sp = dspan[r];
+    const int64_t ib = (int64_t)(sp >> 8), len = (int64_t)(sp & 0xFF);
+    bool ok = len >= 2 && len <= kDocTermMax;
+    TokSig g{0, 0, 0};
+    uint64_t w0, w1;
+    if (ok && span16(t, n, ib, len, w0, w1)) {  // the span's bytes as the signature's words, checked in registers
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (k < len) ok = ok && alnum_byte((uint32_t)((k < 8 ? w0 >> (8 * k) : w1 >> (8 * (k - 8))) & 0xFFu));
+      const uint32_t last = (uint32_t)((len <= 8 ? w0 >> (8 * (len - 1)) : w1 >> (8 * (len - 9))) & 0xFFu);
+      ok = ok && last >= '0' && last <= '9';
+      g = TokSig{sig_head(w0, w1), w0, w1};
+    } else if (ok) {
+      ok = t[ib + len - 1] >= '0' && t[ib + len - 1] <= '9';
+      for (int64_t k = 0; k < len && ok; k++) ok = alnum_byte(t[ib + k]);
+      if (ok) g = sig_bytes(t + ib, len);
+    }
+    if (ok) {  // its raw slot (the table is complete: plain loads)
+      uint64_t s = g.h & tb.mask;
+      for (uint64_t probe = 0; probe <= tb.mask && probe <= kMaxProbe; probe++, s = (s + 1) & tb.mask) {
+        const unsigned long long key = tb.key[s];
+        if (key == 0) break;
+        if (key != g.h) continue;
+        const ulonglong2 tw = tb.tok[s];
+        if (tw.x != g.w0 || tw.y != g.w1) continue;
+        bool eq = true;  // (<= 16 bytes: no token byte is 0, so w0 / w1 decide)
+        if (len > 16) {
+          const uint64_t rp = tb.rep[s];
+          eq = (int64_t)(rp & 0xFFFFFFull) == len;
+          for (int64_t k = 16; k < len && eq; k++) eq = tb.text[(rp >> 24) + k] == t[ib + k];
+        }
+        if (eq) {
+          out = (int32_t)s;
+          break;
+        }
+      }
+      if (out >= 0) dmark[out] = 0u;  // a docid term's slot (a docid in two records: the ascending check fails)
+    }
+    dslot[r] = out;
+  }
+}
+
+// the word vocabulary's raw tokens: every used slot that is no docid term's
+__global__ void k_raw_flags_words(const unsigned long long *key, const uint32_t *dmark, uint64_t n, uint8_t *flag) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < n; s += (uint64_t)gridDim.x * blockDim.x)
+    flag[s] = key[s] != 0 && dmark[s] == kNoRec;
+}
+
+__global__ void k_docid_flags(const int32_t *dslot, int64_t nR, uint8_t *flag) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nR; r += (int64_t)gridDim.x * blockDim.x)
+    flag[r] = dslot[r] >= 0;
+}
+
+// big-endian 16-byte key of a term's first 16 units (all < 256; zero padded: no
+// unit is 0, so a shorter string sorts first) -- exact String.compareTo order for
+// terms of <= 16 such units
+struct Key16 {
+  uint64_t hi, lo;
+};
+__device__ __forceinline__ int cmp_key16(const Key16 &a, const Key16 &b) {
+  if (a.hi != b.hi) return a.hi < b.hi ? -1 : 1;
+  if (a.lo != b.lo) return a.lo < b.lo ? -1 : 1;
+  return 0;
+}
+__device__ __forceinline__ Key16 key16_bytes(const uint8_t *p, int len) {  // lowercase ASCII docid bytes
+  Key16 k{0, 0};
+  for (int i = 0; i < 16; i++) {
+    const uint64_t c = i < len ? lower_ascii(p[i]) : 0;
+    if (i < 8) k.hi |= c << (56 - 8 * i);
+    else k.lo |= c << (56 - 8 * (i - 8));
+  }
+  return k;
+}
+// docid term j: (text offset << 8 | length) of its docid span (the bytes of its
+// raw slot) and its key
+// byte k of a Key16 (k < 16)
+__device__ __forceinline__ uint32_t key16_byte(const Key16 &k, int i) {
+  return (uint32_t)((i < 8 ? k.hi >> (56 - 8 * i) : k.lo >> (56 - 8 * (i - 8))) & 0xFFu);
+}
+__global__ void k_docid_keys(const int32_t *dl, int64_t Vd, const uint64_t *dspan, const uint8_t *text, int64_t n,
+                             uint64_t *dsrc, Key16 *dkey) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < Vd; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t sp = dspan[dl[j]];  // (the docid span's bytes: those of its raw slot)
+    const int64_t ib = (int64_t)(sp >> 8), len = (int64_t)(sp & 0xFF);
+    dsrc[j] = sp;
+    uint64_t w0, w1;
+    if (span16(text, n, ib, len, w0, w1)) {
+      // letters and digits: lowercase = | 0x20 on every byte of the term (digits have the bit)
+      const uint64_t m0 = len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1), m1 = len >= 16 ? ~0ull : len <= 8 ? 0ull
+                                                                                       : ((1ull << (8 * (len - 8))) - 1);
+      dkey[j] = Key16{__builtin_bswap64((w0 | 0x2020202020202020ull) & m0), __builtin_bswap64((w1 | 0x2020202020202020ull) & m1)};
+    } else {
+      dkey[j] = key16_bytes(text + ib, (int)len);
+    }
+  }
+}
+// String.compareTo of two docid terms (lowercase ASCII bytes)
+__device__ int cmp_docid(const uint8_t *text, uint64_t a, uint64_t b) {
+  const uint8_t *x = text + (a >> 8), *y = text + (b >> 8);
+  const int xl = (int)(a & 0xFF), yl = (int)(b & 0xFF), m = xl < yl ? xl : yl;
+  for (int i = 0; i < m; i++) {
+    const int d = (int)lower_ascii(x[i]) - (int)lower_ascii(y[i]);
+    if (d) return d;
+  }
+  return xl - yl;
+}
+// in file order the docid terms must be strictly ascending (else: general path)
+__global__ void k_docid_ascending(const Key16 *dkey, const uint64_t *dsrc, int64_t Vd, const uint8_t *text,
+                                  unsigned long long *bad) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x + 1; j < Vd; j += (int64_t)gridDim.x * blockDim.x) {
+    int c = cmp_key16(dkey[j - 1], dkey[j]);
+    if (c == 0 && ((dsrc[j - 1] & 0xFF) > 16 || (dsrc[j] & 0xFF) > 16)) c = cmp_docid(text, dsrc[j - 1], dsrc[j]);
+    if (c >= 0) atomicAdd(bad, 1ull);
+  }
+}
+// a docid term equal to a word term (final dedup table of the word candidates)
+__global__ void k_docid_collide(const uint64_t *dsrc, const Key16 *dkey, int64_t Vd, const uint8_t *text,
+                                const uint16_t *pool, const uint64_t *cand_str, const unsigned long long *fkeys,
+                                const unsigned long long *freps, uint64_t fmask, unsigned long long *bad) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < Vd; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t *p = text + (dsrc[j] >> 8);
+    const int l = (int)(dsrc[j] & 0xFF);
+    const Key16 kj = dkey[j];
+    auto unit = [&](int i) -> uint32_t { return l <= 16 ? key16_byte(kj, i) : lower_ascii(p[i]); };
+    uint64_t h = 0x84222325cbf29ce4ull;  // hash_u16 of the lowercase units
+    for (int i = 0; i < l; i++) {
+      h ^= unit(i);
+      h *= 0x100000001b3ull;
+    }
+    h = fmix64(h ^ (uint64_t)l);
+    h = h ? h : 1;
+    for (uint64_t s = h & fmask, probe = 0; probe <= fmask; probe++, s = (s + 1) & fmask) {
+      const unsigned long long k = fkeys[s];
+      if (k == 0) break;
+      if (k != h) continue;
+      const uint64_t os = cand_str[freps[s] - 1];
+      const uint16_t *o = pool + (os >> 16);
+      bool eq = (int)(os & 0xFFFF) == l;
+      for (int i = 0; i < l && eq; i++) eq = o[i] == unit(i);
+      if (eq) {
+        atomicAdd(bad, 1ull);
+        break;
+      }
+    }
+  }
+}
+// sorted word term i: its key (exact when it has <= 16 units, all < 256)
+__global__ void k_word_keys(const uint32_t *order, int64_t Vw, const uint64_t *vcs, const uint16_t *pool, Key16 *wkey,
+                            uint8_t *wexact) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < Vw; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t cs = vcs[order[i]];
+    const uint16_t *u = pool + (cs >> 16);
+    const int l = (int)(cs & 0xFFFF);
+    Key16 k{0, 0};
+    bool ex = l <= 16;
+    for (int x = 0; x < 16; x++) {
+      const uint32_t c = x < l ? u[x] : 0u;
+      ex = ex && c < 256u;
+      const uint64_t b = c < 256u ? c : 255u;  // (saturated: the key then only bounds, compare the strings)
+      if (x < 8) k.hi |= b << (56 - 8 * x);
+      else k.lo |= b << (56 - 8 * (x - 8));
+    }
+    wkey[i] = k;
+    wexact[i] = ex;
+  }
+}
+// String.compareTo(word term, docid term)
+__device__ int cmp_word_docid(const uint16_t *pool, uint64_t cs, const uint8_t *text, uint64_t ds) {
+  const uint16_t *w = pool + (cs >> 16);
+  const uint8_t *p = text + (ds >> 8);
+  const int wl = (int)(cs & 0xFFFF), dl = (int)(ds & 0xFF), m = wl < dl ? wl : dl;
+  for (int i = 0; i < m; i++) {
+    const int d = (int)w[i] - (int)lower_ascii(p[i]);
+    if (d) return d;
+  }
+  return wl - dl;
+}
+__device__ __forceinline__ int cmp_wd(const Key16 &wk, bool wex, const uint16_t *pool, uint64_t cs, const Key16 &dk,
+                                      const uint8_t *text, uint64_t ds) {
+  if (wex && (ds & 0xFF) <= 16) return cmp_key16(wk, dk);
+  return cmp_word_docid(pool, cs, text, ds);
+}
+// merged ranks: word i -> i + (docid terms below it); docid j -> j + (words below it)
+__global__ void k_word_rank(const uint32_t *order, int64_t Vw, const uint32_t *vslot, const uint64_t *vcs,
+                            const uint16_t *pool, const Key16 *wkey, const uint8_t *wexact, const Key16 *dkey,
+                            const uint64_t *dsrc, int64_t Vd, const uint8_t *text, int32_t *rank_of_slot,
+                            int64_t *term_len, int64_t *wrank) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < Vw; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t o = order[i];
+    const uint64_t cs = vcs[o];
+    const Key16 wk = wkey[i];
+    const bool wex = wexact[i];
+    int64_t lo = 0, hi = Vd;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (cmp_wd(wk, wex, pool, cs, dkey[mid], text, dsrc[mid]) > 0) lo = mid + 1;
+      else hi = mid;
+    }
+    const int64_t rk = i + lo;
+    rank_of_slot[vslot[o]] = (int32_t)rk;
+    term_len[rk] = (int64_t)(cs & 0xFFFF);
+    wrank[i] = rk;
+  }
+}
+__global__ void k_docid_rank(const Key16 *dkey, const uint64_t *dsrc, int64_t Vd, const uint32_t *order, int64_t Vw,
+                             const uint64_t *vcs, const uint16_t *pool, const Key16 *wkey, const uint8_t *wexact,
+                             const uint8_t *text, int64_t *term_len, int64_t *drank) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < Vd; j += (int64_t)gridDim.x * blockDim.x) {
+    const Key16 dk = dkey[j];
+    const uint64_t ds = dsrc[j];
+    int64_t lo = 0, hi = Vw;  // words below docid term j
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (cmp_wd(wkey[mid], wexact[mid], pool, vcs[order[mid]], dk, text, ds) < 0) lo = mid + 1;
+      else hi = mid;
+    }
+    const int64_t rk = j + lo;
+    term_len[rk] = (int64_t)(ds & 0xFF);
+    drank[j] = rk;
+  }
+}
+// term chars in rank order: the word terms' from the pool, the docid terms'
+// lowercase bytes from the text
+__global__ __launch_bounds__(256) void k_word_gather(const uint32_t *__restrict__ order, int64_t Vw,
+                                                     const uint64_t *__restrict__ vcs,
+                                                     const uint16_t *__restrict__ pool,
+                                                     const int64_t *__restrict__ wrank,
+                                                     const int64_t *__restrict__ term_off,
+                                                     uint16_t *__restrict__ term_chars) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < Vw; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t cs = vcs[order[i]];
+    const uint16_t *w = pool + (cs >> 16);
+    const int l = (int)(cs & 0xFFFF);
+    uint16_t *d = term_chars + term_off[wrank[i]];
+    for (int k0 = 0; k0 < l; k0 += 8) {
+      uint16_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[k] = k0 + k < l ? w[k0 + k] : (uint16_t)0;
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (k0 + k < l) d[k0 + k] = v[k];
+    }
+  }
+}
+__global__ void k_docid_gather(const uint64_t *dsrc, const Key16 *dkey, int64_t Vd, const int64_t *drank,
+                               const uint8_t *text, const int64_t *term_off, uint16_t *term_chars) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < Vd; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t *p = text + (dsrc[j] >> 8);
+    const int l = (int)(dsrc[j] & 0xFF);
+    uint16_t *d = term_chars + term_off[drank[j]];
+    if (l <= 16) {
+      const Key16 kj = dkey[j];
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (k < l) d[k] = (uint16_t)key16_byte(kj, k);
+    } else {
+      for (int k = 0; k < l; k++) d[k] = lower_ascii(p[k]);
+    }
+  }
+}
+// raw slot -> term id of the docid terms (one term each)
+__global__ void k_docid_raw(const int32_t *dl, int64_t Vd, const int32_t *dslot, const int64_t *drank,
+                            int32_t *raw_term, int32_t *raw_nout) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < Vd; j += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t s = dslot[dl[j]];
+    raw_term[s] = (int32_t)drank[j];
+    raw_nout[s] = 1;
+  }
+}
+
 // ============================================================================
 constexpr int kAggNT = 256;
 constexpr int kAggCap = 4096;    // LDS table entries
@@ -2899,7 +3225,7 @@ enum {
   W_TOK, W_NTOK, W_RKEYS, W_RREPS, W_POOL, W_CKEY, W_CSTR, W_NOUT, W_LONG, W_FKEYS, W_FREPS, W_CFINAL,
   W_VSLOT, W_KHI, W_KLO, W_VIDX, W_T0, W_T1, W_T2, W_T3, W_RAWTERM, W_MULTI, W_PERM, W_PREC, W_PTERM, W_PVAL,
   W_MAXNOUT, W_SS, W_SE, W_SC, W_RLIST, W_RFLAG, W_POFF, W_OVFKEY, W_FREC, W_LT, W_RADIX, W_NTOK2, W_BIGL2,
-  W_BIGCAP, W_SEGB, W_VCS,
+  W_BIGCAP, W_SEGB, W_VCS, W_DMARK, W_DSLOT, W_DLIST, W_DSRC, W_DKEY, W_WRANK, W_DSPAN, W_RLISTW,
   W_NSLOTS
 };
 constexpr int kBuildWs = 64;  // build slots live at ctx->ws[64..127]
@@ -3032,11 +3358,13 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
 
   // ---------------- K2 docno ----------------
   int32_t *docno = W[W_DOCNO].as<int32_t>(nR + 1);
+  uint64_t *dspan = job == 0 ? W[W_DSPAN].as<uint64_t>(nR + 1) : nullptr;  // (text offset << 8 | length) of each docid
   SME_HIP(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned long long), st));
   if (nR > 0 && job == 0) {
     hipLaunchKernelGGL(k_docno, dim3(grid_for(nR)), dim3(256), 0, st, t, (int64_t)n, rs, re, nR,
                        (const uint16_t *)cx->map_chars.p, (const int64_t *)cx->map_off.p, cx->map_n,
-                       cx->map_hash_ok ? (const uint32_t *)cx->map_slots.p : nullptr, cx->map_mask, docno, cnt);
+                       cx->map_hash_ok ? (const uint32_t *)cx->map_slots.p : nullptr, cx->map_mask, docno, cnt,
+                       dspan);
     SME_CHECK_LAUNCH();
   } else if (nR > 0) {
     hipLaunchKernelGGL(k_iota_docno, dim3(grid_for(nR)), dim3(256), 0, st, docno, nR);
@@ -3170,14 +3498,67 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
 
   // ---------------- K4 vocabulary ----------------
   // distinct raw tokens -> rlist (ascending slot order)
-  int32_t *rlist = W[W_RLIST].as<int32_t>(rcap);
-  const int64_t nraw = h_nsel;
+  int32_t *const rlist_all = W[W_RLIST].as<int32_t>(rcap);
+  const int64_t nraw_all = h_nsel;
   // next build's raw table: load <= 40 % (fewer probe collisions: c2 tokenizes in 9.2 ms at 8 M
   // slots vs 10.0 ms at 4 M; option raw_load_pct)
   {
     const uint64_t pct = (uint64_t)std::max<int64_t>(10, std::min<int64_t>(90, cx->opt_raw_load_pct));
-    cx->raw_cap_hint = next_pow2(std::max<uint64_t>(1ull << 20, (uint64_t)nraw * 100 / pct + 1));
+    cx->raw_cap_hint = next_pow2(std::max<uint64_t>(1ull << 20, (uint64_t)nraw_all * 100 / pct + 1));
   }
+  // ---------------- K4b docid terms (before the vocabulary: their raw slots skip it) ----------------
+  bool dfast = cx->opt_docid_terms != 0 && nR > 0 && nraw_all > 0 && dspan != nullptr;
+  int32_t *rlist_w = nullptr;  // the raw slots of the word vocabulary (no docid term's)
+  int64_t nraw_w = 0;
+  uint32_t *dmark = nullptr;
+  int32_t *dslot = nullptr, *dl = nullptr;
+  uint64_t *dsrc = nullptr;
+  Key16 *dkey = nullptr;
+  int64_t Vd = 0;
+  if (dfast) {
+    unsigned long long *dcnt = reinterpret_cast<unsigned long long *>(W[W_DSRC].as<uint64_t>(4));  // (reallocated below)
+    dmark = W[W_DMARK].as<uint32_t>(rcap);
+    dslot = W[W_DSLOT].as<int32_t>(nR + 1);
+    SME_HIP(hipMemsetAsync(dmark, 0xFF, rcap * sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_docid_slots, dim3(grid_for(nR)), dim3(256), 0, st, t, (int64_t)n, dspan, nR, tb, dslot,
+                       dmark);
+    uint8_t *dflag = reinterpret_cast<uint8_t *>(W[W_DKEY].as<Key16>(nR / 16 + 1));
+    hipLaunchKernelGGL(k_docid_flags, dim3(grid_for(nR)), dim3(256), 0, st, dslot, nR, dflag);
+    dl = W[W_DLIST].as<int32_t>(nR + 1);
+    SME_HIP(hipMemsetAsync(dcnt, 0, 4 * sizeof(unsigned long long), st));
+    select_flagged(dflag, nR, dl, reinterpret_cast<int32_t *>(dcnt), cx->ws[25], cx->ws[23], st);
+    SME_CHECK_LAUNCH();
+    Vd = (int64_t)(int32_t)(uint32_t)d2h(dcnt, st);
+    if (Vd > 0) {
+      dsrc = W[W_DSRC].as<uint64_t>(Vd + 4);
+      dkey = W[W_DKEY].as<Key16>(Vd);
+      unsigned long long *bad = reinterpret_cast<unsigned long long *>(dsrc + Vd);
+      SME_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned long long), st));
+      hipLaunchKernelGGL(k_docid_keys, dim3(grid_for(Vd)), dim3(256), 0, st, dl, Vd, dspan, t, (int64_t)n, dsrc, dkey);
+      hipLaunchKernelGGL(k_docid_ascending, dim3(grid_for(Vd)), dim3(256), 0, st, dkey, dsrc, Vd, t, bad);
+      SME_CHECK_LAUNCH();
+      if (d2h(bad, st) != 0) dfast = false;  // not in ascending order in the file (or equal terms): general path
+    } else {
+      dfast = false;
+    }
+    if (dfast) {  // the word vocabulary's raw slots
+      uint8_t *wflag = W[W_RFLAG].as<uint8_t>(rcap);
+      rlist_w = W[W_RLISTW].as<int32_t>(rcap);
+      unsigned long long *wcnt = reinterpret_cast<unsigned long long *>(dsrc + Vd + 1);
+      SME_HIP(hipMemsetAsync(wcnt, 0, sizeof(unsigned long long), st));
+      hipLaunchKernelGGL(k_raw_flags_words, dim3(grid_for((int64_t)rcap)), dim3(256), 0, st, tb.key, dmark, rcap,
+                         wflag);
+      select_flagged(wflag, (int64_t)rcap, rlist_w, reinterpret_cast<int32_t *>(wcnt), cx->ws[25], cx->ws[23], st);
+      SME_CHECK_LAUNCH();
+      nraw_w = (int64_t)(int32_t)(uint32_t)d2h(wcnt, st);
+    }
+  }
+  prof.mark("docid_terms");
+  const int32_t *rlist = rlist_all;
+  int64_t nraw = nraw_all;
+vocab_again:  // (a docid term equal to a word term: the general path, from here)
+  rlist = dfast ? rlist_w : rlist_all;
+  nraw = dfast ? nraw_w : nraw_all;
   int64_t *poff = W[W_POFF].as<int64_t>(nraw + 1);
   {
     int64_t *lens = W[W_T0].as<int64_t>(nraw + 1);
@@ -3267,9 +3648,21 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   SME_HIP(hipMemcpyAsync(hv, cnt, sizeof hv, hipMemcpyDeviceToHost, st));
   SME_HIP(hipStreamSynchronize(st));
   if (d2h(ovf, st)) throw Error(SME_ELIMIT, "final term table overflow");
-  const int64_t V = (int64_t)hv[1];
+  const int64_t Vw = (int64_t)hv[1];  // word terms (docid terms of K4b: Vd more)
   const int term_maxlen = (int)(int32_t)(uint32_t)hv[12];
   const bool term_wide = (hv[12] >> 32) != 0;  // maxlen + 1: a term has a unit >= 128
+  if (dfast) {  // a docid term equal to a word term (e.g. the docid also in lowercase in a text): general path
+    unsigned long long *bad = reinterpret_cast<unsigned long long *>(dsrc + Vd);
+    SME_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_docid_collide, dim3(grid_for(Vd)), dim3(256), 0, st, dsrc, dkey, Vd, t, co.pool,
+                       co.cand_str, fkeys, freps, fcap - 1, bad);
+    SME_CHECK_LAUNCH();
+    if (d2h(bad, st) != 0) {
+      dfast = false;
+      goto vocab_again;
+    }
+  }
+  const int64_t V = Vw + (dfast ? Vd : 0);  // all terms
 
   sme_index *ix = new sme_index(cx);
   std::unique_ptr<sme_index> ix_guard(ix);  // freed (back to the pool) if a later stage throws
@@ -3280,18 +3673,18 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   ix->V = V;
 
   int32_t *rank_of_slot = W[W_T3].as<int32_t>(fcap);
-  uint32_t *order = W[W_T2].as<uint32_t>(V + 1);
+  uint32_t *order = W[W_T2].as<uint32_t>(Vw + 1);
   int64_t *term_off = ix->d_term_off.as<int64_t>(V + 1);
-  if (V > 0) {
+  if (Vw > 0) {
     // LSD radix sort of the vocabulary in String.compareTo order: 4 UTF-16 units per
     // 64-bit key word, least significant word first, stable; terms are at most
     // 99 units and all words below the longest term's length are sorted.
     // (9 ASCII units of 7 bits per word when no unit is >= 128)
     const int cpw = term_wide ? 4 : 9, ub = term_wide ? 16 : 7, kbits = cpw * ub;
     const int nwords = std::min(8, (std::max(term_maxlen, 1) + cpw - 1) / cpw);
-    uint64_t *kw = W[W_KHI].as<uint64_t>(V), *kw2 = W[W_KLO].as<uint64_t>(V);
+    uint64_t *kw = W[W_KHI].as<uint64_t>(Vw), *kw2 = W[W_KLO].as<uint64_t>(Vw);
     uint32_t *ord_a = vidx, *ord_b = order;
-    uint32_t *rscr = W[W_RADIX].as<uint32_t>(kv_sort_scratch(V) / sizeof(uint32_t) + 1);
+    uint32_t *rscr = W[W_RADIX].as<uint32_t>(kv_sort_scratch(Vw) / sizeof(uint32_t) + 1);
     bool done = false;
     if (!term_wide && nwords > 1) {
       // ONE key word of the first cpw2 units, in ceil(log2(alphabet + 1)) bits each,
@@ -3310,42 +3703,69 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
       if (cpw2 > cpw) {
         uint8_t *code = reinterpret_cast<uint8_t *>(W[W_SEGB].as<uint64_t>(16));
         SME_HIP(hipMemcpyAsync(code, code_h, 128, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_term_code, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V, vcs, co.pool, code, cpw2, ub2,
+        hipLaunchKernelGGL(k_term_code, dim3(grid_for(Vw)), dim3(256), 0, st, ord_a, Vw, vcs, co.pool, code, cpw2, ub2,
                            kw);
-        uint32_t *so = kv_sort<uint64_t>(kw, ord_a, kw2, ord_b, V, cpw2 * ub2, rscr, st, true);
+        uint32_t *so = kv_sort<uint64_t>(kw, ord_a, kw2, ord_b, Vw, cpw2 * ub2, rscr, st, true);
         const uint64_t *sk = so == ord_a ? kw : kw2;
         unsigned int mr = 0;
         if (term_maxlen > cpw2) {
           unsigned int *d_mr = pres;
           SME_HIP(hipMemsetAsync(d_mr, 0, sizeof(unsigned int), st));
-          hipLaunchKernelGGL(k_key_runs, dim3(grid_for(V)), dim3(256), 0, st, sk, V, d_mr);
+          hipLaunchKernelGGL(k_key_runs, dim3(grid_for(Vw)), dim3(256), 0, st, sk, Vw, d_mr);
           mr = d2h(d_mr, st);
         }
         if (mr <= 64) {
-          if (mr > 1) hipLaunchKernelGGL(k_key_fixup, dim3(grid_for(V)), dim3(256), 0, st, sk, V, so, vcs, co.pool);
-          if (so != order) SME_HIP(hipMemcpyAsync(order, so, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+          if (mr > 1) hipLaunchKernelGGL(k_key_fixup, dim3(grid_for(Vw)), dim3(256), 0, st, sk, Vw, so, vcs, co.pool);
+          if (so != order) SME_HIP(hipMemcpyAsync(order, so, Vw * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
           done = true;
         } else {
-          hipLaunchKernelGGL(k_iota_u32, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V);  // start over
+          hipLaunchKernelGGL(k_iota_u32, dim3(grid_for(Vw)), dim3(256), 0, st, ord_a, Vw);  // start over
         }
       }
     }
     for (int w = nwords - 1; w >= 0 && !done; w--) {
-      hipLaunchKernelGGL(k_term_word, dim3(grid_for(V)), dim3(256), 0, st, ord_a, V, vcs, co.pool, w, cpw, ub, kw);
-      if (kv_sort<uint64_t>(kw, ord_a, kw2, ord_b, V, kbits, rscr, st) != ord_a) std::swap(ord_a, ord_b);
+      hipLaunchKernelGGL(k_term_word, dim3(grid_for(Vw)), dim3(256), 0, st, ord_a, Vw, vcs, co.pool, w, cpw, ub, kw);
+      if (kv_sort<uint64_t>(kw, ord_a, kw2, ord_b, Vw, kbits, rscr, st) != ord_a) std::swap(ord_a, ord_b);
     }
     if (!done && ord_a != order)
-      SME_HIP(hipMemcpyAsync(order, ord_a, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+      SME_HIP(hipMemcpyAsync(order, ord_a, Vw * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     if (term_maxlen > 32)
-      hipLaunchKernelGGL(k_final_fixup, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, freps, co.cand_str,
+      hipLaunchKernelGGL(k_final_fixup, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vslot, freps, co.cand_str,
                          co.pool);
+  }
+  int64_t *drank = nullptr;
+  if (V > 0 && !dfast) {
+    int64_t *tlen = W[W_T0].as<int64_t>(Vw + 1);
+    hipLaunchKernelGGL(k_final_rank, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vslot, vcs, rank_of_slot, tlen);
+    SME_HIP(hipMemsetAsync(tlen + Vw, 0, sizeof(int64_t), st));
+    excl_scan(tlen, term_off, (int64_t)(Vw + 1), cx->ws[23], st);
+    int64_t tchars = d2h(term_off + Vw, st);
+    uint16_t *term_chars = ix->d_term_chars.as<uint16_t>(tchars + 1);
+    hipLaunchKernelGGL(k_final_gather, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vcs, co.pool, term_off,
+                       term_chars);
+    SME_CHECK_LAUNCH();
+  } else if (V > 0) {
+    // K4b: the sorted word terms and the (ascending) docid terms merged by rank
     int64_t *tlen = W[W_T0].as<int64_t>(V + 1);
-    hipLaunchKernelGGL(k_final_rank, dim3(grid_for(V)), dim3(256), 0, st, order, V, vslot, vcs, rank_of_slot, tlen);
+    Key16 *wkey = W[W_KLO].as<Key16>(Vw + 1);  // (the word sort's second key array: free again)
+    uint8_t *wexact = reinterpret_cast<uint8_t *>(W[W_T1].as<uint64_t>(Vw / 8 + 2));
+    int64_t *wrank = W[W_WRANK].as<int64_t>(Vw + Vd + 1);
+    drank = wrank + Vw;
+    if (Vw > 0) {
+      hipLaunchKernelGGL(k_word_keys, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vcs, co.pool, wkey, wexact);
+      hipLaunchKernelGGL(k_word_rank, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vslot, vcs, co.pool, wkey,
+                         wexact, dkey, dsrc, Vd, t, rank_of_slot, tlen, wrank);
+    }
+    hipLaunchKernelGGL(k_docid_rank, dim3(grid_for(Vd)), dim3(256), 0, st, dkey, dsrc, Vd, order, Vw, vcs, co.pool,
+                       wkey, wexact, t, tlen, drank);
     SME_HIP(hipMemsetAsync(tlen + V, 0, sizeof(int64_t), st));
     excl_scan(tlen, term_off, (int64_t)(V + 1), cx->ws[23], st);
     int64_t tchars = d2h(term_off + V, st);
     uint16_t *term_chars = ix->d_term_chars.as<uint16_t>(tchars + 1);
-    hipLaunchKernelGGL(k_final_gather, dim3(grid_for(V)), dim3(256), 0, st, order, V, vcs, co.pool, term_off,
+    if (Vw > 0)
+      hipLaunchKernelGGL(k_word_gather, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vcs, co.pool, wrank, term_off,
+                         term_chars);
+    hipLaunchKernelGGL(k_docid_gather, dim3(grid_for(Vd)), dim3(256), 0, st, dsrc, dkey, Vd, drank, t, term_off,
                        term_chars);
     SME_CHECK_LAUNCH();
   } else {
@@ -3359,6 +3779,8 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   if (nraw > 0)
     hipLaunchKernelGGL(k_raw_term, dim3(grid_for(nraw)), dim3(256), 0, st, rlist, nraw, cand_final, rank_of_slot,
                        co.raw_nout, raw_term);
+  if (dfast)
+    hipLaunchKernelGGL(k_docid_raw, dim3(grid_for(Vd)), dim3(256), 0, st, dl, Vd, dslot, drank, raw_term, co.raw_nout);
   if (novf > 0) {
     uint64_t *ok2 = W[W_T0].as<uint64_t>(novf);
     uint32_t *oi = W[W_T1].as<uint32_t>(novf), *oi2 = W[W_VIDX].as<uint32_t>(novf);

@@ -53,6 +53,7 @@ struct sme_ctx {
   int64_t opt_agg_two_pass = 0;   // "agg_two_pass": 1 = count + emit aggregation passes
   int64_t opt_tok_grid = 4096;    // "tok_grid": tokenizer workgroups (>= 1)
   int64_t opt_raw_load_pct = 40;  // "raw_load_pct": raw-vocabulary table load of the next build (10..90)
+  int64_t opt_docid_terms = 1;    // "docid_terms": docid terms beside the word vocabulary (K4b; 0 = general path)
   int64_t opt_cand_cap = 1024;    // "cand_cap": candidate list per query of k_query_win (1..2048; >= 1024: at least 16 k)
   int64_t opt_seed_m = 64;        // "seed_m": seed postings per term (k_query_seed; 0 = no seed)
   int64_t opt_kgram_rank = 0;     // "kgram_rank": 1 = K >= 2 gram keys by iterated ranking even when packed ids fit

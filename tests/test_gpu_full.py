@@ -14,7 +14,8 @@ made by tools/gen_full_golden.py.  Here the device builds the same corpus in HBM
   * per query batch -- configs[2]'s full 100,000-query c3 batch (2-8 terms drawn by
     df, top-10), its uniform-vocabulary variant, 2,000 top-100; c5's 1,000,000
     top-100 batch, answered whole, of which the golden holds the first 50,000
-    queries' rows (the CPU port needs hours for all of them) -- the sha256 of every
+    queries' rows and every 20th row (50,000 more, spread over the batch; the CPU
+    port needs hours for all of them) -- the sha256 of every
     docno and every fp64 score bit (docno tie-break, reference idf mode).
 """
 import hashlib
@@ -75,10 +76,12 @@ def test_full_config_digests(sme, synth, name):
         tids, qoff = synth.queries_by_df(df, group["n"], seed=group["seed"], uniform=(group["kind"] == "uniform"))
         assert _sha(tids.astype("<i4"), qoff.astype("<i8")) == group["terms_sha256"]
         d, s = ix.query_topk(tids, qoff, group["k"])
-        nc = group.get("checked", group["n"])  # leading queries the golden scored (c5: 50,000 of the 1 M)
-        d, s = d[:nc], s[:nc]
+        nc = group.get("checked", group["n"])  # rows the golden scored (c5: 50,000 of the 1 M)
+        stride = group.get("stride", 1)  # (c5: the leading 50,000 and every 20th row)
+        d, s = d[::stride][:nc], s[::stride][:nc]
         if _sha(d.astype("<i4"), s.astype("<f8")) != group["result_sha256"]:
-            bad = _first_mismatch(group, d, s, lambda q: [ix.term(int(t)) for t in tids[qoff[q]:qoff[q + 1]]])
+            bad = _first_mismatch(group, d, s, lambda q: [ix.term(int(t)) for t in
+                                                          tids[qoff[q * stride]:qoff[q * stride + 1]]])
             pytest.fail("%s %s batch (%d queries, top-%d) differs from the golden; first listed mismatch: %r"
                         % (name, group["kind"], group["n"], group["k"], bad))
     ix.close()

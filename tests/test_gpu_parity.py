@@ -840,3 +840,46 @@ def test_c1_sample_on_device(sme, tmp_path):
         rd, rs = ref.query(tl, 10, 0, 0)
         assert [d for d, _ in top] == rd and [s for _, s in top] == rs, tl
         assert dn[q, :len(rd)].tolist() == rd and sc[q, :len(rd)].tolist() == rs, tl
+
+
+def _trec(docs):
+    return "".join("<DOC>\n<DOCNO> %s </DOCNO>\n<TEXT>\n%s\n</TEXT>\n</DOC>\n" % (d, body) for d, body in docs).encode()
+
+
+@pytest.mark.parametrize("case", ["ascending", "shuffled", "mixed_forms", "case_twins", "docid_in_text",
+                                  "duplicates"])
+@pytest.mark.parametrize("docid_terms", [1, 0])
+def test_build_docid_terms(sme, synth, case, docid_terms):
+    """K4b: docid terms (T7) beside the word vocabulary.  A record's DOCNO token
+    that is its own term (ASCII letters and digits ending in a digit, unchanged by
+    Porter2) skips the per-distinct vocabulary work and is ranked by a merge with
+    the sorted word terms when the docids ascend in file order; otherwise (docids
+    out of order, two raw forms of one term, a docid term also a word term) the
+    build stays on the general path.  Either way the partition records and the
+    term strings equal the oracle's (TrecDocument.java:94-96: the DOCNO text is
+    indexed), with the option on and off."""
+    g = np.random.default_rng(hash(case) & 0xFFFF)
+    words = ["alpha", "bravo", "charlie", "delta", "echo", "foxtrot", "golf", "hotel", "india", "kilo", "lima", "zulu",
+             "running", "ponies", "x9", "abc123", "42"]
+    n = 300
+    ids = ["D%09d" % (1000 + 3 * i) for i in range(n)]
+    bodies = [" ".join(g.choice(words, size=int(g.integers(5, 40)))) for _ in range(n)]
+    if case == "shuffled":
+        perm = g.permutation(n)
+        ids = [ids[i] for i in perm]
+    elif case == "mixed_forms":
+        forms = ["LA%06d-%04d", "ab%d", "XY%d", "FT%dA", "doc.%d", "%d"]
+        ids = sorted(forms[i % len(forms)] % ((i,) if forms[i % len(forms)].count("%") == 1 else (i, i)) for i in
+                     range(n))
+    elif case == "case_twins":
+        ids = ["d%09d" % (1000 + 3 * i) if i == 7 else ids[i] for i in range(n)]
+        ids[8] = "D%09d" % (1000 + 3 * 7)  # the same term as record 7's, another raw form
+    elif case == "docid_in_text":
+        bodies[5] += " " + ids[200].lower() + " " + ids[100]  # a word equal to a docid term; a docid in a body
+    elif case == "duplicates":
+        ids[11] = ids[10]
+        ids[50] = ids[49]
+    c = _trec(list(zip(ids, bodies)))
+    mapping = sorted(set(ids))
+    _check_build(sme, c, mapping, R=1, opts={"docid_terms": docid_terms})
+    _check_build(sme, c, mapping, R=7, opts={"docid_terms": docid_terms})

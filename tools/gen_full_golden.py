@@ -19,6 +19,8 @@ full c2 corpus in about a minute here.  Recorded per configuration:
           its uniform-vocabulary variant (seed 8), 2,000 top-100 (seed 17)
   c5full  configs[4]: 8,841,823 passages x U[40,72] tokens, V_w = 30,000, seed 9;
           the 1,000,000-query top-100 batch (seed 9): its first 50,000 queries' results
+          and a strided sample (every 20th query, 50,000 rows), so the late window
+          stages and the lists that overflow anywhere in the batch are pinned too
 
 Run from the repo root (8 threads, ~25 GB of host memory for c5full):
     python tools/gen_full_golden.py [c2full] [c5full]
@@ -44,7 +46,8 @@ CONFIGS = {
     # c5: the 1 M batch is drawn in full (its terms digest covers all of it), the CPU
     # scores its first 50,000 queries (all 1 M take the CPU port many hours); the GPU
     # test answers the whole batch and compares those rows
-    "c5full": dict(n=8_841_823, V=30_000, seed=9, lo=40, hi=72, queries=[("df", 1_000_000, 9, 100, 50_000)]),
+    "c5full": dict(n=8_841_823, V=30_000, seed=9, lo=40, hi=72,
+                   queries=[("df", 1_000_000, 9, 100, 50_000), ("df", 1_000_000, 9, 100, 50_000, 20)]),
 }
 NSHOW = 20
 
@@ -98,15 +101,27 @@ def main(names):
         del dn, tf
         for qspec in cfg["queries"]:
             kind, nq, seed, k = qspec[:4]
-            nc = qspec[4] if len(qspec) > 4 else nq  # leading queries scored here
+            nc = qspec[4] if len(qspec) > 4 else nq  # queries scored here
+            stride = qspec[5] if len(qspec) > 5 else 1  # rows 0, stride, 2 stride, ... (else the leading nc)
             tq = time.time()
             tids, qoff = synth.queries_by_df(df, nq, seed=seed, uniform=(kind == "uniform"))
-            d, s, _ = ix.query(tids[:qoff[nc]], qoff[:nc + 1], k, 0, threads)
-            show = [[[terms[t] for t in tids[qoff[q]:qoff[q + 1]]], d[q].tolist(), [float(x).hex() for x in s[q]]]
-                    for q in range(min(NSHOW, nc))]
-            out["queries"].append({"kind": kind, "n": nq, "checked": nc, "seed": seed, "k": k, "idf_mode": 0,
-                                   "terms_sha256": sha(tids.astype("<i4"), qoff.astype("<i8")),
-                                   "result_sha256": sha(d.astype("<i4"), s.astype("<f8")), "first": show})
+            rows = np.arange(nc, dtype=np.int64) * stride
+            if stride == 1:
+                st, so = tids[:qoff[nc]], qoff[:nc + 1]
+            else:
+                lens = qoff[rows + 1] - qoff[rows]
+                so = np.zeros(nc + 1, np.int64)
+                so[1:] = np.cumsum(lens)
+                st = np.concatenate([tids[qoff[q]:qoff[q + 1]] for q in rows]).astype(tids.dtype)
+            d, s, _ = ix.query(st, so, k, 0, threads)
+            show = [[[terms[t] for t in st[so[i]:so[i + 1]]], d[i].tolist(), [float(x).hex() for x in s[i]]]
+                    for i in range(min(NSHOW, nc))]
+            grp = {"kind": kind, "n": nq, "checked": nc, "seed": seed, "k": k, "idf_mode": 0,
+                   "terms_sha256": sha(tids.astype("<i4"), qoff.astype("<i8")),
+                   "result_sha256": sha(d.astype("<i4"), s.astype("<f8")), "first": show}
+            if stride > 1:
+                grp["stride"] = stride
+            out["queries"].append(grp)
             print("  %s %d of %d queries top-%d: %.1f s" % (kind, nc, nq, k, time.time() - tq), flush=True)
         path = os.path.join(ROOT, "tests", "golden", "full_%s.json" % name[:2])
         with open(path, "w") as f:
