@@ -110,6 +110,8 @@ void sme_destroy(sme_ctx *ctx);
  *                   digits ending in a digit, unchanged by the stemmer) skips the per-distinct
  *                   vocabulary work and is ranked by a merge with the sorted word terms when the
  *                   docids ascend in file order; 0: every raw token through the general path
+ *   "sort_digit_bits"  most bits per digit of the term sort's LSD passes, 6..11 (default 11:
+ *                   two passes for up to 2^22 terms)
  *   "query_table_budget"  bytes a batch's skip table may take (default 0 =
  *                   a quarter of the free HBM); a batch over it is split by
  *                   query range, and queries still overflowing their

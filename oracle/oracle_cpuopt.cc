@@ -59,7 +59,8 @@ struct U16Hash {
 
 struct CpuIndex {
   int64_t N = 0, V = 0, P = 0;
-  std::vector<u16s> terms;           // TermDF order
+  std::vector<int64_t> toff;         // term strings, TermDF order: units [toff[t], toff[t + 1])
+  std::vector<char16_t> tchars;
   std::vector<int64_t> off;          // V + 1
   std::vector<int32_t> docno, tf;    // reduce order: tf desc, docno asc
   double build_s = 0;
@@ -338,6 +339,90 @@ struct RawTab {
   }
 };
 
+// raw-token bytes of the normalize fast path: ASCII letters, digits, apostrophe
+struct AlnumApoTab {
+  bool t[256];
+  AlnumApoTab() {
+    for (int c = 0; c < 256; c++)
+      t[c] = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '\'';
+  }
+};
+const AlnumApoTab kAlnumApo;
+
+// the stopword list (GalagoTokenizer's, oracle_tok.c) as an open-addressing set
+// of ASCII words of <= 16 units keyed by their bytes (every stopword is ASCII
+// and shorter; checked when the table is built)
+struct StopTab {
+  struct E {
+    uint64_t w0, w1;
+    int32_t len;
+  };
+  std::vector<E> e;
+  uint64_t mask = 0;
+  static uint64_t h(uint64_t w0, uint64_t w1, int32_t n) {
+    uint64_t x = (w0 ^ 0x9E3779B97F4A7C15ull ^ (uint64_t)n) * 0xFF51AFD7ED558CCDull;
+    x = (x ^ (x >> 31) ^ w1) * 0xC4CEB9FE1A85EC53ull;
+    return x ^ (x >> 29);
+  }
+  static void pack(const uint16_t *w, int32_t n, uint64_t *w0, uint64_t *w1) {
+    uint64_t a = 0, b = 0;
+    for (int32_t i = 0; i < n && i < 8; i++) a |= (uint64_t)(uint8_t)w[i] << (8 * i);
+    for (int32_t i = 8; i < n; i++) b |= (uint64_t)(uint8_t)w[i] << (8 * (i - 8));
+    *w0 = a;
+    *w1 = b;
+  }
+  StopTab() {
+    const int cnt = or_stopword_count();
+    e.assign(1024, E{0, 0, 0});
+    while (e.size() < (size_t)cnt * 4) e.resize(e.size() * 2);
+    mask = e.size() - 1;
+    for (int i = 0; i < cnt; i++) {
+      const char *s = or_stopword(i);
+      const int32_t n = (int32_t)strlen(s);
+      uint16_t w[16];
+      if (n > 16 || n == 0) abort();  // (never: the list is short ASCII words)
+      for (int32_t k = 0; k < n; k++) {
+        if ((unsigned char)s[k] >= 0x80) abort();
+        w[k] = (uint8_t)s[k];
+      }
+      uint64_t w0, w1;
+      pack(w, n, &w0, &w1);
+      uint64_t j = h(w0, w1, n) & mask;
+      while (e[j].len) j = (j + 1) & mask;
+      e[j] = E{w0, w1, n};
+    }
+  }
+  // w: ASCII units
+  bool has(const uint16_t *w, int32_t n) const {
+    if (n > 16) return false;
+    uint64_t w0, w1;
+    pack(w, n, &w0, &w1);
+    for (uint64_t j = h(w0, w1, n) & mask; e[j].len; j = (j + 1) & mask)
+      if (e[j].len == n && e[j].w0 == w0 && e[j].w1 == w1) return true;
+    return false;
+  }
+};
+const StopTab &stop_tab() {
+  static const StopTab t;
+  return t;
+}
+
+// bump allocator of UTF-16 units (pointers stay valid until it is destroyed)
+struct Arena {
+  std::vector<std::unique_ptr<char16_t[]>> blk;
+  size_t used = 0, cap = 0;
+  char16_t *take(size_t n) {
+    if (used + n > cap) {
+      cap = std::max<size_t>(n, (size_t)1 << 20);
+      blk.emplace_back(new char16_t[cap]);
+      used = 0;
+    }
+    char16_t *p = blk.back().get() + used;
+    used += n;
+    return p;
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -403,7 +488,11 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   //  3. per record (threads): local raw ids -> term ids -> tf
   const int nthr = omp_get_max_threads();
   std::vector<int32_t> rdocno((size_t)nR);
-  std::vector<std::vector<int32_t>> rtok((size_t)nR);   // local raw ids (simple records)
+  // a simple record's local raw ids: [rbeg[r], rbeg[r] + rcnt[r]) of its thread's
+  // buffer (one flat buffer per thread, no allocation per record)
+  std::vector<int64_t> rbeg((size_t)nR, 0);
+  std::vector<int32_t> rcnt((size_t)nR, 0);
+  std::vector<std::vector<int32_t>> tokb((size_t)nthr);
   std::vector<std::vector<u16s>> rterm((size_t)nR);     // terms (complex records)
   std::vector<int16_t> rthr((size_t)nR);
   std::vector<RawTab> tabs((size_t)nthr);
@@ -412,6 +501,8 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   {
     const int me = omp_get_thread_num();
     RawTab &raw = tabs[(size_t)me];
+    std::vector<int32_t> &tb = tokb[(size_t)me];
+    tb.reserve((size_t)(n / (size_t)nthr / 6 + 1024));
     struct Pend {
       const uint8_t *s;
       int64_t l;
@@ -465,7 +556,6 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
         // two passes over the record's tokens: bounds, head words and hashes with
         // the home slots prefetched, then the table lookups (the slots of the
         // record's tail tokens are in flight together instead of one miss each)
-        auto &out = rtok[(size_t)r];
         pend.clear();
         int64_t i = 0;
         while (i < len) {
@@ -493,9 +583,10 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
           pend.push_back(q);
           i = j;
         }
-        out.resize(pend.size());
+        rbeg[(size_t)r] = (int64_t)tb.size();
+        rcnt[(size_t)r] = (int32_t)pend.size();
         for (size_t k = 0; k < pend.size(); k++)
-          out[k] = raw.find_or_add(pend[k].s, pend[k].l, pend[k].h, pend[k].w0, pend[k].w1);
+          tb.push_back(raw.find_or_add(pend[k].s, pend[k].l, pend[k].h, pend[k].w0, pend[k].w1));
       } else {
         // complex markup: the oracle's TagTokenizer over the decoded record
         utf8_to_utf16(b, (size_t)len, &text);
@@ -566,27 +657,71 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
     for (size_t i = 0; i < tb.lp.size(); i++) lmap[(size_t)t][i] += (int32_t)sbase[(size_t)((tb.lh[i] >> 56) % kShards)];
   }
   std::vector<RawTab>().swap(shard);
-  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "merge", omp_get_wtime() - t0);
-  // processContent of each distinct raw token, once (parallel)
-  std::vector<std::vector<u16s>> gout((size_t)G);
+  std::vector<RawTab>().swap(tabs);
+  if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f (%lld distinct raw tokens)\n", "merge", omp_get_wtime() - t0, (long long)G);
+  // processContent of each distinct raw token, once (parallel).  A raw token of
+  // ASCII letters, digits and apostrophes is one TagTokenizer token whose fix
+  // (simpleFix; complexFix = simpleFix + toLowerCase on ASCII) lowercases it and
+  // drops the apostrophes (TagTokenizer.java:403-476); other raw tokens go through
+  // the oracle's TagTokenizer.  Outputs land in per-thread arenas as runs of
+  // (length, units): token g has gn[g] outputs starting at gp[g].
+  const StopTab &stab = stop_tab();
+  std::vector<int32_t> gn((size_t)G, 0);
+  std::vector<const char16_t *> gp((size_t)G, nullptr);
+  std::vector<Arena> arena((size_t)nthr);
 #pragma omp parallel
   {
+    Arena &ar = arena[(size_t)omp_get_thread_num()];
     jstr text, st;
     js_init(&text);
     js_init(&st);
     jstr_list toks;
     jl_init(&toks);
+    std::vector<u16s> outs;
+    uint16_t w16[128];
 #pragma omp for schedule(dynamic, 1024)
     for (int64_t g = 0; g < G; g++) {
-      utf8_to_utf16(glob.lp[(size_t)g], (size_t)glob.ll[(size_t)g], &text);
+      const uint8_t *s = glob.lp[(size_t)g];
+      const int32_t l = glob.ll[(size_t)g];
+      bool fast = l < 100;
+      for (int32_t i = 0; fast && i < l; i++) fast = kAlnumApo.t[s[i]];
+      if (fast) {
+        int32_t m = 0;
+        for (int32_t i = 0; i < l; i++) {
+          const uint8_t c = s[i];
+          if (c == '\'') continue;
+          w16[m++] = (uint16_t)((c >= 'A' && c <= 'Z') ? c + 32 : c);
+        }
+        if (m == 0 || stab.has(w16, m)) continue;  // (add_token drops an empty token)
+        or_stem_js(w16, m, &st);
+        char16_t *o = ar.take((size_t)st.n + 1);
+        o[0] = (char16_t)st.n;
+        memcpy(o + 1, st.p, (size_t)st.n * sizeof(uint16_t));
+        gn[(size_t)g] = 1;
+        gp[(size_t)g] = o;
+        continue;
+      }
+      utf8_to_utf16(s, (size_t)l, &text);
       for (int i = 0; i < toks.n; i++) js_free(&toks.v[i]);
       toks.n = 0;
       or_tag_tokenize(text.p, text.n, &toks);
+      outs.clear();
+      size_t tot = 0;
       for (int i = 0; i < toks.n; i++) {
         u16s w((const char16_t *)toks.v[i].p, (size_t)toks.v[i].n);
         if (stop.count(w)) continue;
         or_stem_js(toks.v[i].p, toks.v[i].n, &st);
-        gout[(size_t)g].emplace_back((const char16_t *)st.p, (size_t)st.n);
+        outs.emplace_back((const char16_t *)st.p, (size_t)st.n);
+        tot += (size_t)st.n + 1;
+      }
+      if (outs.empty()) continue;
+      char16_t *o = ar.take(tot);
+      gp[(size_t)g] = o;
+      gn[(size_t)g] = (int32_t)outs.size();
+      for (const u16s &w : outs) {
+        o[0] = (char16_t)w.size();  // (a token is < 100 units: add_token)
+        memcpy(o + 1, w.data(), w.size() * sizeof(char16_t));
+        o += w.size() + 1;
       }
     }
     jl_free(&toks);
@@ -594,18 +729,19 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
     js_free(&st);
   }
   if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "normalize", omp_get_wtime() - t0);
-  // vocabulary in String.compareTo order (UTF-16 unit order = u16string operator<):
-  // the sorted distinct outputs.  Keys: units 0-3 and 4-7 (zero padded; no term
-  // unit is 0, a split character), so strings of <= 8 units compare by key alone
+  // vocabulary in String.compareTo order (UTF-16 unit order): the sorted distinct
+  // outputs.  Keys: units 0-3 and 4-7 (zero padded; no term unit is 0, a split
+  // character), so strings of <= 8 units compare by key alone
   struct TK {
     uint64_t k0, k1;
-    const u16s *s;
+    const char16_t *p;
+    int32_t len;
     int32_t slot;  // the output's place in gterm (-1: a complex record's term)
   };
-  auto tkey = [](const u16s *w) {
-    TK t{0, 0, w, -1};
-    for (size_t i = 0; i < 8; i++) {
-      const uint64_t u = i < w->size() ? (uint64_t)(uint16_t)(*w)[i] : 0ull;
+  auto tkey = [](const char16_t *p, int32_t n) {
+    TK t{0, 0, p, n, -1};
+    for (int32_t i = 0; i < 8; i++) {
+      const uint64_t u = i < n ? (uint64_t)(uint16_t)p[i] : 0ull;
       if (i < 4) t.k0 = (t.k0 << 16) | u;
       else t.k1 = (t.k1 << 16) | u;
     }
@@ -614,32 +750,36 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   auto tless = [](const TK &x, const TK &y) {
     if (x.k0 != y.k0) return x.k0 < y.k0;
     if (x.k1 != y.k1) return x.k1 < y.k1;
-    if (x.s->size() <= 8 && y.s->size() <= 8) return x.s->size() < y.s->size();
-    return *x.s < *y.s;
+    if (x.len <= 8 && y.len <= 8) return x.len < y.len;
+    return std::lexicographical_compare(x.p + 8, x.p + x.len, y.p + 8, y.p + y.len);  // (equal keys: both >= 8 units)
   };
   auto teq = [](const TK &x, const TK &y) {
-    return x.k0 == y.k0 && x.k1 == y.k1 && (x.s->size() <= 8 && y.s->size() <= 8 ? x.s->size() == y.s->size() : *x.s == *y.s);
+    return x.k0 == y.k0 && x.k1 == y.k1 && x.len == y.len &&
+           (x.len <= 8 || memcmp(x.p + 8, y.p + 8, (size_t)(x.len - 8) * sizeof(char16_t)) == 0);
   };
   // every distinct raw token's outputs keyed in parallel (slot = its place in
   // gterm), the complex records' terms after them; after the sort each output's
   // term id is its run's rank (no search per output)
   std::vector<int32_t> go0((size_t)G + 1, 0);
-  for (int64_t g = 0; g < G; g++) go0[(size_t)g + 1] = go0[(size_t)g] + (int32_t)gout[(size_t)g].size();
+  for (int64_t g = 0; g < G; g++) go0[(size_t)g + 1] = go0[(size_t)g] + gn[(size_t)g];
   const size_t nout = (size_t)go0[(size_t)G];
   size_t nrt = 0;
   for (auto &v : rterm) nrt += v.size();
   std::vector<TK> keyed(nout + nrt);
 #pragma omp parallel for schedule(dynamic, 4096)
-  for (int64_t g = 0; g < G; g++)
-    for (size_t k = 0; k < gout[(size_t)g].size(); k++) {
-      TK t = tkey(&gout[(size_t)g][k]);
-      t.slot = go0[(size_t)g] + (int32_t)k;
+  for (int64_t g = 0; g < G; g++) {
+    const char16_t *o = gp[(size_t)g];
+    for (int32_t k = 0; k < gn[(size_t)g]; k++) {
+      TK t = tkey(o + 1, (int32_t)o[0]);
+      t.slot = go0[(size_t)g] + k;
       keyed[(size_t)t.slot] = t;
+      o += (size_t)o[0] + 1;
     }
+  }
   {
     size_t i = nout;
     for (auto &v : rterm)
-      for (auto &w : v) keyed[i++] = tkey(&w);
+      for (auto &w : v) keyed[i++] = tkey(w.data(), (int32_t)w.size());
   }
   __gnu_parallel::sort(keyed.begin(), keyed.end(), tless);
   std::vector<int32_t> gterm(nout);
@@ -649,18 +789,19 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
     if (keyed[i].slot >= 0) gterm[(size_t)keyed[i].slot] = (int32_t)(first.size() - 1);
   }
   const int64_t V = (int64_t)first.size();
-  std::vector<u16s> vocab((size_t)V);
   std::vector<TK> vk((size_t)V);
-#pragma omp parallel for schedule(static)
+  std::vector<int64_t> toff((size_t)V + 1, 0);
   for (int64_t i = 0; i < V; i++) {
-    vocab[(size_t)i] = *keyed[first[(size_t)i]].s;
     vk[(size_t)i] = keyed[first[(size_t)i]];
+    toff[(size_t)i + 1] = toff[(size_t)i] + vk[(size_t)i].len;
   }
-  keyed.clear();
-  keyed.shrink_to_fit();
-  for (int64_t i = 0; i < V; i++) vk[(size_t)i].s = &vocab[(size_t)i];
+  std::vector<char16_t> tchars((size_t)toff[(size_t)V]);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < V; i++)
+    memcpy(tchars.data() + toff[(size_t)i], vk[(size_t)i].p, (size_t)vk[(size_t)i].len * sizeof(char16_t));
+  std::vector<TK>().swap(keyed);
   auto term_of = [&](const u16s &w) {  // (complex records' terms)
-    const TK k = tkey(&w);
+    const TK k = tkey(w.data(), (int32_t)w.size());
     return (int32_t)(std::lower_bound(vk.begin(), vk.end(), k, tless) - vk.begin());
   };
   // per thread: local raw id -> its single term id (>= 0), no term (-1) or the
@@ -689,7 +830,9 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
         if (tfc[(size_t)id]++ == 0) touched.push_back(id);
       };
       const std::vector<int32_t> &lm = ltm[(size_t)rthr[(size_t)r]];
-      for (int32_t x : rtok[(size_t)r]) {
+      const int32_t *rt = tokb[(size_t)rthr[(size_t)r]].data() + rbeg[(size_t)r];
+      for (int32_t i = 0; i < rcnt[(size_t)r]; i++) {
+        const int32_t x = rt[i];
         const int32_t v = lm[(size_t)x];
         if (v >= 0) {
           count(v);
@@ -705,7 +848,6 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
         out.emplace_back(id, tfc[(size_t)id]);
         tfc[(size_t)id] = 0;
       }
-      std::vector<int32_t>().swap(rtok[(size_t)r]);
     }
   }
   if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "lmap", omp_get_wtime() - t0);
@@ -713,7 +855,9 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   // docnos keep input order before they merge)
   std::vector<int64_t> order((size_t)nR);
   for (int64_t r = 0; r < nR; r++) order[(size_t)r] = r;
-  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return rdocno[(size_t)a] < rdocno[(size_t)b]; });
+  if (!std::is_sorted(rdocno.begin(), rdocno.end()))  // (file order is usually docno order already)
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int64_t a, int64_t b) { return rdocno[(size_t)a] < rdocno[(size_t)b]; });
   // counting sort by term, in docno order: the docno-ordered records cut into one
   // contiguous chunk per thread; per-thread term counts, a prefix over (term,
   // thread), then every thread scatters its chunk (the chunks' order is docno order)
@@ -765,7 +909,8 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   CpuIndex *ix = new CpuIndex();
   ix->N = nR;
   ix->V = V;
-  ix->terms = std::move(vocab);
+  ix->toff = std::move(toff);
+  ix->tchars = std::move(tchars);
   std::vector<int64_t> merged((size_t)V, 0);
 #pragma omp parallel for schedule(dynamic, 1024)
   for (int64_t t = 0; t < V; t++) {
@@ -796,6 +941,13 @@ void *or_cpuopt_build(const uint8_t *corpus, size_t n, const uint8_t *map, size_
   ix->off.assign((size_t)V + 1, 0);
   for (int64_t t = 0; t < V; t++) ix->off[(size_t)t + 1] = ix->off[(size_t)t] + merged[(size_t)t];
   ix->P = ix->off[(size_t)V];
+  if (ix->P == Pm) {  // no duplicate docnos merged: the lists are in place
+    ix->docno = std::move(pd);
+    ix->tf = std::move(pf);
+    if (getenv("SME_CPU_PROF")) fprintf(stderr, "cpuopt %s %.3f\n", "finish", omp_get_wtime() - t0);
+    ix->build_s = omp_get_wtime() - t0;
+    return ix;
+  }
   ix->docno.resize((size_t)ix->P);
   ix->tf.resize((size_t)ix->P);
 #pragma omp parallel for schedule(dynamic, 1024)
@@ -842,14 +994,12 @@ void or_cpuopt_csr(const void *h, int64_t *off, int32_t *docno, int32_t *tf, int
   memcpy(off, ix->off.data(), ix->off.size() * sizeof(int64_t));
   memcpy(docno, ix->docno.data(), ix->docno.size() * sizeof(int32_t));
   memcpy(tf, ix->tf.data(), ix->tf.size() * sizeof(int32_t));
-  int64_t o = 0;
-  toff[0] = 0;
-  for (int64_t t = 0; t < ix->V; t++) {
-    const u16s &s = ix->terms[(size_t)t];
-    if (tchars) memcpy(tchars + o, s.data(), s.size() * sizeof(uint16_t));
-    o += (int64_t)s.size();
-    toff[t + 1] = o;
+  if (ix->toff.empty()) {  // (an index over given CSR arrays: no term strings)
+    for (int64_t t = 0; t <= ix->V; t++) toff[t] = 0;
+    return;
   }
+  memcpy(toff, ix->toff.data(), ix->toff.size() * sizeof(int64_t));
+  if (tchars) memcpy(tchars, ix->tchars.data(), ix->tchars.size() * sizeof(uint16_t));
 }
 
 /* Batched rank(): term ids (-1 skipped) per query, k results per query (docno

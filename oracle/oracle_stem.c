@@ -27,42 +27,45 @@ typedef struct {
   const char *s;
   int substring_i;
   int result;
+  int n; /* strlen(s) */
 } among;
+#define AM(str, sub, res) \
+  { str, sub, res, (int)sizeof(str) - 1 }
 
-static const among a_0[] = {{"arsen", -1, -1}, {"commun", -1, -1}, {"gener", -1, -1}};
-static const among a_1[] = {{"'", -1, 1}, {"'s'", 0, 1}, {"'s", -1, 1}};
-static const among a_2[] = {{"ied", -1, 2}, {"s", -1, 3},   {"ies", 1, 2},
-                            {"sses", 1, 1}, {"ss", 1, -1}, {"us", 1, -1}};
-static const among a_3[] = {{"", -1, 3},  {"bb", 0, 2}, {"dd", 0, 2}, {"ff", 0, 2}, {"gg", 0, 2},
-                            {"bl", 0, 1}, {"mm", 0, 2}, {"nn", 0, 2}, {"pp", 0, 2}, {"rr", 0, 2},
-                            {"at", 0, 1}, {"tt", 0, 2}, {"iz", 0, 1}};
-static const among a_4[] = {{"ed", -1, 2},   {"eed", 0, 1},   {"ing", -1, 2},
-                            {"edly", -1, 2}, {"eedly", 3, 1}, {"ingly", -1, 2}};
+static const among a_0[] = {AM("arsen", -1, -1), AM("commun", -1, -1), AM("gener", -1, -1)};
+static const among a_1[] = {AM("'", -1, 1), AM("'s'", 0, 1), AM("'s", -1, 1)};
+static const among a_2[] = {AM("ied", -1, 2), AM("s", -1, 3),   AM("ies", 1, 2),
+                            AM("sses", 1, 1), AM("ss", 1, -1), AM("us", 1, -1)};
+static const among a_3[] = {AM("", -1, 3),  AM("bb", 0, 2), AM("dd", 0, 2), AM("ff", 0, 2), AM("gg", 0, 2),
+                            AM("bl", 0, 1), AM("mm", 0, 2), AM("nn", 0, 2), AM("pp", 0, 2), AM("rr", 0, 2),
+                            AM("at", 0, 1), AM("tt", 0, 2), AM("iz", 0, 1)};
+static const among a_4[] = {AM("ed", -1, 2),   AM("eed", 0, 1),   AM("ing", -1, 2),
+                            AM("edly", -1, 2), AM("eedly", 3, 1), AM("ingly", -1, 2)};
 static const among a_5[] = {
-    {"anci", -1, 3},    {"enci", -1, 2},   {"ogi", -1, 13},     {"li", -1, 16},
-    {"bli", 3, 12},     {"abli", 4, 4},    {"alli", 3, 8},      {"fulli", 3, 14},
-    {"lessli", 3, 15},  {"ousli", 3, 10},  {"entli", 3, 5},     {"aliti", -1, 8},
-    {"biliti", -1, 12}, {"iviti", -1, 11}, {"tional", -1, 1},   {"ational", 14, 7},
-    {"alism", -1, 8},   {"ation", -1, 7},  {"ization", 17, 6},  {"izer", -1, 6},
-    {"ator", -1, 7},    {"iveness", -1, 11}, {"fulness", -1, 9}, {"ousness", -1, 10}};
-static const among a_6[] = {{"icate", -1, 4}, {"ative", -1, 6},   {"alize", -1, 3},
-                            {"iciti", -1, 4}, {"ical", -1, 4},    {"tional", -1, 1},
-                            {"ational", 5, 2}, {"ful", -1, 5},    {"ness", -1, 5}};
-static const among a_7[] = {{"ic", -1, 1},   {"ance", -1, 1}, {"ence", -1, 1}, {"able", -1, 1},
-                            {"ible", -1, 1}, {"ate", -1, 1},  {"ive", -1, 1},  {"ize", -1, 1},
-                            {"iti", -1, 1},  {"al", -1, 1},   {"ism", -1, 1},  {"ion", -1, 2},
-                            {"er", -1, 1},   {"ous", -1, 1},  {"ant", -1, 1},  {"ent", -1, 1},
-                            {"ment", 15, 1}, {"ement", 16, 1}};
-static const among a_8[] = {{"e", -1, 1}, {"l", -1, 2}};
-static const among a_9[] = {{"succeed", -1, -1}, {"proceed", -1, -1}, {"exceed", -1, -1},
-                            {"canning", -1, -1}, {"inning", -1, -1},  {"earring", -1, -1},
-                            {"herring", -1, -1}, {"outing", -1, -1}};
-static const among a_10[] = {{"andes", -1, -1}, {"atlas", -1, -1}, {"bias", -1, -1},
-                             {"cosmos", -1, -1}, {"dying", -1, 3}, {"early", -1, 9},
-                             {"gently", -1, 7}, {"howe", -1, -1}, {"idly", -1, 6},
-                             {"lying", -1, 4},  {"news", -1, -1}, {"only", -1, 10},
-                             {"singly", -1, 11}, {"skies", -1, 2}, {"skis", -1, 1},
-                             {"sky", -1, -1},   {"tying", -1, 5}, {"ugly", -1, 8}};
+    AM("anci", -1, 3),    AM("enci", -1, 2),   AM("ogi", -1, 13),     AM("li", -1, 16),
+    AM("bli", 3, 12),     AM("abli", 4, 4),    AM("alli", 3, 8),      AM("fulli", 3, 14),
+    AM("lessli", 3, 15),  AM("ousli", 3, 10),  AM("entli", 3, 5),     AM("aliti", -1, 8),
+    AM("biliti", -1, 12), AM("iviti", -1, 11), AM("tional", -1, 1),   AM("ational", 14, 7),
+    AM("alism", -1, 8),   AM("ation", -1, 7),  AM("ization", 17, 6),  AM("izer", -1, 6),
+    AM("ator", -1, 7),    AM("iveness", -1, 11), AM("fulness", -1, 9), AM("ousness", -1, 10)};
+static const among a_6[] = {AM("icate", -1, 4), AM("ative", -1, 6),   AM("alize", -1, 3),
+                            AM("iciti", -1, 4), AM("ical", -1, 4),    AM("tional", -1, 1),
+                            AM("ational", 5, 2), AM("ful", -1, 5),    AM("ness", -1, 5)};
+static const among a_7[] = {AM("ic", -1, 1),   AM("ance", -1, 1), AM("ence", -1, 1), AM("able", -1, 1),
+                            AM("ible", -1, 1), AM("ate", -1, 1),  AM("ive", -1, 1),  AM("ize", -1, 1),
+                            AM("iti", -1, 1),  AM("al", -1, 1),   AM("ism", -1, 1),  AM("ion", -1, 2),
+                            AM("er", -1, 1),   AM("ous", -1, 1),  AM("ant", -1, 1),  AM("ent", -1, 1),
+                            AM("ment", 15, 1), AM("ement", 16, 1)};
+static const among a_8[] = {AM("e", -1, 1), AM("l", -1, 2)};
+static const among a_9[] = {AM("succeed", -1, -1), AM("proceed", -1, -1), AM("exceed", -1, -1),
+                            AM("canning", -1, -1), AM("inning", -1, -1),  AM("earring", -1, -1),
+                            AM("herring", -1, -1), AM("outing", -1, -1)};
+static const among a_10[] = {AM("andes", -1, -1), AM("atlas", -1, -1), AM("bias", -1, -1),
+                             AM("cosmos", -1, -1), AM("dying", -1, 3), AM("early", -1, 9),
+                             AM("gently", -1, 7), AM("howe", -1, -1), AM("idly", -1, 6),
+                             AM("lying", -1, 4),  AM("news", -1, -1), AM("only", -1, 10),
+                             AM("singly", -1, 11), AM("skies", -1, 2), AM("skis", -1, 1),
+                             AM("sky", -1, -1),   AM("tying", -1, 5), AM("ugly", -1, 8)};
 
 static const unsigned char g_v[] = {17, 65, 16, 1};
 static const unsigned char g_v_WXY[] = {1, 17, 65, 208, 1};
@@ -147,7 +150,7 @@ static int find_among(sn *z, const among *v, int v_size) {
     int diff = 0;
     int common = common_i < common_j ? common_i : common_j;
     const among *w = &v[k];
-    int wn = (int)strlen(w->s);
+    int wn = w->n;
     for (int i2 = common; i2 < wn; i2++) {
       if (c + common == l) {
         diff = -1;
@@ -173,7 +176,7 @@ static int find_among(sn *z, const among *v, int v_size) {
   }
   for (;;) {
     const among *w = &v[i];
-    int wn = (int)strlen(w->s);
+    int wn = w->n;
     if (common_i >= wn) {
       z->cursor = c + wn;
       return w->result;
@@ -193,7 +196,7 @@ static int find_among_b(sn *z, const among *v, int v_size) {
     int diff = 0;
     int common = common_i < common_j ? common_i : common_j;
     const among *w = &v[k];
-    int wn = (int)strlen(w->s);
+    int wn = w->n;
     for (int i2 = wn - 1 - common; i2 >= 0; i2--) {
       if (c - common == lb) {
         diff = -1;
@@ -219,7 +222,7 @@ static int find_among_b(sn *z, const among *v, int v_size) {
   }
   for (;;) {
     const among *w = &v[i];
-    int wn = (int)strlen(w->s);
+    int wn = w->n;
     if (common_i >= wn) {
       z->cursor = c - wn;
       return w->result;

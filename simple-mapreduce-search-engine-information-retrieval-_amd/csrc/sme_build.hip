@@ -4145,7 +4145,8 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
       weights_fused = true;
     }
     key_s = term_sort(p_term, v32, key_s, v32s, sort_nrec, sort_reg, sort_xoff, P, tbits, dmin, F, docno_d, tf_d, rscr,
-                      st, wf ? (const double *)ix->d_lut.p : nullptr, log10((double)(std::max<int64_t>(nR, 0) / 1)), wf);
+                      st, wf ? (const double *)ix->d_lut.p : nullptr, log10((double)(std::max<int64_t>(nR, 0) / 1)), wf,
+                      (int)cx->opt_sort_bits);
     off = ix->d_off.as<int64_t>(Vi + 1);
     SME_HIP(hipMemsetAsync(off, 0, (Vi + 1) * sizeof(int64_t), st));
     hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, Vi);

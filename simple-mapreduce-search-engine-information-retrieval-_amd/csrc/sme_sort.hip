@@ -675,11 +675,12 @@ void rs_scan(uint32_t *gsum, int64_t n, uint32_t *sums, hipStream_t st) {
 // tf.  counts: ceil(P / 16384) * 2048 + 2048 * 256 u32 of scratch.
 uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t nrec, const int64_t *reg,
                     const int64_t *xoff, int64_t P, int bits, int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf,
-                    uint32_t *counts, hipStream_t st, const double *lut, double idf, double *w) {
+                    uint32_t *counts, hipStream_t st, const double *lut, double idf, double *w, int maxbits) {
   if (P <= 0) return k0;
   if (P > 0xFFFFFFFFll) throw Error(SME_ELIMIT, "term sort of more than 2^32 pairs");
   bits = std::max(bits, 1);
-  const int npass = (bits + kRsMaxBits - 1) / kRsMaxBits;
+  maxbits = std::min(std::max(maxbits, 1), kRsMaxBits);
+  const int npass = (bits + maxbits - 1) / maxbits;
   const int64_t ntiles = (P + kRsTile - 1) / kRsTile;
   const RsGroups rg = rs_groups(ntiles);
   const int64_t tpg = rg.tpg;

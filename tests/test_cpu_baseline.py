@@ -57,6 +57,20 @@ def test_cpuopt_kat_and_invalid_utf8():
     _check(bad, sorted("D%d" % i for i in range(40)), 2)
 
 
+def test_cpuopt_ascii_fast_path_edges():
+    """Raw tokens of the normalize fast path (ASCII letters, digits, apostrophes):
+    apostrophes dropped anywhere, case folded, stopwords in any case or with
+    apostrophes, empty results, and the 100-byte token limit on both sides."""
+    words = ["The", "THE", "tHe", "Don't", "don't", "'", "''", "'a'", "x'", "'s", "ABC's", "O'Neil", "rock'n'roll",
+             "Running", "RUNNING", "runs", "a" * 99, "b" * 100, "C" * 101, "'" + "d" * 99, "e'" * 50, "Ab1'2",
+             "1984", "x", "I", "it's", "IT'S", "you'll", "isn't", "a.b", "Ie", "Y", "yy", "sky", "Skies", "news"]
+    recs = []
+    for i in range(40):
+        ws = [words[(i * 7 + j) % len(words)] for j in range(25)]
+        recs.append(b"<DOC><DOCNO>E%02d</DOCNO> %s</DOC>\n" % (i, " ".join(ws).encode()))
+    _check(b"".join(recs), sorted("E%02d" % i for i in range(40)), 3)
+
+
 def test_cpuopt_from_csr_matches_built_index():
     """The cpu-opt rank() over an index wrapped from CSR arrays (bench.py's
     full-index CPU query leg) answers like the cpu-opt index built from text."""

@@ -83,6 +83,15 @@ def test_build_large_segments(sme, synth):
     assert int(np.diff(off).max()) > 8192
 
 
+@pytest.mark.parametrize("bits", [6, 8, 11])
+def test_build_sort_digit_bits(sme, synth, bits):
+    """The term sort's LSD digit width (sme_set_option "sort_digit_bits"): 2 to 4
+    passes over the same pairs give the reducer's order."""
+    n = 3000
+    c = synth.gen_corpus(n, V=40000, seed=3, len_lo=40, len_hi=160)
+    _check_build(sme, c, synth.docids(n), R=2, opts={"sort_digit_bits": bits})
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_build_fuzz(sme, seed):
     corpus, ids = common.fuzz_corpus(seed, 120)
