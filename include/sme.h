@@ -244,9 +244,10 @@ int sme_query_topk_tie(sme_index *ix, const int32_t *term_ids, const int64_t *q_
 
 /* Query-side structures of an index (the role the reference's forward index,
  * BuildIntDocVectorsForwardIndex.java:84-158, plays for rank()): heavy-term tf
- * and impact rows with their block maxima (at most a quarter of the free HBM,
- * 64 GB), and one 4-byte window-pass word per posting of the other terms (if 4 B
- * per posting fits a quarter of the free HBM; else the window-major scorer is
+ * and impact rows with their block maxima (at most a quarter of the free HBM --
+ * counting the device blocks the context holds for reuse --, 64 GB), and one
+ * 4-byte window-pass word per posting of the other terms (if 4 B per posting
+ * fits a quarter of the free HBM; else the window-major scorer is
  * not used and batches take the block-max path).  Built once per index; the
  * impact rows and their scale depend on idf, so sme_index_reweight DROPS them:
  * call this after the last reweight (sme_query_topk* rebuilds them on first

@@ -45,6 +45,11 @@ struct BufPool {
     return p;
   }
   void put(void *p, size_t cap) { blocks.emplace_back(p, cap); }
+  size_t idle() const {  // bytes held for reuse (free to this context, not in hipMemGetInfo's free)
+    size_t s = 0;
+    for (const auto &b : blocks) s += b.second;
+    return s;
+  }
   ~BufPool() {
     for (auto &b : blocks) (void)hipFree(b.first);
   }

@@ -1469,6 +1469,12 @@ struct QWinArgs {
 #ifndef SME_QSBG
 #define SME_QSBG 2
 #endif
+// SME_QW_KARG (default 1): the pair loop reads its pointer arguments from the
+// kernarg segment where it uses them (SGPR spills into VGPR lanes 106 -> 36 reads;
+// c3 20.64 -> 20.21 ms, c5 1 M top-100 1782 -> 1741 ms, digests unchanged)
+#ifndef SME_QW_KARG
+#define SME_QW_KARG 1
+#endif
 #ifndef SME_QWIN_SPARSE_NT
 #define SME_QWIN_SPARSE_NT 0
 #endif
@@ -1530,6 +1536,17 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
   QPos NP{0, 0, 0};  // next query's position record, loaded a pair ahead
   if (pos + kWNT / 64 < p_hi) NP = ld_pos_uni(a.qpos + pos + kWNT / 64);
   for (;;) {
+#if SME_QW_KARG
+    // the arguments re-read from the kernarg segment through a pointer the
+    // compiler cannot hoist: loop-invariant pointers then live only where they
+    // are used instead of in SGPRs spilled to VGPR lanes across the whole loop
+    const __attribute__((address_space(4))) QWinArgs *ka =
+        (const __attribute__((address_space(4))) QWinArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+#define QA (*ka)
+#else
+#define QA a
+#endif
     const int npos = pos + kWNT / 64;
     const bool hasn = npos < p_hi;
     // the next query's term records and gate, and the position record after it
@@ -1537,9 +1554,9 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     uint32_t ngate = 0;
     QPos NNP{0, 0, 0};
     if (hasn) {
-      ND = ld_desc_nt(a.desc, NP.q0, NP.nt, lane);
-      ngate = ld_uni(a.gate + NP.q);
-      if (npos + kWNT / 64 < p_hi) NNP = ld_pos_uni(a.qpos + npos + kWNT / 64);
+      ND = ld_desc_nt(QA.desc, NP.q0, NP.nt, lane);
+      ngate = ld_uni(QA.gate + NP.q);
+      if (npos + kWNT / 64 < p_hi) NNP = ld_pos_uni(QA.qpos + npos + kWNT / 64);
     }
 #ifdef SME_EXPERIMENTS  // timing switches: 4 = no sparse terms, 8 = no heavy terms
     const uint64_t hm = (QW_EXPER & 8) ? 0ull : (uint64_t)__ballot(D.hr >= 0);
@@ -1562,7 +1579,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     for (int i = 0; i < 8; i++) sb[i] = bias2;
     {
       const int64_t soff = (x << (kWinB - 2)) + 16 * lane;
-      const int64_t hstr4 = a.hstride >> 2;
+      const int64_t hstr4 = QA.hstride >> 2;
       for (uint64_t mh = hm; mh;) {
         uint4 v[SME_QSBG];
 #pragma unroll
@@ -1571,7 +1588,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
           if (mh) {
             const int j = (int)__builtin_ctzll(mh);
             mh &= mh - 1;
-            v[g] = *reinterpret_cast<const uint4 *>(a.sbq + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * hstr4 + soff);
+            v[g] = *reinterpret_cast<const uint4 *>(QA.sbq + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * hstr4 + soff);
           }
         }
 #pragma unroll
@@ -1610,9 +1627,9 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
         if (e < total) {
           // the posting's word: its place in the window, q(tf) and tf, as the list keeps them
 #if SME_QWIN_SPARSE_NT  // the window's sparse postings without L2 allocation (kept for the heavy rows)
-          const uint32_t pw = __builtin_nontemporal_load(a.spk + pb + e);
+          const uint32_t pw = __builtin_nontemporal_load(QA.spk + pb + e);
 #else
-          const uint32_t pw = a.spk[pb + e];
+          const uint32_t pw = QA.spk[pb + e];
 #endif
           const int r = (int)(pw & 0xFFFu);
           const uint32_t qv = (pw >> 12) & 0xFFu;
@@ -1628,8 +1645,8 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     // the next query's skip entries (its records arrived during the sparse pass)
     int32_t nmc = 0, nme = 0;
     if (ND.mdf > 0 && ND.hr < 0) {
-      nmc = a.skt[x * a.nrows + ND.brow];
-      nme = a.skt[(x + 1) * a.nrows + ND.brow];
+      nmc = QA.skt[x * QA.nrows + ND.brow];
+      nme = QA.skt[(x + 1) * QA.nrows + ND.brow];
     }
     // sub-blocks over the gate: heavy maxima + their block's sparse impact sum
     if (total > 0) {
@@ -1703,7 +1720,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
             if (e >= pj) pb = rl64(plo, j) - pj;
           }
           if (e < total) {
-            const uint32_t pw = a.spk[pb + e];
+            const uint32_t pw = QA.spk[pb + e];
             const int r = (int)(pw & 0xFFFu);
             const uint32_t sw = bsum[r >> 4];
             if (sw >> 31) {
@@ -1790,7 +1807,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
                   mh &= mh - 1;
                   if (hs)
                     wq[g] = *reinterpret_cast<const uint32_t *>(
-                        a.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + io);
+                        QA.imp + (int64_t)__builtin_amdgcn_readlane(D.hr, j) * QA.hstride + io);
                 }
               }
 #pragma unroll
@@ -1809,8 +1826,8 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
           const int32_t ncand = (QW_EXPER & 2) ? 0 : __builtin_amdgcn_readlane(cincl, 63);
           if (QW_STATS && lane == 0) atomicAdd(QW_STATS + 4, (unsigned long long)ncand);
           // the threshold itself (score, key) only where documents reached the gate
-          const double th0 = ncand > 0 ? ld_uni(a.th0 + P.q) : 0.0;
-          const uint64_t thk = ncand > 0 ? ld_uni(a.thk + P.q) : kNoKey;
+          const double th0 = ncand > 0 ? ld_uni(QA.th0 + P.q) : 0.0;
+          const uint64_t thk = ncand > 0 ? ld_uni(QA.thk + P.q) : kNoKey;
           for (int32_t k0 = 0; k0 < ncand; k0 += kCList) {
             const int32_t kn = min(ncand - k0, kCList);
             qwave_sync();
@@ -1840,7 +1857,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
                     if (mh) {
                       const int j = (int)__builtin_ctzll(mh);
                       mh &= mh - 1;
-                      fb[c] = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
+                      fb[c] = QA.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * QA.hstride + (x << kWinB) + r];
                     }
                   }
 #pragma unroll
@@ -1855,7 +1872,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
                       f = (int)(hb8 & 0xFFu);
                       hb8 >>= 8;
                     } else {
-                      f = a.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * a.hstride + (x << kWinB) + r];
+                      f = QA.tfrow[(int64_t)__builtin_amdgcn_readlane(D.hr, j) * QA.hstride + (x << kWinB) + r];
                     }
                     hseen++;
                   } else if (listed) {
@@ -1880,30 +1897,30 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
                     int64_t hi = e;
                     while (lo < hi) {
                       const int64_t mid = (lo + hi) >> 1;
-                      if (a.docno[mid] < d) lo = mid + 1;
+                      if (QA.docno[mid] < d) lo = mid + 1;
                       else hi = mid;
                     }
-                    f = (lo < e && a.docno[lo] == d) ? a.tf[lo] : 0;
+                    f = (lo < e && QA.docno[lo] == d) ? QA.tf[lo] : 0;
                   }
                   if (f != 0) {
-                    S = __dadd_rn(S, __dmul_rn(f < kWinLut ? s_lut[f] : a.lut[f], rld(D.idf, j)));
-                    if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f, a.reftie);
+                    S = __dadd_rn(S, __dmul_rn(f < kWinLut ? s_lut[f] : QA.lut[f], rld(D.idf, j)));
+                    if (tie == 0xFFFFFFFFu) tie = ref_tie(j, f, QA.reftie);
                   }
                 }
-                key = doc_key(a.reftie ? tie : 0u, d);
+                key = doc_key(QA.reftie ? tie : 0u, d);
                 keep = S > th0 || (S == th0 && key <= thk);  // th0 < 0 (no seed): every touched document
               }
               const uint64_t km = (uint64_t)__ballot(keep);
               if (QW_STATS && lane == 0) atomicAdd(QW_STATS + 5, (unsigned long long)__popcll(km));
               if (km) {
                 unsigned int base = 0;
-                if (lane == 0) base = atomicAdd(&a.ccnt[P.q], (unsigned int)__popcll(km));
+                if (lane == 0) base = atomicAdd(&QA.ccnt[P.q], (unsigned int)__popcll(km));
                 base = (unsigned int)__shfl((int)base, 0, 64);
                 if (keep) {
                   const unsigned int idx = base + lane_prefix(km);
-                  if (idx < (unsigned int)a.cap) {
-                    a.cs[(int64_t)P.q * a.cap + idx] = S;
-                    a.ck[(int64_t)P.q * a.cap + idx] = key;
+                  if (idx < (unsigned int)QA.cap) {
+                    QA.cs[(int64_t)P.q * QA.cap + idx] = S;
+                    QA.ck[(int64_t)P.q * QA.cap + idx] = key;
                   }
                 }
               }
@@ -1925,6 +1942,7 @@ __global__ __launch_bounds__(kWNT, SME_QWIN_WAVES) void k_query_win(QWinArgs a) 
     gate = ngate;
     mc = nmc;
     me = nme;
+#undef QA
   }
 }
 
@@ -2172,11 +2190,16 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     SME_HIP(hipStreamSynchronize(st));
     // memory budget for the rows: a quarter of the device's free memory, at most
     // 64 GB (a heavy term without a row reaches the window pass as a long sparse
-    // list; the c4 shard's ~2,300 heavy terms need ~30 GB of rows)
+    // list; the c4 shard's ~2,300 heavy terms need ~33 GB of rows).  Free memory
+    // includes the blocks the context's pool holds for reuse (a closed index's
+    // rows among them) and this index's own row buffer: hipMemGetInfo counts
+    // neither, so a second index on the same context got fewer rows than the first
+    // (the c4 shard's 100 k batch: 100 -> 373 ms)
     size_t fr = 0, tot = 0;
     SME_HIP(hipMemGetInfo(&fr, &tot));
+    const double avail = (double)fr + (double)cx->pool.idle() + (double)ix->d_heavy.cap;
     const double per_row = 2.0 * (double)stride + (double)(T << 6) + (double)T + (double)(T << 8);
-    const int64_t cap = (int64_t)(std::min<double>((double)fr / 4.0, 64e9) / per_row);
+    const int64_t cap = (int64_t)(std::min<double>(avail / 4.0, 64e9) / per_row);
     const int64_t H = std::min<int64_t>(nh, cap);
     int32_t *hrow_of = ix->d_hrow_of.as<int32_t>(V);
     int32_t *hterm = W[38].as<int32_t>(H + 1);
@@ -2218,7 +2241,7 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     size_t fr = 0, tot = 0;
     SME_HIP(hipMemGetInfo(&fr, &tot));
     const size_t need = (size_t)ix->P * sizeof(uint32_t);
-    if (ix->d_spk.cap >= need || need <= fr / 4) {
+    if (ix->d_spk.cap >= need || need <= (fr + cx->pool.idle()) / 4) {
       uint32_t *spk = ix->d_spk.as<uint32_t>((size_t)ix->P);
       const int32_t *hro = ix->q_H > 0 ? (const int32_t *)ix->d_hrow_of.p : nullptr;
       hipLaunchKernelGGL(k_sparse_pack, dim3((unsigned)std::min<int64_t>((V + 3) / 4, 65536)), dim3(256), 0, st,
