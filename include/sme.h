@@ -56,6 +56,14 @@ extern "C" {
                                (IntDocVectorsForwardIndex.java:195-215,363-365) is a stable sort by
                                score desc (its merge sort only asks compareTo <= 0 / > 0, which is
                                score order for finite scores), so equal scores keep that order */
+#define SME_TIE_JAVA7 2     /* rank()'s list as a Java 7 JVM leaves it: Collections.sort is then
+                               ComparableTimSort, and DocScore.compareTo = (int)Math.ceil(o.score -
+                               score) -- 0 for score gaps in (-1, 0] -- is not a total order, so the
+                               whole first-encounter list is sorted by the JDK 7 GA algorithm on the
+                               device (one thread per query; a compatibility mode, not the serving
+                               path).  A query whose sort Java aborts with IllegalArgumentException
+                               ("Comparison method violates its general contract!") gets docno -2
+                               in all k slots; tie words are 0xFFFFFFFF (no shard merge) */
 
 typedef struct sme_ctx sme_ctx;
 typedef struct sme_index sme_index;

@@ -24,6 +24,7 @@ LIB_PATH = os.environ.get("SME_LIB_PATH") or os.path.join(_HERE, "libsme.so")
 SME_IDF_REFERENCE = 0
 SME_TIE_DOCNO = 0      # score desc, docno asc (north star)
 SME_TIE_REFERENCE = 1  # score desc, then rank()'s printed order (first encounter; include/sme.h)
+SME_TIE_JAVA7 = 2      # rank()'s list as Java 7's Collections.sort (TimSort) leaves it; -2 rows: it throws
 SME_IDF_TRUE_DF = 1
 
 

@@ -244,7 +244,7 @@ int sme_create(const sme_config *cfg, sme_ctx **out) {
     if (cfg->num_partitions < 1) throw sme::Error(SME_EINVAL, "num_partitions must be >= 1");
     if (cfg->idf_mode != SME_IDF_REFERENCE && cfg->idf_mode != SME_IDF_TRUE_DF)
       throw sme::Error(SME_EINVAL, "bad idf_mode");
-    if (cfg->tiebreak != SME_TIE_DOCNO && cfg->tiebreak != SME_TIE_REFERENCE)
+    if (cfg->tiebreak != SME_TIE_DOCNO && cfg->tiebreak != SME_TIE_REFERENCE && cfg->tiebreak != SME_TIE_JAVA7)
       throw sme::Error(SME_EINVAL, "bad tiebreak");
     int ndev = 0;
     SME_HIP(hipGetDeviceCount(&ndev));

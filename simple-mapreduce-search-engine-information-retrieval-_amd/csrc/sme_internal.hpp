@@ -252,6 +252,10 @@ void prepare_queries(sme_index *ix, hipStream_t st);
 // batch -- on every doc shard answering it -- gets the same tie words.
 void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k,
                 int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie, hipStream_t st, int tie_bits = 0);
+// SME_TIE_JAVA7 (sme_timsort.hip): every query's whole first-encounter list and
+// the JDK 7 ComparableTimSort over it, one thread per query
+void query_topk_java7(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, int nq, int k,
+                      int32_t *d_out_docno, double *d_out_score, uint32_t *d_out_tie, hipStream_t st);
 void tokenize_string(sme_ctx *cx, const uint8_t *h_utf8, size_t n, std::vector<std::vector<uint16_t>> &out,
                      hipStream_t st);
 void term_fingerprints(sme_index *ix, uint64_t *d_out, hipStream_t st);

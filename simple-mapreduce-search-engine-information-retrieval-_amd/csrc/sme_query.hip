@@ -2317,6 +2317,10 @@ void query_topk(sme_index *ix, const int32_t *d_terms, const int64_t *d_qoff, in
   if (k > kListCap - kQNT) throw Error(SME_ELIMIT, "top-k with k > 1792");
   if (nq <= 0) return;
   sme_ctx *cx = ix->ctx;
+  if (cx->cfg.tiebreak == SME_TIE_JAVA7) {  // the whole list and Java 7's TimSort (sme_timsort.hip)
+    query_topk_java7(ix, d_terms, d_qoff, nq, k, d_out_docno, d_out_score, d_out_tie, st);
+    return;
+  }
   auto &W = cx->ws;
   int *err = W[63].as<int>(4);
   unsigned long long *wmax = reinterpret_cast<unsigned long long *>(err + 2);

@@ -415,6 +415,43 @@ def test_queries_reference_order(sme, synth, idf_mode):
         assert np.array_equal(md.numpy(), dn) and np.array_equal(ms.numpy(), sc)
 
 
+@pytest.mark.parametrize("idf_mode", [0, 1])
+def test_queries_java7_timsort_order(sme, synth, idf_mode):
+    """SME_TIE_JAVA7: rank()'s whole first-encounter list sorted by the JDK 7 GA
+    ComparableTimSort over DocScore.compareTo (IntDocVectorsForwardIndex.java:
+    195-222,363-365) on the device, held to the oracle's restatement (order 3):
+    the same k documents and scores where Java prints a list, docno -2 rows
+    where its TimSort throws IllegalArgumentException -- which must happen for
+    some of these multi-term queries (profiles/t5_divergence.json: 13 % of c3
+    top-10 queries in reference idf mode).  Unknown and repeated terms, k = 10 /
+    100, lists past TimSort's 32-element binary-insertion cut."""
+    n = 3000
+    c = synth.gen_corpus(n, V=600, seed=37, len_lo=20, len_hi=90)
+    ix, ref = _check_build(sme, c, synth.docids(n), R=1, idf_mode=idf_mode, tiebreak=2)
+    _, _, _, df = ix.csr()
+    names = [ix.term(i) for i in range(ix.V)]
+    terms, qoff = synth.queries_by_df(df, 150, seed=11, qlen_lo=1, qlen_hi=8)
+    terms[::17] = -1
+    terms[9] = terms[8]
+    thrown = listed = 0
+    for k in (10, 100):
+        dn, sc = ix.query_topk(terms, qoff, k)
+        for q in range(len(qoff) - 1):
+            tl = [names[t] for t in terms[qoff[q]:qoff[q + 1]] if t >= 0]
+            rd, rs = ref.query(tl, k, idf_mode, 3)
+            if rd is None:
+                thrown += 1
+                assert (dn[q] == -2).all(), (k, q)
+                continue
+            listed += 1
+            assert dn[q, :len(rd)].tolist() == rd, (k, q)
+            assert np.array_equal(sc[q, :len(rd)], np.array(rs)), (k, q)
+            assert (dn[q, len(rd):] == -1).all()
+    assert listed > 0
+    if idf_mode == 0:
+        assert thrown > 0  # the contract-violation path is exercised
+
+
 def test_queries_reference_order_long(sme, synth):
     """SME_TIE_REFERENCE with queries of more than 256 terms (up to 1024): the
     tie key holds the token index in 10 bits above 22 tf bits for such a batch,
