@@ -1796,6 +1796,7 @@ __global__ void k_raw_multi(const uint64_t *okey_s, const uint32_t *oidx_s, int6
 // (unsorted or equal docid terms, a docid term equal to a word term) keeps
 // the build on the general path; the result is the same either way.
 constexpr int kDocTermMax = 48;
+constexpr int32_t kDocCode = 0x40000000;  // K6b: a docid term's code in raw_term (| its docid index)
 constexpr uint32_t kNoRec = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint8_t lower_ascii(uint8_t c) { return (c >= 'A' && c <= 'Z') ? (uint8_t)(c + 32) : c; }
@@ -2020,7 +2021,7 @@ __device__ __forceinline__ int cmp_wd(const Key16 &wk, bool wex, const uint16_t 
 __global__ void k_word_rank(const uint32_t *order, int64_t Vw, const uint32_t *vslot, const uint64_t *vcs,
                             const uint16_t *pool, const Key16 *wkey, const uint8_t *wexact, const Key16 *dkey,
                             const uint64_t *dsrc, int64_t Vd, const uint8_t *text, int32_t *rank_of_slot,
-                            int64_t *term_len, int64_t *wrank) {
+                            int64_t *term_len, int64_t *wrank, int split) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < Vw; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t o = order[i];
     const uint64_t cs = vcs[o];
@@ -2033,7 +2034,7 @@ __global__ void k_word_rank(const uint32_t *order, int64_t Vw, const uint32_t *v
       else hi = mid;
     }
     const int64_t rk = i + lo;
-    rank_of_slot[vslot[o]] = (int32_t)rk;
+    rank_of_slot[vslot[o]] = (int32_t)(split ? i : rk);  // (split: the word's own rank, see kDocCode)
     term_len[rk] = (int64_t)(cs & 0xFFFF);
     wrank[i] = rk;
   }
@@ -2096,11 +2097,94 @@ __global__ void k_docid_gather(const uint64_t *dsrc, const Key16 *dkey, int64_t 
 }
 // raw slot -> term id of the docid terms (one term each)
 __global__ void k_docid_raw(const int32_t *dl, int64_t Vd, const int32_t *dslot, const int64_t *drank,
-                            int32_t *raw_term, int32_t *raw_nout) {
+                            int32_t *raw_term, int32_t *raw_nout, int split) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < Vd; j += (int64_t)gridDim.x * blockDim.x) {
     const int32_t s = dslot[dl[j]];
-    raw_term[s] = (int32_t)drank[j];
+    raw_term[s] = split ? (kDocCode | (int32_t)j) : (int32_t)drank[j];
     raw_nout[s] = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K6b: docid pairs beside the term sort.  On c5 / the c4 shard the docid terms
+// push the term ids past 22 bits (three LSD passes), while the word terms alone
+// fit two.  With the split, the raw slots carry term CODES -- a word's rank among
+// the words, kDocCode | j for docid term j -- and the aggregation writes each
+// record's one docid pair (its own docid) beside its word pairs instead of into
+// its region.  The word pairs are sorted by word rank; the last pass shifts word
+// i's postings by the docid pairs whose terms sort below it (wshift.x) and writes
+// its merged id (wshift.y); the docid pairs (one per record, docno order, sorted
+// by j when they are not already) then fill the remaining slots: pair q of
+// docid term j lands after the word pairs below j.  The CSR is the one the
+// single sort builds; a record with two docid-term pairs (a docid in another
+// record's text) sends the aggregation back to merged ids.
+__global__ void k_code_to_merged(int32_t *raw_term, uint64_t rcap, int32_t *multi, int64_t nmulti,
+                                 const int64_t *wrank, const int64_t *drank) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < rcap + (uint64_t)nmulti; s += gs) {
+    int32_t *p = s < rcap ? raw_term + s : multi + (s - rcap);
+    const int32_t v = *p;
+    if (v >= 0) *p = (int32_t)((v & kDocCode) ? drank[v & ~kDocCode] : wrank[v]);
+  }
+}
+__global__ void k_dsplit_flags(const int32_t *dk_rec, int64_t nR, uint8_t *flag) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nR; i += (int64_t)gridDim.x * blockDim.x)
+    flag[i] = dk_rec[i] >= 0;
+}
+__global__ void k_dsplit_gather(const int32_t *idx, const unsigned long long *nd, const int32_t *dk_rec,
+                                const uint32_t *dv_rec, uint32_t *dk, uint32_t *dv, unsigned long long *desc) {
+  const int64_t n = (int64_t)*nd;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+    dk[q] = (uint32_t)dk_rec[idx[q]];
+    dv[q] = dv_rec[idx[q]];
+    if (q > 0 && dk_rec[idx[q - 1]] > dk_rec[idx[q]]) atomicAdd(desc, 1ull);
+  }
+}
+// word i: (docid pairs of terms below it, its merged id)
+__global__ void k_word_shift(const int64_t *wrank, int64_t Vw, const uint32_t *dk, int64_t Nd, uint2 *ws) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < Vw; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t below = (uint32_t)(wrank[i] - i);  // docid terms below word i
+    int64_t lo = 0, hi = Nd;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (dk[m] < below) lo = m + 1;
+      else hi = m;
+    }
+    ws[i] = make_uint2((uint32_t)lo, (uint32_t)wrank[i]);
+  }
+}
+// word pairs below docid term j: where word x = (words below j) starts, less its shift
+__device__ __forceinline__ int64_t words_below(int64_t j, const int64_t *drank, const int64_t *wrank, int64_t Vw,
+                                               const uint2 *ws, const int64_t *off, int64_t Pw) {
+  const int64_t x = drank[j] - j;
+  return x < Vw ? off[wrank[x]] - (int64_t)ws[x].x : Pw;
+}
+// docid pair q -> its CSR slot (docno / tf / weight / key)
+__global__ void k_docid_place(const uint32_t *dk, const uint32_t *dv, int64_t Nd, const int64_t *drank,
+                              const int64_t *wrank, int64_t Vw, const uint2 *ws, const int64_t *off, int64_t Pw,
+                              int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf, uint32_t *key, const double *lut,
+                              double idf, double *w) {
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < Nd; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = dk[q];
+    const int64_t p = q + words_below(j, drank, wrank, Vw, ws, off, Pw);
+    const uint32_t v = dv[q];
+    docno[p] = (int32_t)((int64_t)(v / F) + dmin);
+    tf[p] = (int32_t)(v % F);
+    key[p] = (uint32_t)drank[j];
+    if (w) w[p] = __dmul_rn(lut[v % F], idf);
+  }
+}
+// docid term j's first posting (its df may be 0 or > 1)
+__global__ void k_docid_off(const uint32_t *dk, int64_t Nd, int64_t Vd, const int64_t *drank, const int64_t *wrank,
+                            int64_t Vw, const uint2 *ws, int64_t Pw, int64_t *off) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < Vd; j += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = Nd;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if ((int64_t)dk[m] < j) lo = m + 1;
+      else hi = m;
+    }
+    off[drank[j]] = lo + words_below(j, drank, wrank, Vw, ws, off, Pw);
   }
 }
 
@@ -2164,7 +2248,18 @@ struct AggIn {
   int64_t *dcnt = nullptr;
   int64_t *big_out = nullptr;
   unsigned long long *nbig = nullptr;
+  // K6b split (single-pass form only): a pair whose term code has kDocCode goes to
+  // dk_rec[i] / dv_rec[i] (record i in docno order) instead of the region; a
+  // second one in the same record sets *dbad
+  int32_t *dk_rec = nullptr;
+  uint32_t *dv_rec = nullptr;
+  unsigned long long *dbad = nullptr;
 };
+// a record's docid pair beside its region (K6b): the first claims the record's slot
+__device__ __forceinline__ void put_docid_pair(const AggIn &in, int64_t i, int32_t code, uint32_t v) {
+  if (atomicCAS(&in.dk_rec[i], -1, code & ~kDocCode) == -1) in.dv_rec[i] = v;
+  else atomicAdd(in.dbad, 1ull);
+}
 
 // Aggregate record r into table (keys/cnt, capacity mask). Returns distinct count or -1 on overflow.
 __device__ int32_t agg_record(const AggIn &in, int64_t r, int32_t *keys, int32_t *cnt, uint32_t cap_mask,
@@ -2335,22 +2430,31 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
     }
     int64_t base = fused ? in.reg_off[i] : pair_off[i];
     const uint64_t dn = (uint64_t)(uint32_t)in.docno[r] << 32;
+    int32_t nd = 0;  // K6b: docid pairs kept beside the region
     for (uint32_t k = 0; k < cap; k += 64) {
       const int32_t key = keys[k + lane];
-      const uint64_t m = __ballot(key >= 0);
+      const bool isd = fused && in.dk_rec && key >= 0 && (key & kDocCode);
+      const uint64_t m = __ballot(key >= 0 && !isd);
       if (key >= 0) {
-        const int64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
         const int32_t c = cnt_at(k + lane);
-        st_stream(p_term + o, (uint32_t)key);
-        if (in.v32)
-          st_stream(in.v32 + o, (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c));
-        else
-          p_val[o] = dn | (uint32_t)c;
+        if (isd) {  // (plain stores: a second docid pair in the record is caught by nd below)
+          in.dk_rec[i] = key & ~kDocCode;
+          in.dv_rec[i] = (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c);
+        } else {
+          const int64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
+          st_stream(p_term + o, (uint32_t)key);
+          if (in.v32)
+            st_stream(in.v32 + o, (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c));
+          else
+            p_val[o] = dn | (uint32_t)c;
+        }
         if (fused) wmax = max(wmax, (uint32_t)c);
       }
+      if (in.dk_rec) nd += __popcll((uint64_t)__ballot(isd));
       base += __popcll(m);
     }
-    if (fused && lane == 0) in.dcnt[i] = d;
+    if (fused && lane == 0) in.dcnt[i] = d - nd;
+    if (nd > 1 && lane == 0) *in.dbad = 1ull;  // two docid terms' pairs: merged ids (K6b fallback)
     wave_sync_lds();
   }
   if (fused || (!EMIT && in.max_tf)) {  // largest tf: one atomic per block (single-address atomics serialise)
@@ -2401,6 +2505,10 @@ __global__ __launch_bounds__(kAggNT) void k_agg_big(AggIn in, const int64_t *big
     for (uint32_t c0 = 0; c0 < cap; c0 += kAggNT) {
       uint32_t k = c0 + threadIdx.x;
       int32_t key = k < cap ? keys[k] : -1;
+      if (pass == 2 && in.dk_rec && key >= 0 && (key & kDocCode)) {  // K6b: beside the region
+        put_docid_pair(in, i, key, (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + cnt[k]));
+        key = -1;
+      }
       int32_t tot;
       int32_t o = block_excl_sum<kAggNT, int32_t>(key >= 0 ? 1 : 0, sc32, &tot);
       if (key >= 0) {
@@ -2421,20 +2529,24 @@ __global__ __launch_bounds__(kAggNT) void k_agg_big(AggIn in, const int64_t *big
 // K6-K8: CSR assembly
 // ============================================================================
 // first posting of every term (key sorted); four keys per 16-byte load
+// (HOLES: slots keyed 0xFFFFFFFF -- the docid pairs' places in the K6b split --
+// are skipped; the docid terms' offsets are set by k_docid_off)
+template <bool HOLES>
 __global__ void k_term_offsets(const uint32_t *key, int64_t P, int64_t *off, int64_t V) {
   const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
   const int64_t n4 = P >> 2;
+  constexpr uint32_t H = 0xFFFFFFFFu;
   for (int64_t q = gid; q < n4; q += gs) {
     const uint4 k = reinterpret_cast<const uint4 *>(key)[q];
     const int64_t i = q << 2;
     const uint32_t prev = i == 0 ? ~k.x : key[i - 1];
-    if (k.x != prev) off[k.x] = i;
-    if (k.y != k.x) off[k.y] = i + 1;
-    if (k.z != k.y) off[k.z] = i + 2;
-    if (k.w != k.z) off[k.w] = i + 3;
+    if (k.x != prev && (!HOLES || k.x != H)) off[k.x] = i;
+    if (k.y != k.x && (!HOLES || k.y != H)) off[k.y] = i + 1;
+    if (k.z != k.y && (!HOLES || k.z != H)) off[k.z] = i + 2;
+    if (k.w != k.z && (!HOLES || k.w != H)) off[k.w] = i + 3;
   }
   for (int64_t i = (n4 << 2) + gid; i < P; i += gs)
-    if (i == 0 || key[i] != key[i - 1]) off[key[i]] = i;
+    if ((i == 0 || key[i] != key[i - 1]) && (!HOLES || key[i] != H)) off[key[i]] = i;
   if (gid == 0) off[V] = P;
 }
 
@@ -3349,7 +3461,7 @@ sme_index *build_index(sme_ctx *cx, const uint8_t *t, uint64_t n, hipStream_t st
   DevBuf *W = cx->ws + kBuildWs;
   Prof prof(st, &cx->prof_events);
   auto cub_tmp = [&](size_t bytes) { return cx->cub_tmp.get(bytes); };
-  unsigned long long *cnt = W[W_CNT].as<unsigned long long>(32);  // [20] max tf, [22..23] docno range
+  unsigned long long *cnt = W[W_CNT].as<unsigned long long>(40);  // [20] max tf, [22..23] docno range, [32..34] K6b
 
   uint8_t early_code[128];  // vocabulary sort: unit -> code (host copy outlives its async upload)
   const RecordSpans rsp = find_records(cx, t, n, st, &prof);
@@ -3733,7 +3845,13 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
       hipLaunchKernelGGL(k_final_fixup, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vslot, freps, co.cand_str,
                          co.pool);
   }
-  int64_t *drank = nullptr;
+  int64_t *drank = nullptr, *wrank_all = nullptr;
+  // K6b: docid pairs beside the term sort when the word ranks need fewer key bits
+  // than the merged ids (c5: 24 -> 15 bits, one LSD pass less; the c4 shard: 24 ->
+  // 22, which with the records' tf bound lets the single-pass aggregation run)
+  bool dsplit = false;
+  if (dfast && job == 0 && cx->cfg.k == 1 && !dup_docno && cx->opt_docid_split && Vd < (int64_t)kDocCode)
+    dsplit = bits_for((uint64_t)std::max<int64_t>(Vw - 1, 1)) < bits_for((uint64_t)std::max<int64_t>(V - 1, 1));
   if (V > 0 && !dfast) {
     int64_t *tlen = W[W_T0].as<int64_t>(Vw + 1);
     hipLaunchKernelGGL(k_final_rank, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vslot, vcs, rank_of_slot, tlen);
@@ -3751,10 +3869,11 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
     uint8_t *wexact = reinterpret_cast<uint8_t *>(W[W_T1].as<uint64_t>(Vw / 8 + 2));
     int64_t *wrank = W[W_WRANK].as<int64_t>(Vw + Vd + 1);
     drank = wrank + Vw;
+    wrank_all = wrank;
     if (Vw > 0) {
       hipLaunchKernelGGL(k_word_keys, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vcs, co.pool, wkey, wexact);
       hipLaunchKernelGGL(k_word_rank, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vslot, vcs, co.pool, wkey,
-                         wexact, dkey, dsrc, Vd, t, rank_of_slot, tlen, wrank);
+                         wexact, dkey, dsrc, Vd, t, rank_of_slot, tlen, wrank, (int)dsplit);
     }
     hipLaunchKernelGGL(k_docid_rank, dim3(grid_for(Vd)), dim3(256), 0, st, dkey, dsrc, Vd, order, Vw, vcs, co.pool,
                        wkey, wexact, t, tlen, drank);
@@ -3780,7 +3899,8 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
     hipLaunchKernelGGL(k_raw_term, dim3(grid_for(nraw)), dim3(256), 0, st, rlist, nraw, cand_final, rank_of_slot,
                        co.raw_nout, raw_term);
   if (dfast)
-    hipLaunchKernelGGL(k_docid_raw, dim3(grid_for(Vd)), dim3(256), 0, st, dl, Vd, dslot, drank, raw_term, co.raw_nout);
+    hipLaunchKernelGGL(k_docid_raw, dim3(grid_for(Vd)), dim3(256), 0, st, dl, Vd, dslot, drank, raw_term, co.raw_nout,
+                       (int)dsplit);
   if (novf > 0) {
     uint64_t *ok2 = W[W_T0].as<uint64_t>(novf);
     uint32_t *oi = W[W_T1].as<uint32_t>(novf), *oi2 = W[W_VIDX].as<uint32_t>(novf);
@@ -3842,6 +3962,14 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
   int64_t P = 0;
   uint32_t *p_term = nullptr;
   uint64_t *p_val = nullptr;
+  // K6b fallback: the raw slots' term codes back to merged ids (every path but the
+  // split single-pass aggregation reads merged ids)
+  auto to_merged = [&]() {
+    hipLaunchKernelGGL(k_code_to_merged, dim3(grid_for((int64_t)rcap + novf)), dim3(256), 0, st, raw_term, rcap, multi,
+                       novf, (const int64_t *)wrank_all, (const int64_t *)drank);
+    SME_CHECK_LAUNCH();
+    dsplit = false;
+  };
   // K = 1 with distinct docnos: the count pass also finds the largest tf, so the
   // emit pass can write the term sort's packed u32 values ((docno - dmin) * F + tf)
   // directly (no 8-byte pair values, no separate pack / stats passes)
@@ -3875,7 +4003,9 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
     SME_HIP(hipMemcpyAsync(&h_rmx, cnt + 24, sizeof h_rmx, hipMemcpyDeviceToHost, st));
     SME_HIP(hipMemcpyAsync(h_drange, dmn, sizeof h_drange, hipMemcpyDeviceToHost, st));
     SME_HIP(hipStreamSynchronize(st));
-    const int32_t tbits0 = bits_for((uint64_t)std::max<int64_t>(Vi, 1));
+    // (K6b: the sort keys are word ranks -- on the c4 shard 22 bits, which with the
+    // records' tf bound fit the 32 the single pass asks for, where 24-bit merged ids do not)
+    const int32_t tbits0 = dsplit ? bits_for((uint64_t)std::max<int64_t>(Vw - 1, 1)) : bits_for((uint64_t)std::max<int64_t>(Vi, 1));
     const uint64_t Fq = h_rmx + 1, D = (uint64_t)((int64_t)h_drange[1] - h_drange[0] + 1);
     if (Pb > 0 && Pb < (1ll << 32) && D * Fq < (1ull << 32) && tbits0 + bits_for(Fq - 1) <= 32) {
       fused = true;
@@ -3887,25 +4017,45 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
       ai.dcnt = W[W_T3].as<int64_t>(nR + 1);
       ai.nbig = cnt + 26;
       ai.big_out = W[W_SLOWLIST].as<int64_t>(nR + 1);
-      SME_HIP(hipMemsetAsync(mtf, 0, sizeof(unsigned int), st));
-      const unsigned agg_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
-      hipLaunchKernelGGL(k_agg_w<true>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, nullptr, nullptr, p_term,
-                         nullptr);
-      SME_CHECK_LAUNCH();
-      const int64_t nbig = (int64_t)d2h(cnt + 26, st);
-      if (nbig > 0) {
-        int64_t *bl2 = W[W_BIGL2].as<int64_t>(nbig);
-        sort_pairs_v64<uint64_t>(reinterpret_cast<uint64_t *>(ai.big_out), reinterpret_cast<uint64_t *>(bl2), nullptr,
-                                 nullptr, nbig, 64, cx->ws[120], cx->ws[121], cx->ws[122], st);
-        int64_t *bcap = W[W_BIGCAP].as<int64_t>(nbig + 1), *boff = W[W_RLIST].as<int64_t>(nbig + 1);
-        hipLaunchKernelGGL(k_big_caps, dim3(grid_for(nbig)), dim3(256), 0, st, bl2, nbig, perm, ntok, max_nout, bcap);
-        SME_HIP(hipMemsetAsync(bcap + nbig, 0, sizeof(int64_t), st));
-        excl_scan(bcap, boff, (int64_t)(nbig + 1), cx->ws[23], st);
-        const int64_t gtot = d2h(boff + nbig, st);
-        int32_t *gkeys = W[W_U16].as<int32_t>(gtot), *gcnt = W[W_BOFF].as<int32_t>(gtot);
-        hipLaunchKernelGGL(k_agg_big, dim3((unsigned)std::min<int64_t>(nbig, 4096)), dim3(kAggNT), 0, st, ai, bl2,
-                           nbig, boff, bcap, gkeys, gcnt, nullptr, reg_off, p_term, nullptr, 2);
+      if (dsplit) {  // K6b: docid pairs beside the regions
+        ai.dk_rec = W[W_KHI].as<int32_t>(nR + 1);
+        ai.dv_rec = W[W_VSLOT].as<uint32_t>(nR + 1);
+        ai.dbad = cnt + 32;
+      }
+      auto run_fused = [&]() {
+        SME_HIP(hipMemsetAsync(mtf, 0, sizeof(unsigned int), st));
+        SME_HIP(hipMemsetAsync(cnt + 26, 0, sizeof(unsigned long long), st));
+        if (ai.dk_rec) {
+          SME_HIP(hipMemsetAsync(ai.dk_rec, 0xFF, (size_t)nR * sizeof(int32_t), st));
+          SME_HIP(hipMemsetAsync(ai.dbad, 0, sizeof(unsigned long long), st));
+        }
+        const unsigned agg_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
+        hipLaunchKernelGGL(k_agg_w<true>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, nullptr, nullptr, p_term,
+                           nullptr);
         SME_CHECK_LAUNCH();
+        const int64_t nbig = (int64_t)d2h(cnt + 26, st);
+        if (nbig > 0) {
+          int64_t *bl2 = W[W_BIGL2].as<int64_t>(nbig);
+          sort_pairs_v64<uint64_t>(reinterpret_cast<uint64_t *>(ai.big_out), reinterpret_cast<uint64_t *>(bl2), nullptr,
+                                   nullptr, nbig, 64, cx->ws[120], cx->ws[121], cx->ws[122], st);
+          int64_t *bcap = W[W_BIGCAP].as<int64_t>(nbig + 1), *boff = W[W_RLIST].as<int64_t>(nbig + 1);
+          hipLaunchKernelGGL(k_big_caps, dim3(grid_for(nbig)), dim3(256), 0, st, bl2, nbig, perm, ntok, max_nout, bcap);
+          SME_HIP(hipMemsetAsync(bcap + nbig, 0, sizeof(int64_t), st));
+          excl_scan(bcap, boff, (int64_t)(nbig + 1), cx->ws[23], st);
+          const int64_t gtot = d2h(boff + nbig, st);
+          int32_t *gkeys = W[W_U16].as<int32_t>(gtot), *gcnt = W[W_BOFF].as<int32_t>(gtot);
+          hipLaunchKernelGGL(k_agg_big, dim3((unsigned)std::min<int64_t>(nbig, 4096)), dim3(kAggNT), 0, st, ai, bl2,
+                             nbig, boff, bcap, gkeys, gcnt, nullptr, reg_off, p_term, nullptr, 2);
+          SME_CHECK_LAUNCH();
+        }
+      };
+      run_fused();
+      if (dsplit && d2h(ai.dbad, st) != 0) {  // a record with two docid-term pairs: merged ids, one sort
+        to_merged();
+        ai.dk_rec = nullptr;
+        ai.dv_rec = nullptr;
+        ai.dbad = nullptr;
+        run_fused();
       }
       // exact pair offsets of the records (docno order)
       int64_t *xoff = W[W_NTOK2].as<int64_t>(nR + 1);
@@ -3920,6 +4070,7 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
       sort_nrec = nR;
     }
   }
+  if (dsplit && !(fused && ai.dk_rec)) to_merged();
   if (K == 1 && !fused) {
   int32_t *prec = W[W_PREC].as<int32_t>(nR + 1);
   int64_t *pair_off = W[W_T3].as<int64_t>(nR + 1);  // rank_of_slot no longer needed
@@ -4088,7 +4239,46 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
   prof.mark("aggregate");
 
   // ---------------- K6 sort by term ----------------
-  const int tbits = bits_for((uint64_t)std::max<int64_t>(Vi, 1));
+  // K6b: the docid pairs (one per record at most, docno order) as a list sorted by
+  // docid index j, and every word's (shift, merged id)
+  const bool split = dsplit && ai.dk_rec != nullptr;
+  int64_t Pw = P, Nd = 0;
+  uint32_t *dk = nullptr, *dv = nullptr;
+  uint2 *xw = nullptr;
+  if (split) {
+    uint8_t *dfl = W[W_RREPS].as<uint8_t>(nR + 1);
+    int32_t *didx = W[W_CFINAL].as<int32_t>(nR + 1);
+    hipLaunchKernelGGL(k_dsplit_flags, dim3(grid_for(nR)), dim3(256), 0, st, ai.dk_rec, nR, dfl);
+    SME_HIP(hipMemsetAsync(cnt + 33, 0, 2 * sizeof(unsigned long long), st));
+    select_flagged(dfl, nR, didx, reinterpret_cast<int32_t *>(cnt + 33), cx->ws[25], cx->ws[23], st);
+    dk = W[W_CSTR].as<uint32_t>(nR + 1);
+    dv = W[W_VIDX].as<uint32_t>(nR + 1);
+    hipLaunchKernelGGL(k_dsplit_gather, dim3(grid_for(nR)), dim3(256), 0, st, didx, cnt + 33, ai.dk_rec, ai.dv_rec, dk,
+                       dv, cnt + 34);
+    SME_CHECK_LAUNCH();
+    unsigned long long hd[2];
+    SME_HIP(hipMemcpyAsync(hd, cnt + 33, sizeof hd, hipMemcpyDeviceToHost, st));
+    SME_HIP(hipStreamSynchronize(st));
+    Nd = (int64_t)(uint32_t)hd[0];
+    if (hd[1] != 0 && Nd > 1) {  // docno order is not docid order: a stable sort by j
+      uint32_t *dk2 = W[W_LONG].as<uint32_t>(Nd + 1), *dv2 = reinterpret_cast<uint32_t *>(W[W_OVFKEY].as<uint64_t>(Nd / 2 + 1));
+      uint32_t *rs2 = W[W_RADIX].as<uint32_t>(kv_sort_scratch(Nd) / sizeof(uint32_t) + 1);
+      if (kv_sort<uint32_t>(dk, dv, dk2, dv2, Nd, bits_for((uint64_t)Vd), rs2, st, true) != dv) {
+        dk = dk2;
+        dv = dv2;
+      }
+    }
+    xw = reinterpret_cast<uint2 *>(W[W_DKEY].as<Key16>(Vw / 2 + 1));
+    if (Vw > 0)
+      hipLaunchKernelGGL(k_word_shift, dim3(grid_for(Vw)), dim3(256), 0, st, (const int64_t *)wrank_all, Vw, dk, Nd,
+                         xw);
+    SME_CHECK_LAUNCH();
+    P = Pw + Nd;
+    if (P > 0xFFFFFFFFll) throw Error(SME_ELIMIT, "term sort of more than 2^32 pairs");
+    ix->P = P;
+    prof.mark("docid_pairs");
+  }
+  const int tbits = split ? bits_for((uint64_t)std::max<int64_t>(Vw - 1, 1)) : bits_for((uint64_t)std::max<int64_t>(Vi, 1));
   uint32_t *key_s = W[W_T0].as<uint32_t>(P + 1);
   int64_t Pm = P;
   int32_t max_tf = 1;
@@ -4144,12 +4334,24 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
       wf = ix->d_w.as<double>(P + 1);
       weights_fused = true;
     }
-    key_s = term_sort(p_term, v32, key_s, v32s, sort_nrec, sort_reg, sort_xoff, P, tbits, dmin, F, docno_d, tf_d, rscr,
-                      st, wf ? (const double *)ix->d_lut.p : nullptr, log10((double)(std::max<int64_t>(nR, 0) / 1)), wf,
-                      (int)cx->opt_sort_bits);
+    const double idf_r = log10((double)(std::max<int64_t>(nR, 0) / 1));
+    key_s = term_sort(p_term, v32, key_s, v32s, sort_nrec, sort_reg, sort_xoff, Pw, tbits, dmin, F, docno_d, tf_d, rscr,
+                      st, wf ? (const double *)ix->d_lut.p : nullptr, idf_r, wf, (int)cx->opt_sort_bits, xw, P);
     off = ix->d_off.as<int64_t>(Vi + 1);
     SME_HIP(hipMemsetAsync(off, 0, (Vi + 1) * sizeof(int64_t), st));
-    hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, Vi);
+    if (!split) {
+      hipLaunchKernelGGL(k_term_offsets<false>, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, Vi);
+    } else {
+      // word terms' offsets over the sorted keys (the docid slots are holes), then
+      // the docid terms' offsets and their pairs in the holes
+      hipLaunchKernelGGL(k_term_offsets<true>, dim3(grid_for(P)), dim3(256), 0, st, key_s, P, off, Vi);
+      hipLaunchKernelGGL(k_docid_off, dim3(grid_for(Vd)), dim3(256), 0, st, dk, Nd, Vd, (const int64_t *)drank,
+                         (const int64_t *)wrank_all, Vw, xw, Pw, off);
+      if (Nd > 0)
+        hipLaunchKernelGGL(k_docid_place, dim3(grid_for(Nd)), dim3(256), 0, st, dk, dv, Nd, (const int64_t *)drank,
+                           (const int64_t *)wrank_all, Vw, xw, off, Pw, dmin, F, docno_d, tf_d, key_s,
+                           wf ? (const double *)ix->d_lut.p : nullptr, idf_r, wf);
+    }
     SME_CHECK_LAUNCH();
   } else {
     uint64_t *val_s = W[W_T1].as<uint64_t>(P + 1);
@@ -4167,7 +4369,7 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
     }
     off = ix->d_off.as<int64_t>(Vi + 1);
     SME_HIP(hipMemsetAsync(off, 0, (Vi + 1) * sizeof(int64_t), st));
-    if (Pm > 0) hipLaunchKernelGGL(k_term_offsets, dim3(grid_for(Pm)), dim3(256), 0, st, key_s, Pm, off, Vi);
+    if (Pm > 0) hipLaunchKernelGGL(k_term_offsets<false>, dim3(grid_for(Pm)), dim3(256), 0, st, key_s, Pm, off, Vi);
     docno_d = ix->d_docno_d.as<int32_t>(Pm + 1);
     tf_d = ix->d_tf_d.as<int32_t>(Pm + 1);
     if (Pm > 0) hipLaunchKernelGGL(k_unpack_vals, dim3(grid_for(Pm)), dim3(256), 0, st, val_s, Pm, docno_d, tf_d);

@@ -55,6 +55,7 @@ struct sme_ctx {
   int64_t opt_raw_load_pct = 40;  // "raw_load_pct": raw-vocabulary table load of the next build (10..90)
   int64_t opt_docid_terms = 1;    // "docid_terms": docid terms beside the word vocabulary (K4b; 0 = general path)
   int64_t opt_sort_bits = 11;     // "sort_digit_bits": most bits per digit of the term sort's LSD passes (6..11)
+  int64_t opt_docid_split = 1;    // "docid_split": docid pairs beside the term sort when that saves an LSD pass (K6b)
   int64_t opt_cand_cap = 1024;    // "cand_cap": candidate list per query of k_query_win (1..2048; >= 1024: at least 16 k)
   int64_t opt_seed_m = 64;        // "seed_m": seed postings per term (k_query_seed; 0 = no seed)
   int64_t opt_kgram_rank = 0;     // "kgram_rank": 1 = K >= 2 gram keys by iterated ranking even when packed ids fit
@@ -206,10 +207,12 @@ void chargram_stage(sme_ctx *cx, sme_index *ix, const int32_t *tstream, int64_t 
 // stable LSD radix sort of (term id, packed posting) pairs (sme_sort.hip)
 // (reg != nullptr: the first pass reads pair x from reg[i] + x - xoff[i], record i
 // holding it -- the single-pass aggregation's layout)
+// (xw != nullptr: K6b -- the keys are word ranks; the last pass writes word i's
+// postings shifted by xw[i].x and keyed xw[i].y into Pout slots keyed 0xFFFFFFFF)
 uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t nrec, const int64_t *reg,
                     const int64_t *xoff, int64_t P, int bits, int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf,
                     uint32_t *counts, hipStream_t st, const double *lut = nullptr, double idf = 0.0,
-                    double *w = nullptr, int maxbits = 11);
+                    double *w = nullptr, int maxbits = 11, const uint2 *xw = nullptr, int64_t Pout = 0);
 size_t term_sort_scratch(int64_t P);
 // stable LSD radix sort of (key, u32 value) pairs by the key's low `bits` bits
 // (sme_sort.hip; K = uint32_t or uint64_t); ping-pongs between (k0, v0) and

@@ -248,7 +248,7 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
                                                       uint32_t *__restrict__ oval, int32_t *__restrict__ odocno,
                                                       int32_t *__restrict__ otf, int64_t dmin, uint32_t F,
                                                       Gather g, const double *__restrict__ lut, double idf,
-                                                      double *__restrict__ ow) {
+                                                      double *__restrict__ ow, const uint2 *__restrict__ xw) {
   // wc: per-wave running digit counts, then each (wave, digit)'s first slot in
   // the tile sorted by digit; gd: global offset - tile slot of each digit
   __shared__ uint16_t wc[kRsWaves * kRsMaxBins];
@@ -373,7 +373,13 @@ __global__ __launch_bounds__(kRsNT) void k_rs_scatter(const uint32_t *__restrict
     if (p < n) {
       const uint32_t kk = stage[p];
       dst[j] = gd[(kk >> shift) & mask] + (uint32_t)p;
-      okey[dst[j]] = kk;
+      if (LAST && xw) {  // K6b: word kk's docid shift and merged id
+        const uint2 x = xw[kk];
+        dst[j] += x.x;
+        okey[dst[j]] = x.y;
+      } else {
+        okey[dst[j]] = kk;
+      }
     }
   }
   __syncthreads();
@@ -675,7 +681,8 @@ void rs_scan(uint32_t *gsum, int64_t n, uint32_t *sums, hipStream_t st) {
 // tf.  counts: ceil(P / 16384) * 2048 + 2048 * 256 u32 of scratch.
 uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int64_t nrec, const int64_t *reg,
                     const int64_t *xoff, int64_t P, int bits, int64_t dmin, uint32_t F, int32_t *docno, int32_t *tf,
-                    uint32_t *counts, hipStream_t st, const double *lut, double idf, double *w, int maxbits) {
+                    uint32_t *counts, hipStream_t st, const double *lut, double idf, double *w, int maxbits,
+                    const uint2 *xw, int64_t Pout) {
   if (P <= 0) return k0;
   if (P > 0xFFFFFFFFll) throw Error(SME_ELIMIT, "term sort of more than 2^32 pairs");
   bits = std::max(bits, 1);
@@ -705,12 +712,14 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
     rs_scan(gsum, (int64_t)nbins * G, gsum + kRsMaxBins * kRsGroups, st);
     hipLaunchKernelGGL(k_rs_colscan, dim3(G), dim3(kRsNT), 0, st, counts, ntiles, nbins, tpg, G, gsum);
     const unsigned sgrid = (unsigned)(8 * ((ntiles + 7) / 8));  // see the XCD tile order in k_rs_scatter
+    if (last && xw)  // K6b: the docid pairs' slots stay keyed 0xFFFFFFFF (k_term_offsets<true> skips them)
+      SME_HIP(hipMemsetAsync(k1, 0xFF, (size_t)Pout * sizeof(uint32_t), st));
     if (last)
       hipLaunchKernelGGL(k_rs_scatter<true>, dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, P, shift, nb, counts,
-                         k1, nullptr, docno, tf, dmin, F, g, lut, idf, w);
+                         k1, nullptr, docno, tf, dmin, F, g, lut, idf, w, xw);
     else
       hipLaunchKernelGGL(k_rs_scatter<false>, dim3(sgrid), dim3(kRsNT), 0, st, k0, v0, P, shift, nb,
-                         counts, k1, v1, nullptr, nullptr, dmin, F, g, nullptr, 0.0, nullptr);
+                         counts, k1, v1, nullptr, nullptr, dmin, F, g, nullptr, 0.0, nullptr, nullptr);
     SME_CHECK_LAUNCH();
     std::swap(k0, k1);
     std::swap(v0, v1);

@@ -660,6 +660,33 @@ def _expected_weights(ix, idf_mode, N=None, df_override=None):
 
 
 @pytest.mark.parametrize("idf_mode", [0, 1])
+def test_build_docid_split(sme, synth, idf_mode):
+    """K6b: docid pairs beside the term sort (6-bit digits: 5,000 docid terms
+    beside ~800 word terms take three LSD passes, the words alone two).  The
+    split build's partition records and reduce-order CSR equal the oracle's,
+    and its docno-order CSR, TF-IDF weights and query results equal those of
+    the single sort (docid_split 0), in both idf modes."""
+    n = 5000
+    c = synth.gen_corpus(n, V=800, seed=23, len_lo=20, len_hi=90)
+    ixs = []
+    for split in (1, 0):
+        ix, _ = _check_build(sme, c, synth.docids(n), R=3, idf_mode=idf_mode,
+                             opts={"sort_digit_bits": 6, "docid_split": split})
+        assert ("docid_pairs" in ix.ctx.last_build_profile()) == bool(split)  # the split ran (or not)
+        ixs.append(ix)
+    a, b = ixs
+    for x, y in zip(a.weights(), b.weights()):
+        assert np.array_equal(x, y)
+    assert np.array_equal(a.weights()[2], _expected_weights(a, idf_mode))
+    _, _, _, df = a.csr()
+    terms, qoff = synth.queries_by_df(df, 200, seed=5)
+    for k in (10, 100):
+        d1, s1 = a.query_topk(terms, qoff, k)
+        d2, s2 = b.query_topk(terms, qoff, k)
+        assert np.array_equal(d1, d2) and np.array_equal(s1, s2)
+
+
+@pytest.mark.parametrize("idf_mode", [0, 1])
 def test_weight_pass_and_reweight(sme, synth, idf_mode):
     """The build's fused TF-IDF pass (k_weights) and sme_index_reweight with
     all-reduced statistics: every fp64 weight bit-equal to the reference formula."""
@@ -893,9 +920,9 @@ def _trec(docs):
 
 
 @pytest.mark.parametrize("case", ["ascending", "shuffled", "mixed_forms", "case_twins", "docid_in_text",
-                                  "duplicates"])
-@pytest.mark.parametrize("docid_terms", [1, 0])
-def test_build_docid_terms(sme, synth, case, docid_terms):
+                                  "duplicates", "docid_in_other_text", "mixed_case"])
+@pytest.mark.parametrize("docid_terms,bits", [(1, 11), (0, 11), (1, 6)])
+def test_build_docid_terms(sme, synth, case, docid_terms, bits):
     """K4b: docid terms (T7) beside the word vocabulary.  A record's DOCNO token
     that is its own term (ASCII letters and digits ending in a digit, unchanged by
     Porter2) skips the per-distinct vocabulary work and is ranked by a merge with
@@ -925,7 +952,14 @@ def test_build_docid_terms(sme, synth, case, docid_terms):
     elif case == "duplicates":
         ids[11] = ids[10]
         ids[50] = ids[49]
+    elif case == "docid_in_other_text":
+        bodies[5] += " " + ids[100]  # record 5 holds two docid terms' pairs (K6b falls back to merged ids)
+    elif case == "mixed_case":
+        # docid terms ascend in file order, the mapping's (case-sensitive) docno order differs
+        ids = [("A%07d" if i % 2 == 0 else "a%07d") % i for i in range(n)]
     c = _trec(list(zip(ids, bodies)))
     mapping = sorted(set(ids))
-    _check_build(sme, c, mapping, R=1, opts={"docid_terms": docid_terms})
-    _check_build(sme, c, mapping, R=7, opts={"docid_terms": docid_terms})
+    # bits 6: the word ranks need fewer LSD passes than the merged ids -> the K6b split
+    opts = {"docid_terms": docid_terms, "sort_digit_bits": bits}
+    _check_build(sme, c, mapping, R=1, opts=opts)
+    _check_build(sme, c, mapping, R=7, opts=opts)
