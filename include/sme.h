@@ -118,11 +118,13 @@ void sme_destroy(sme_ctx *ctx);
  *                   digits ending in a digit, unchanged by the stemmer) skips the per-distinct
  *                   vocabulary work and is ranked by a merge with the sorted word terms when the
  *                   docids ascend in file order; 0: every raw token through the general path
- *   "sort_digit_bits"  most bits per digit of the term sort's LSD passes, 6..11 (default 11:
- *                   two passes for up to 2^22 terms)
- *   "docid_split"   1 (default): with docid terms (K4b) whose ids push the term sort to one
- *                   more LSD pass than the word terms need, each record's docid pair is kept
- *                   beside the sort and merged into the CSR after it; 0: one sort of all pairs
+ *   "sort_digit_bits"  most bits per digit of the term sort's LSD passes, 6..11, or 0 (default:
+ *                   11 -- two passes for up to 2^22 terms -- and 8 past 2^30 pairs)
+ *   "docid_split"   1 (default): with docid terms (K4b) that push the term ids past 22 bits
+ *                   while the word terms need fewer, each record's docid pair is kept beside
+ *                   the sort of word-rank keys and merged into the CSR after it; 2: whenever
+ *                   the word ranks need fewer bits than the merged ids; 0: one sort of all
+ *                   pairs by merged id
  *   "query_table_budget"  bytes a batch's skip table may take (default 0 =
  *                   a quarter of the free HBM); a batch over it is split by
  *                   query range, and queries still overflowing their

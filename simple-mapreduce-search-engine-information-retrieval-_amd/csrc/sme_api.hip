@@ -322,10 +322,10 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
       range(0, 1);
       cx->opt_docid_terms = v;
     } else if (n == "sort_digit_bits") {
-      range(6, 11);
+      if (v != 0) range(6, 11);
       cx->opt_sort_bits = v;
     } else if (n == "docid_split") {
-      range(0, 1);
+      range(0, 2);
       cx->opt_docid_split = v;
     } else {
       throw sme::Error(SME_EINVAL, "unknown option " + n);

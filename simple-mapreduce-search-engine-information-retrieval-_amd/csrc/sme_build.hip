@@ -3848,10 +3848,13 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
   int64_t *drank = nullptr, *wrank_all = nullptr;
   // K6b: docid pairs beside the term sort when the word ranks need fewer key bits
   // than the merged ids (c5: 24 -> 15 bits, one LSD pass less; the c4 shard: 24 ->
-  // 22, which with the records' tf bound lets the single-pass aggregation run)
+  // 22, which with the records' tf bound lets the single-pass aggregation run).  Not
+  // below 23 merged bits (c2: 21 -> 20 bits saves no pass; the split costs 0.1 ms)
   bool dsplit = false;
-  if (dfast && job == 0 && cx->cfg.k == 1 && !dup_docno && cx->opt_docid_split && Vd < (int64_t)kDocCode)
-    dsplit = bits_for((uint64_t)std::max<int64_t>(Vw - 1, 1)) < bits_for((uint64_t)std::max<int64_t>(V - 1, 1));
+  if (dfast && job == 0 && cx->cfg.k == 1 && !dup_docno && cx->opt_docid_split && Vd < (int64_t)kDocCode) {
+    const int bm = bits_for((uint64_t)std::max<int64_t>(V - 1, 1));
+    dsplit = (bm > 22 || cx->opt_docid_split == 2) && bits_for((uint64_t)std::max<int64_t>(Vw - 1, 1)) < bm;
+  }
   if (V > 0 && !dfast) {
     int64_t *tlen = W[W_T0].as<int64_t>(Vw + 1);
     hipLaunchKernelGGL(k_final_rank, dim3(grid_for(Vw)), dim3(256), 0, st, order, Vw, vslot, vcs, rank_of_slot, tlen);
@@ -4335,8 +4338,13 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
       weights_fused = true;
     }
     const double idf_r = log10((double)(std::max<int64_t>(nR, 0) / 1));
+    // digit width (sort_digit_bits; 0 = auto): 11, or 8 past 2^30 pairs -- a pass's
+    // per-(tile, digit) counts grow with the pairs, and 2048 digits over an 8192-pair
+    // tile leave 4-pair runs to scatter (c4 shard, 22-bit keys: two 11-bit passes
+    // 34.5 ms, three of <= 8 bits 30.9 ms; c2 / c5 keep 11)
+    const int sort_bits = cx->opt_sort_bits > 0 ? (int)cx->opt_sort_bits : (Pw > (int64_t(1) << 30) ? 8 : 11);
     key_s = term_sort(p_term, v32, key_s, v32s, sort_nrec, sort_reg, sort_xoff, Pw, tbits, dmin, F, docno_d, tf_d, rscr,
-                      st, wf ? (const double *)ix->d_lut.p : nullptr, idf_r, wf, (int)cx->opt_sort_bits, xw, P);
+                      st, wf ? (const double *)ix->d_lut.p : nullptr, idf_r, wf, sort_bits, xw, P);
     off = ix->d_off.as<int64_t>(Vi + 1);
     SME_HIP(hipMemsetAsync(off, 0, (Vi + 1) * sizeof(int64_t), st));
     if (!split) {

@@ -54,8 +54,8 @@ struct sme_ctx {
   int64_t opt_tok_grid = 4096;    // "tok_grid": tokenizer workgroups (>= 1)
   int64_t opt_raw_load_pct = 40;  // "raw_load_pct": raw-vocabulary table load of the next build (10..90)
   int64_t opt_docid_terms = 1;    // "docid_terms": docid terms beside the word vocabulary (K4b; 0 = general path)
-  int64_t opt_sort_bits = 11;     // "sort_digit_bits": most bits per digit of the term sort's LSD passes (6..11)
-  int64_t opt_docid_split = 1;    // "docid_split": docid pairs beside the term sort when that saves an LSD pass (K6b)
+  int64_t opt_sort_bits = 0;      // "sort_digit_bits": most bits per digit of the term sort's LSD passes (6..11; 0 auto)
+  int64_t opt_docid_split = 1;    // "docid_split": docid pairs beside the term sort (K6b): 1 past 22 merged id bits, 2 whenever the words need fewer, 0 never
   int64_t opt_cand_cap = 1024;    // "cand_cap": candidate list per query of k_query_win (1..2048; >= 1024: at least 16 k)
   int64_t opt_seed_m = 64;        // "seed_m": seed postings per term (k_query_seed; 0 = no seed)
   int64_t opt_kgram_rank = 0;     // "kgram_rank": 1 = K >= 2 gram keys by iterated ranking even when packed ids fit

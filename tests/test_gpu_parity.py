@@ -671,7 +671,7 @@ def test_build_docid_split(sme, synth, idf_mode):
     ixs = []
     for split in (1, 0):
         ix, _ = _check_build(sme, c, synth.docids(n), R=3, idf_mode=idf_mode,
-                             opts={"sort_digit_bits": 6, "docid_split": split})
+                             opts={"sort_digit_bits": 6, "docid_split": 2 * split})
         assert ("docid_pairs" in ix.ctx.last_build_profile()) == bool(split)  # the split ran (or not)
         ixs.append(ix)
     a, b = ixs
@@ -959,7 +959,7 @@ def test_build_docid_terms(sme, synth, case, docid_terms, bits):
         ids = [("A%07d" if i % 2 == 0 else "a%07d") % i for i in range(n)]
     c = _trec(list(zip(ids, bodies)))
     mapping = sorted(set(ids))
-    # bits 6: the word ranks need fewer LSD passes than the merged ids -> the K6b split
-    opts = {"docid_terms": docid_terms, "sort_digit_bits": bits}
+    # bits 6: the K6b split forced (docid_split 2), with more LSD passes than the words' two
+    opts = {"docid_terms": docid_terms, "sort_digit_bits": bits, "docid_split": 2 if bits == 6 else 1}
     _check_build(sme, c, mapping, R=1, opts=opts)
     _check_build(sme, c, mapping, R=7, opts=opts)
