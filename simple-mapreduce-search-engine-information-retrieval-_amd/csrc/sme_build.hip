@@ -2372,11 +2372,41 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
   const int64_t nwaves = (int64_t)gridDim.x * (kAggNT / 64);
   uint32_t wmax = 0;  // count pass / single pass: largest tf over this wave's records
   const bool fused = EMIT && in.reg_off != nullptr;
-  for (int64_t i = (int64_t)blockIdx.x * (kAggNT / 64) + wv; i < nR; i += nwaves) {
-    if (EMIT && !fused && prec[i] < 0) continue;  // big record: block path
-    const int64_t r = in.perm[i];
-    const uint32_t *ts = in.tokstream + (in.rs[r] >> 1);
-    const int32_t nt = in.ntok[r];
+  const int32_t max_nout = max(in.max_nout ? *in.max_nout : 1, 1);
+  // software pipeline over the wave's records: the next record's metadata (its
+  // record index, token-stream offset, token count, docno, pair base) loads while
+  // this one runs, and the record index after it -- a short record (c5: ~56
+  // tokens) otherwise waits on three dependent global loads before its first
+  // token load
+  struct Meta {
+    int64_t r, base;
+    uint64_t rs;
+    int32_t nt, dn, pr;
+  };
+  auto load_meta = [&](int64_t j, int64_t r) {
+    Meta m{r, 0, 0, 0, 0, 0};
+    if (j < nR) {
+      m.rs = in.rs[r];
+      m.nt = in.ntok[r];
+      if (EMIT) {
+        m.dn = in.docno[r];
+        m.base = fused ? in.reg_off[j] : pair_off[j];
+        if (!fused) m.pr = prec[j];
+      }
+    }
+    return m;
+  };
+  const int64_t i0 = (int64_t)blockIdx.x * (kAggNT / 64) + wv;
+  Meta cur = load_meta(i0, i0 < nR ? in.perm[i0] : 0);
+  int64_t rn = i0 + nwaves < nR ? in.perm[i0 + nwaves] : 0;
+  for (int64_t i = i0; i < nR; i += nwaves) {
+    const Meta nxt = load_meta(i + nwaves, rn);
+    rn = i + 2 * nwaves < nR ? in.perm[i + 2 * nwaves] : 0;
+    const Meta m = cur;
+    cur = nxt;
+    if (EMIT && !fused && m.pr < 0) continue;  // big record: block path
+    const uint32_t *ts = in.tokstream + (m.rs >> 1);
+    const int32_t nt = m.nt;
     // table of cap slots: 2 x the token count (load <= 1/2 when every token has
     // one term), so short records clear and scan little; a record whose terms do
     // not fit goes to the big-record path
@@ -2390,7 +2420,7 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
     // the u16 counts hold up to 65535: bound the record's TERM count (a raw token
     // can yield up to max_nout terms, e.g. a dotted split), not its token count;
     // beyond it the record takes the big-record path
-    bool ok = (int64_t)nt * (int64_t)max(in.max_nout ? *in.max_nout : 1, 1) < 65536;
+    bool ok = (int64_t)nt * (int64_t)max_nout < 65536;
     // kAggU tokens per lane step: their stream loads, then their raw_term
     // gathers, are in flight together (one step was two dependent latencies)
     for (int32_t t0 = lane; t0 < nt; t0 += kAggU * 64) {
@@ -2428,8 +2458,9 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
       wave_sync_lds();
       continue;
     }
-    int64_t base = fused ? in.reg_off[i] : pair_off[i];
-    const uint64_t dn = (uint64_t)(uint32_t)in.docno[r] << 32;
+    int64_t base = m.base;
+    const uint64_t dn = (uint64_t)(uint32_t)m.dn << 32;
+    const uint32_t vdoc = (uint32_t)(((int64_t)m.dn - in.dmin) * (int64_t)in.F);
     int32_t nd = 0;  // K6b: docid pairs kept beside the region
     for (uint32_t k = 0; k < cap; k += 64) {
       const int32_t key = keys[k + lane];
@@ -2439,12 +2470,12 @@ __global__ __launch_bounds__(kAggNT) void k_agg_w(AggIn in, int64_t nR, int32_t 
         const int32_t c = cnt_at(k + lane);
         if (isd) {  // (plain stores: a second docid pair in the record is caught by nd below)
           in.dk_rec[i] = key & ~kDocCode;
-          in.dv_rec[i] = (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c);
+          in.dv_rec[i] = vdoc + (uint32_t)c;
         } else {
           const int64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
           st_stream(p_term + o, (uint32_t)key);
           if (in.v32)
-            st_stream(in.v32 + o, (uint32_t)(((int64_t)in.docno[r] - in.dmin) * (int64_t)in.F + c));
+            st_stream(in.v32 + o, vdoc + (uint32_t)c);
           else
             p_val[o] = dn | (uint32_t)c;
         }
