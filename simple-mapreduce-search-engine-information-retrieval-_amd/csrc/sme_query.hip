@@ -478,22 +478,6 @@ __global__ __launch_bounds__(256) void k_heavy_fill(const int64_t *hpre, int64_t
     }
   }
 }
-// bm16[i] = largest tf byte of 16-document block i (flat over all rows: a row is
-// T * 64 blocks, its tf row T * 64 * 16 bytes, so the indexing is the same)
-__global__ void k_heavy_bm16(const uint4 *tfrow, int64_t n, uint8_t *bm16) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint4 v = tfrow[i];
-    bm16[i] = (uint8_t)max(max(max_u8x4(v.x), max_u8x4(v.y)), max(max_u8x4(v.z), max_u8x4(v.w)));
-  }
-}
-// sbq[i] = largest impact byte of the 4-document sub-block i of the impact rows
-// (flat over all rows, like bm16): k_query_win's second-level bound
-__global__ void k_heavy_sbq(const uint4 *imp, int64_t n, uint32_t *sbq) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint4 v = imp[i];
-    sbq[i] = max_u8x4(v.x) | (max_u8x4(v.y) << 8) | (max_u8x4(v.z) << 16) | (max_u8x4(v.w) << 24);
-  }
-}
 // bm1k[i] = largest of the 64 block maxima of tile i
 __global__ void k_heavy_bm1k(const uint4 *bm16, int64_t n, uint8_t *bm1k) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -2075,10 +2059,12 @@ __global__ void k_reset_cnt(const int32_t *qlist, int n, unsigned int *ccnt, uns
   }
 }
 
-// impact rows from tf rows: q(tf) = floor(lut[tf] * idf * alpha) + 1 (0 for tf = 0)
-__global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const int32_t *hterm, int64_t H,
-                                                   int64_t stride, const double *lut, int max_tf, const double *idf,
-                                                   double alpha, uint8_t *imp) {
+// impact rows q(tf) = floor(lut[tf] * idf * alpha) + 1 (0 for tf = 0), 16-document
+// tf maxima (bm16) and 4-document impact maxima (sbq) in one pass over the tf rows: thread = one 16-byte block of 16 documents (the
+// three used to re-read the tf and impact rows in separate passes)
+__global__ __launch_bounds__(256) void k_heavy_imp3(const uint8_t *tfrow, const int32_t *hterm, int64_t H,
+                                                    int64_t stride, const double *lut, int max_tf, const double *idf,
+                                                    double alpha, uint8_t *imp, uint8_t *bm16, uint32_t *sbq) {
   __shared__ uint8_t ql[256];
   const int64_t chunks = stride >> 12;  // 4096-byte chunks per row
   for (int64_t c = blockIdx.x; c < H * chunks; c += gridDim.x) {
@@ -2088,16 +2074,17 @@ __global__ __launch_bounds__(256) void k_heavy_imp(const uint8_t *tfrow, const i
     const int f = threadIdx.x;
     ql[f] = (uint8_t)(f == 0 ? 0u : f <= max_tf ? impact(lut[f], wi, alpha) : 255u);
     __syncthreads();
-    const uint4 *src = reinterpret_cast<const uint4 *>(tfrow + c * 4096);
-    const uint4 v = src[threadIdx.x];
+    const int64_t i = c * 256 + threadIdx.x;  // flat 16-document block
+    const uint4 v = reinterpret_cast<const uint4 *>(tfrow)[i];
     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-    uint4 *dst = reinterpret_cast<uint4 *>(imp + c * 4096);
     uint32_t o[4];
 #pragma unroll
     for (int u = 0; u < 4; u++)
       o[u] = (uint32_t)ql[w4[u] & 0xFF] | ((uint32_t)ql[(w4[u] >> 8) & 0xFF] << 8) |
              ((uint32_t)ql[(w4[u] >> 16) & 0xFF] << 16) | ((uint32_t)ql[w4[u] >> 24] << 24);
-    dst[threadIdx.x] = make_uint4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<uint4 *>(imp)[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    bm16[i] = (uint8_t)max(max(max_u8x4(v.x), max_u8x4(v.y)), max(max_u8x4(v.z), max_u8x4(v.w)));
+    sbq[i] = max_u8x4(o[0]) | (max_u8x4(o[1]) << 8) | (max_u8x4(o[2]) << 16) | (max_u8x4(o[3]) << 24);
   }
 }
 // k_query_win's sparse posting words (index-resident, like the impact rows):
@@ -2216,15 +2203,11 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
       hipLaunchKernelGGL(k_heavy_fill, dim3(16384), dim3(256), 0, st, hpre, H, hterm, off,
                          (const int32_t *)ix->d_docno_d.p, (const int32_t *)ix->d_tf_d.p, ix->dmin, stride, tfrow);
       const int64_t n16 = H * (T << 6), n1k = H * T;
-      hipLaunchKernelGGL(k_heavy_bm16, dim3((unsigned)std::min<int64_t>((n16 + 255) / 256, 1 << 16)), dim3(256), 0,
-                         st, (const uint4 *)tfrow, n16, bm16);
+      hipLaunchKernelGGL(k_heavy_imp3, dim3((unsigned)std::min<int64_t>(H * (stride >> 12), 1 << 16)), dim3(256), 0, st,
+                         tfrow, hterm, H, stride, (const double *)ix->d_lut.p, ix->max_tf,
+                         (const double *)ix->d_idf.p, ix->q_alpha, imp, bm16, reinterpret_cast<uint32_t *>(sbq));
       hipLaunchKernelGGL(k_heavy_bm1k, dim3((unsigned)std::min<int64_t>((n1k + 255) / 256, 1 << 16)), dim3(256), 0,
                          st, (const uint4 *)bm16, n1k, bm1k);
-      hipLaunchKernelGGL(k_heavy_imp, dim3((unsigned)std::min<int64_t>(H * (stride >> 12), 1 << 16)), dim3(256), 0, st,
-                         tfrow, hterm, H, stride, (const double *)ix->d_lut.p, ix->max_tf,
-                         (const double *)ix->d_idf.p, ix->q_alpha, imp);
-      hipLaunchKernelGGL(k_heavy_sbq, dim3((unsigned)std::min<int64_t>((n16 + 255) / 256, 1 << 16)), dim3(256), 0, st,
-                         (const uint4 *)imp, n16, reinterpret_cast<uint32_t *>(sbq));
       SME_CHECK_LAUNCH();
       ix->q_imp = imp;
       ix->q_sbq = sbq;
