@@ -203,6 +203,9 @@ def main():
     # every rank loads the global mapping (all docids), so docnos are global
     mapping = synth.mapping_bytes(n_total)
     ctx = sme.Context(k=1, num_partitions=1, device=local)
+    # SME_BENCH_OPTS="name=value,...": result-preserving path options (sme_set_option) for A/B runs
+    for kv in filter(None, os.environ.get("SME_BENCH_OPTS", "").split(",")):
+        ctx.set_option(kv.split("=")[0], int(kv.split("=")[1]))
     ctx.load_docno_mapping(mapping)
     stream = torch.cuda.current_stream().cuda_stream
 

@@ -793,11 +793,22 @@ constexpr int kStageV = kTokNT * kTokWords + 64;  // staged 16-byte words: chunk
 constexpr int kRecWin = 384 * (kTokNT / 256);  // records overlapping one chunk: fast-path records are >= kMinFastRec bytes
 constexpr int kTokCap = 2560 * (kTokNT / 256);  // chunk tokens per round (a c2 16 KiB chunk holds ~1950; more take further rounds)
 constexpr int kTokMiss = 256;  // deferred raw-vocabulary inserts per round (more: inserted in place)
+// SME_TOK_V2 (default 1): every probe lane stores its token's raw slot straight to
+// the token stream (the lanes of a wave hold consecutive chunk ranks, so the
+// stores stay coalesced), so tl keeps only the 16-bit start positions, the
+// record ids are read from frec where a record ends, and the store pass and its
+// barrier are gone: 37.9 -> 31.3 KB of LDS, five workgroups per CU instead of four
+#ifndef SME_TOK_V2
+#define SME_TOK_V2 1
+#endif
+// V2: five workgroups per CU (its 31.3 KB of LDS) with one token per lane step in
+// the probe pass (96 VGPRs, no spills; two tokens per step spill at five):
+// c2 k_tok_fast 8.46 -> 7.87 ms
 #ifndef SME_TOKOCC
-#define SME_TOKOCC (1024 / SME_TOKNT)
+#define SME_TOKOCC (SME_TOK_V2 ? 1280 / SME_TOKNT : 1024 / SME_TOKNT)
 #endif
 #ifndef SME_TOKG
-#define SME_TOKG 2
+#define SME_TOKG (SME_TOK_V2 ? 1 : 2)
 #endif
 constexpr int kTokG = SME_TOKG;  // tokens per lane step in the probe pass
 #ifndef SME_FASTPROBES
@@ -845,11 +856,17 @@ struct TokLds {
   int32_t rs[kRecWin], re[kRecWin];  // chunk-relative, clamped
   int64_t tbase0;                    // tokstream offset (rs >> 1) of window record 0 (others: from rs)
   int32_t c0[kRecWin];
+#if !SME_TOK_V2
   int32_t rid[kRecWin];               // record index
+#endif
   uint64_t emask[kTokNT];             // token-end bytes of every lane's 64: split, outside a fast record, record start
   int32_t sc32[kTokNT / 64 + 1];
   uint32_t cls[256];                  // byte class: bit 0 split byte, bit 16 span starter ('<' or '&')
+#if SME_TOK_V2
+  uint16_t tl[kTokCap];               // round's chunk tokens by rank: start position (< 2^15)
+#else
   uint32_t tl[kTokCap];               // round's chunk tokens by rank: start position, then raw slot
+#endif
   int32_t miss[kTokMiss];             // round's tokens whose probe found no slot: inserted together
   int32_t nmiss;
 };
@@ -998,7 +1015,9 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
       L.rs[i] = ok ? (int32_t)max<int64_t>(a - c_lo, -1) : kFar;
       L.re[i] = ok ? (int32_t)min<int64_t>(b - c_lo, kFar) : kFar;
       if (i == 0) L.tbase0 = ok ? (a >> 1) : 0;
+#if !SME_TOK_V2
       L.rid[i] = ok ? r : -1;
+#endif
       L.c0[i] = 0;
     }
     for (int i = tid; i < kStageV; i += kTokNT) {
@@ -1109,7 +1128,11 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
       const int32_t last = L.re[k] - 1;
       if (last >= p0 && last < p0 + kTokBytes) {
         const int32_t r0k = k == 0 ? L.c0[0] - carry0 : L.c0[k];
+#if SME_TOK_V2
+        ntok[frec[fcur + k]] = base + __popcll(keep_all & ((1ull << (last - p0)) - 1ull)) - r0k;
+#else
         ntok[L.rid[k]] = base + __popcll(keep_all & ((1ull << (last - p0)) - 1ull)) - r0k;
+#endif
       }
     }
     // next chunk: records wholly before it are dropped from the window; the one
@@ -1136,6 +1159,24 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
       nk = lo;
     }
     auto fr = [&](int k) { return (k == 0 && L.rs[0] < 0) ? 0 : L.c0[k]; };
+#if SME_TOK_V2
+    // token stream index of chunk token i of window record k
+    auto dest_of = [&](int k, int32_t i) -> int64_t {
+      const int32_t r0k = k == 0 ? L.c0[0] - carry0 : L.c0[k];
+      const int64_t tbse = k == 0 ? L.tbase0 : ((c_lo + L.rs[k]) >> 1);
+      return tbse + (i - r0k);
+    };
+    // last window record k < nk with fr(k) <= i
+    auto rec_of = [&](int32_t i) -> int {
+      int lo = 0, hi = nk;
+      while (hi - lo > 1) {
+        const int m = (lo + hi) >> 1;
+        if (fr(m) <= i) lo = m;
+        else hi = m;
+      }
+      return lo;
+    };
+#endif
     for (int32_t rlo = 0; rlo < ((texp & 16) ? 0 : blk_cnt); rlo += kTokCap) {  // (16: no token passes)
       const int32_t nr = min(kTokCap, blk_cnt - rlo);
       // pass 2: start positions of the round's tokens by chunk rank
@@ -1147,7 +1188,7 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
           while (keep) {
             const int i0 = __ffsll((unsigned long long)keep) - 1;
             keep &= keep - 1;
-            if (idx >= 0 && idx < nr) L.tl[idx] = (uint32_t)(p0 + i0);
+            if (idx >= 0 && idx < nr) L.tl[idx] = (std::remove_reference_t<decltype(L.tl[0])>)(p0 + i0);
             idx++;
           }
         }
@@ -1155,6 +1196,9 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
       __syncthreads();
       // pass 3: signature + raw-vocabulary slot, kTokG tokens per lane step (their
       // home-slot loads in flight together)
+#if SME_TOK_V2
+      int kc = tid < nr ? rec_of(rlo + tid) : 0;  // record of the lane's next token (ranks ascend)
+#endif
       for (int32_t r0 = (texp & 1) ? nr : tid; r0 < nr; r0 += kTokG * kTokNT) {
         TokSig g[kTokG];
         int32_t len[kTokG], x[kTokG];
@@ -1172,6 +1216,11 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
         for (int u = 0; u < kTokG; u++) {
           const int32_t r = r0 + u * kTokNT;
           if (r < nr) {
+#if SME_TOK_V2
+            const int32_t ci = rlo + r;
+            while (kc + 1 < nk && fr(kc + 1) <= ci) kc++;
+            uint32_t *const dst = tokstream + dest_of(kc, ci);
+#endif
             // linear probing over occupied slots of other tokens with plain
             // loads (a slot, once filled, never changes); an empty-looking slot,
             // a token of >= 16 bytes or a long probe run take raw_insert
@@ -1190,7 +1239,11 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
               }
             }
             if (hit || (texp & 12)) {  // (timing experiments 4 / 8: no insert / no probe walk)
+#if SME_TOK_V2
+              if (!(texp & 2)) st_stream(dst, (uint32_t)sl);
+#else
               L.tl[r] = (uint32_t)sl;
+#endif
             } else {
               // a new raw token (or a long / contended probe): inserted after the
               // probe pass, with the round's other inserts, so a wave waits on one
@@ -1199,7 +1252,11 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
               if (k < kTokMiss)
                 L.miss[k] = r;
               else
+#if SME_TOK_V2
+                *dst = raw_insert(tb, g[u], (uint64_t)(c_lo + x[u]), (uint64_t)len[u], SlotVal{0, 0, 0, 0});
+#else
                 L.tl[r] = raw_insert(tb, g[u], (uint64_t)(c_lo + x[u]), (uint64_t)len[u], SlotVal{0, 0, 0, 0});
+#endif
             }
           }
         }
@@ -1213,8 +1270,17 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
         TokSig g;
         int32_t len;
         tok_sig_at(L, t, c_lo, x, &g, &len);
+#if SME_TOK_V2
+        tokstream[dest_of(rec_of(rlo + r), rlo + r)] =
+            raw_insert(tb, g, (uint64_t)(c_lo + x), (uint64_t)len, SlotVal{0, 0, 0, 0});
+#else
         L.tl[r] = raw_insert(tb, g, (uint64_t)(c_lo + x), (uint64_t)len, SlotVal{0, 0, 0, 0});
+#endif
       }
+#if SME_TOK_V2
+      if (rlo + kTokCap < blk_cnt) __syncthreads();  // the next round rewrites tl / miss
+    }
+#else
       __syncthreads();
       // pass 4: coalesced stores: chunk token i belongs to the last window record
       // whose first chunk token is <= i (records without tokens share that rank
@@ -1240,6 +1306,7 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
       }
       if (rlo + kTokCap < blk_cnt) __syncthreads();  // the next round rewrites tl
     }
+#endif
     __syncthreads();  // LDS is overwritten by the next chunk (s_adv / sc32[0] are rewritten only after
                       // the next chunk's staging barrier)
     fcur += s_adv;

@@ -704,7 +704,11 @@ uint32_t *term_sort(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, int6
   int shift = 0;
   for (int p = 0; p < npass; p++) {
     const Gather g = p == 0 ? g0 : Gather{nullptr, nullptr, nullptr, 0};
+#ifdef SME_RS_LOFIRST  // (experiment: the narrower digit first)
+    const int nb = (bits - shift) / (npass - p);
+#else
     const int nb = (bits - shift + (npass - p) - 1) / (npass - p);  // near-equal digits
+#endif
     const int nbins = 1 << nb;
     const bool last = p == npass - 1;
     hipLaunchKernelGGL(k_rs_count, dim3((unsigned)ntiles), dim3(kRsNT), 0, st, k0, P, shift, nbins, counts, g);
