@@ -112,6 +112,7 @@ void sme_destroy(sme_ctx *ctx);
  *   "agg_two_pass"  1 count + emit aggregation passes (default 0: single pass)
  *   "kgram_rank"    1: K >= 2 gram keys by iterated ranking (the path of K * ceil(log2 V) > 63)
  *                   even when the packed term ids fit 64 bits (default 0: automatic)
+ *   "agg_grid"      aggregation workgroups, 0 = auto (default 0)
  *   "tok_grid"      tokenizer workgroups, >= 1 (default 5120)
  *   "raw_load_pct"  raw-vocabulary table load of the next build, 10..90 (default 40)
  *   "docid_terms"   1 (default): a record's DOCNO token that is its own term (ASCII letters and

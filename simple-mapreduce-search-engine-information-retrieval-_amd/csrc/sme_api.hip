@@ -288,6 +288,9 @@ int sme_set_option(sme_ctx *cx, const char *name, int64_t v) {
     } else if (n == "agg_two_pass") {
       range(0, 1);
       cx->opt_agg_two_pass = v;
+    } else if (n == "agg_grid") {
+      range(0, int64_t(1) << 30);
+      cx->opt_agg_grid = v;
     } else if (n == "tok_grid") {
       range(1, int64_t(1) << 30);
       cx->opt_tok_grid = v;

@@ -534,7 +534,10 @@ __global__ __launch_bounds__(256) void k_docno(const uint8_t *t, int64_t n, cons
 }
 
 // mark records that contain a complex '<' (sorted complex list)
-constexpr int64_t kMinFastRec = 48;
+#ifndef SME_MINFASTREC
+#define SME_MINFASTREC 48
+#endif
+constexpr int64_t kMinFastRec = SME_MINFASTREC;
 
 __global__ void k_mark_slow(const uint64_t *rs, const uint64_t *re, int64_t nR, const uint64_t *C, int64_t nC,
                             uint8_t *slow, unsigned long long *nslow) {
@@ -789,10 +792,20 @@ constexpr int kTokNT = SME_TOKNT;  // lanes per workgroup (one 64-byte lane slic
 constexpr int kTokWords = 4;                      // 16-byte words per lane
 constexpr int kTokBytes = 16 * kTokWords;         // 64 bytes per lane
 constexpr int kChunk = kTokNT * kTokBytes;        // 16 KiB of text per block step
-constexpr int kStageV = kTokNT * kTokWords + 64;  // staged 16-byte words: chunk + 1 KiB lookahead
-constexpr int kRecWin = 384 * (kTokNT / 256);  // records overlapping one chunk: fast-path records are >= kMinFastRec bytes
-constexpr int kTokCap = 2560 * (kTokNT / 256);  // chunk tokens per round (a c2 16 KiB chunk holds ~1950; more take further rounds)
-constexpr int kTokMiss = 256;  // deferred raw-vocabulary inserts per round (more: inserted in place)
+#ifndef SME_TOKLA
+#define SME_TOKLA 64
+#endif
+constexpr int kStageV = kTokNT * kTokWords + SME_TOKLA;  // staged 16-byte words: chunk + lookahead (1 KiB)
+constexpr int kRecWin = (SME_MINFASTREC >= 72 ? 256 : 384) * (kTokNT / 256);  // records overlapping one chunk: fast-path records are >= kMinFastRec bytes
+static_assert(16384 / SME_MINFASTREC + 2 <= 384, "kRecWin");
+#ifndef SME_TOKCAP
+#define SME_TOKCAP 2560
+#endif
+constexpr int kTokCap = SME_TOKCAP * (kTokNT / 256);  // chunk tokens per round (a c2 16 KiB chunk holds ~1950; more take further rounds)
+#ifndef SME_TOKMISS
+#define SME_TOKMISS 256
+#endif
+constexpr int kTokMiss = SME_TOKMISS;  // deferred raw-vocabulary inserts per round (more: inserted in place)
 // SME_TOK_V2 (default 1): every probe lane stores its token's raw slot straight to
 // the token stream (the lanes of a wave hold consecutive chunk ranks, so the
 // stores stay coalesced), so tl keeps only the 16-bit start positions, the
@@ -2425,6 +2438,13 @@ __device__ __forceinline__ bool aggw_insert(int32_t *keys, uint32_t *cnt2, int32
     h = (h + 1) & (cap - 1);
   }
   return false;
+}
+
+// aggregation workgroups: one wave per record in turn, at most 8192 workgroups
+// ("agg_grid" overrides)
+static unsigned agg_grid_for(const sme_ctx *cx, int64_t nR) {
+  const int64_t g = cx->opt_agg_grid > 0 ? cx->opt_agg_grid : 8192;
+  return (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), g);
 }
 
 template <bool EMIT>
@@ -4130,7 +4150,7 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
           SME_HIP(hipMemsetAsync(ai.dk_rec, 0xFF, (size_t)nR * sizeof(int32_t), st));
           SME_HIP(hipMemsetAsync(ai.dbad, 0, sizeof(unsigned long long), st));
         }
-        const unsigned agg_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
+        const unsigned agg_grid = agg_grid_for(cx, nR);
         hipLaunchKernelGGL(k_agg_w<true>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, nullptr, nullptr, p_term,
                            nullptr);
         SME_CHECK_LAUNCH();
@@ -4175,7 +4195,7 @@ vocab_again:  // (a docid term equal to a word term: the general path, from here
   if (K == 1 && !fused) {
   int32_t *prec = W[W_PREC].as<int32_t>(nR + 1);
   int64_t *pair_off = W[W_T3].as<int64_t>(nR + 1);  // rank_of_slot no longer needed
-  unsigned agg_grid = (unsigned)std::min<int64_t>(std::max<int64_t>((nR + 3) / 4, 1), 8192);
+  unsigned agg_grid = agg_grid_for(cx, nR);
   if (nR > 0) {
     hipLaunchKernelGGL(k_agg_w<false>, dim3(agg_grid), dim3(kAggNT), 0, st, ai, nR, prec, nullptr, nullptr, nullptr);
     SME_CHECK_LAUNCH();

@@ -51,6 +51,7 @@ struct sme_ctx {
   int64_t opt_seed_tiles = 4;     // "seed_tiles": best-bound tiles scored before the sweep (0..8)
   int64_t opt_query_order = 1;    // "query_order": 1 heaviest-term query order, 0 batch order
   int64_t opt_agg_two_pass = 0;   // "agg_two_pass": 1 = count + emit aggregation passes
+  int64_t opt_agg_grid = 0;      // "agg_grid": aggregation workgroups (0 = auto)
   int64_t opt_tok_grid = 5120;    // "tok_grid": tokenizer workgroups (>= 1): four rounds of 5 per CU x 256 CUs
   int64_t opt_raw_load_pct = 40;  // "raw_load_pct": raw-vocabulary table load of the next build (10..90)
   int64_t opt_docid_terms = 1;    // "docid_terms": docid terms beside the word vocabulary (K4b; 0 = general path)
