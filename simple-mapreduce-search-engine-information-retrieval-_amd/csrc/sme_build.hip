@@ -814,6 +814,11 @@ constexpr int kTokMiss = SME_TOKMISS;  // deferred raw-vocabulary inserts per ro
 #ifndef SME_TOK_V2
 #define SME_TOK_V2 1
 #endif
+// SME_TOK_V3: one-barrier block scans and per-wave deferred inserts (no block
+// barrier between the probe pass and the inserts): c2 k_tok_fast 7.12 -> 6.88 ms
+#ifndef SME_TOK_V3
+#define SME_TOK_V3 1
+#endif
 // V2: five workgroups per CU (its 31.3 KB of LDS) with one token per lane step in
 // the probe pass (96 VGPRs, no spills; two tokens per step spill at five):
 // c2 k_tok_fast 8.46 -> 7.87 ms
@@ -874,6 +879,10 @@ struct TokLds {
 #endif
   uint64_t emask[kTokNT];             // token-end bytes of every lane's 64: split, outside a fast record, record start
   int32_t sc32[kTokNT / 64 + 1];
+#if SME_TOK_V3
+  int32_t sm32[kTokNT / 64];          // the max scan's wave totals (sc32: the sum scan's)
+  int32_t nmissw[kTokNT / 64];        // per-wave deferred inserts (miss[64 w ..])
+#endif
   uint32_t cls[256];                  // byte class: bit 0 split byte, bit 16 span starter ('<' or '&')
 #if SME_TOK_V2
   uint16_t tl[kTokCap];               // round's chunk tokens by rank: start position (< 2^15)
@@ -992,6 +1001,45 @@ __device__ __forceinline__ void tok_sig_at(const TokLds &L, const uint8_t *t, in
 __device__ __forceinline__ bool slot_hit16(const ulonglong2 &v, const TokSig &g, int32_t len) {
   return len < 16 && v.x == g.w0 && v.y == g.w1;
 }
+
+#if SME_TOK_V3
+// one-barrier block scans: every thread reads the NT/64 wave totals itself (no
+// serial step, no trailing barrier: a scratch array is next written a chunk later,
+// after further barriers)
+template <int NT, typename T>
+__device__ __forceinline__ T tok_block_excl_sum(T v, T *scratch, T *total) {
+  const int w = threadIdx.x >> 6, l = lane_id();
+  const T inc = wave_incl_sum(v);
+  if (l == 63) scratch[w] = inc;
+  __syncthreads();
+  T pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) {
+    const T t = scratch[i];
+    pre += i < w ? t : (T)0;
+    tot += t;
+  }
+  *total = tot;
+  return pre + inc - v;
+}
+template <int NT>
+__device__ __forceinline__ int32_t tok_block_excl_max(int32_t v, int32_t lo, int32_t *scratch, int32_t *total) {
+  const int w = threadIdx.x >> 6, l = lane_id();
+  const int32_t inc = wave_incl_max(v);
+  const int32_t exc = __builtin_amdgcn_update_dpp(lo, inc, 0x138, 0xF, 0xF, false);  // wave_shr:1 (lane 0: lo)
+  if (l == 63) scratch[w] = inc;
+  __syncthreads();
+  int32_t pre = lo, tot = lo;
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) {
+    const int32_t t = scratch[i];
+    pre = i < w ? max(pre, t) : pre;
+    tot = max(tot, t);
+  }
+  *total = tot;
+  return max(pre, exc);
+}
+#endif
 
 // rs_g / re_g: record bounds of the fast records in frec order (rsF[f] = rs[frec[f]])
 __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *__restrict__ t, int64_t n,
@@ -1123,14 +1171,22 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
       }
     }
     int32_t blk_max;
+#if SME_TOK_V3
+    int32_t before = tok_block_excl_max<kTokNT>(lane_max, -1, L.sm32, &blk_max);
+#else
     int32_t before = block_excl_max<kTokNT, int32_t>(lane_max, -1, L.sc32, &blk_max);
+#endif
     before = before > mc ? before : mc;
     // candidates at or below `before` lie inside a span begun in an earlier lane
     const int32_t cut = before - p0 + 1;  // bits [0, cut) are covered
     const uint64_t keep_all =
         cut <= 0 ? cand : (cut >= kTokBytes ? 0ull : cand & ~((1ull << cut) - 1ull));
     int32_t blk_cnt;
+#if SME_TOK_V3
+    const int32_t base = tok_block_excl_sum<kTokNT, int32_t>(__popcll(keep_all), L.sc32, &blk_cnt);
+#else
     const int32_t base = block_excl_sum<kTokNT, int32_t>(__popcll(keep_all), L.sc32, &blk_cnt);
+#endif
     // c0: chunk rank of the first token of every record that starts in this lane
     for (int k = (j < 0 ? 0 : j); k < kRecWin && L.rs[k] < p0 + kTokBytes; k++)
       if (L.rs[k] >= p0) L.c0[k] = base + __popcll(keep_all & ((1ull << (L.rs[k] - p0)) - 1ull));
@@ -1193,7 +1249,11 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
     for (int32_t rlo = 0; rlo < ((texp & 16) ? 0 : blk_cnt); rlo += kTokCap) {  // (16: no token passes)
       const int32_t nr = min(kTokCap, blk_cnt - rlo);
       // pass 2: start positions of the round's tokens by chunk rank
+#if SME_TOK_V3
+      if (tid < kTokNT / 64) L.nmissw[tid] = 0;
+#else
       if (tid == 0) L.nmiss = 0;
+#endif
       {
         uint64_t keep = keep_all;
         int32_t idx = base - rlo;
@@ -1261,9 +1321,15 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
               // a new raw token (or a long / contended probe): inserted after the
               // probe pass, with the round's other inserts, so a wave waits on one
               // insert chain rather than on one per lane step
+#if SME_TOK_V3
+              const int k = atomicAdd(&L.nmissw[tid >> 6], 1);
+              if (k < kTokMiss / (kTokNT / 64))
+                L.miss[(tid >> 6) * (kTokMiss / (kTokNT / 64)) + k] = r;
+#else
               const int k = atomicAdd(&L.nmiss, 1);
               if (k < kTokMiss)
                 L.miss[k] = r;
+#endif
               else
 #if SME_TOK_V2
                 *dst = raw_insert(tb, g[u], (uint64_t)(c_lo + x[u]), (uint64_t)len[u], SlotVal{0, 0, 0, 0});
@@ -1274,11 +1340,22 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
           }
         }
       }
+#if SME_TOK_V3
+      // pass 3b per wave (its own deferred inserts, right after its probes: no
+      // block barrier; the noinline raw_insert re-reads the home slot coherently,
+      // concurrent inserts of one token resolve there)
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      constexpr int kMissW = kTokMiss / (kTokNT / 64);
+      for (int i = tid & 63; i < min(L.nmissw[tid >> 6], kMissW); i += 64) {
+        const int32_t r = L.miss[(tid >> 6) * kMissW + i];
+#else
       __syncthreads();
       // pass 3b: the deferred inserts (the noinline raw_insert re-reads the home
       // slot coherently; concurrent inserts of one token resolve there)
       for (int i = tid; i < min(L.nmiss, kTokMiss); i += kTokNT) {
         const int32_t r = L.miss[i];
+#endif
         const int32_t x = (int32_t)L.tl[r];
         TokSig g;
         int32_t len;
