@@ -819,6 +819,9 @@ constexpr int kTokMiss = SME_TOKMISS;  // deferred raw-vocabulary inserts per ro
 #ifndef SME_TOK_V3
 #define SME_TOK_V3 1
 #endif
+#ifndef SME_TOK_WIN
+#define SME_TOK_WIN 1
+#endif
 // V2: five workgroups per CU (its 31.3 KB of LDS) with one token per lane step in
 // the probe pass (96 VGPRs, no spills; two tokens per step spill at five):
 // c2 k_tok_fast 8.46 -> 7.87 ms
@@ -1069,10 +1072,20 @@ __global__ __launch_bounds__(kTokNT, SME_TOKOCC) void k_tok_fast(const uint8_t *
     const int64_t c_lo = Q - mis;  // chunk = positions c_lo + [0, kChunk)
     for (int i = tid; i < kRecWin; i += kTokNT) {
       const int64_t f = fcur + i;
+#if SME_TOK_V2 && SME_TOK_WIN
+      // (the record id is read only where a record ends: both bounds load
+      // independently, no rs -> re chain)
+      const bool in = f < f1;
+      const int64_t a = in ? (int64_t)rs_g[f] : INT64_MAX;
+      const int64_t b0 = in ? (int64_t)re_g[f] : INT64_MAX;
+      const bool ok = a < c_lo + kChunk;
+      const int64_t b = ok ? b0 : INT64_MAX;
+#else
       const int32_t r = f < f1 ? frec[f] : -1;
       const int64_t a = r >= 0 ? (int64_t)rs_g[f] : INT64_MAX;  // (independent loads: no frec -> rs chain)
       const bool ok = a < c_lo + kChunk;
       const int64_t b = ok ? (int64_t)re_g[f] : INT64_MAX;
+#endif
       L.rs[i] = ok ? (int32_t)max<int64_t>(a - c_lo, -1) : kFar;
       L.re[i] = ok ? (int32_t)min<int64_t>(b - c_lo, kFar) : kFar;
       if (i == 0) L.tbase0 = ok ? (a >> 1) : 0;
