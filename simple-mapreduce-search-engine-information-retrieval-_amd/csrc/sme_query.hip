@@ -2092,6 +2092,46 @@ __global__ __launch_bounds__(256) void k_heavy_imp3(const uint8_t *tfrow, const 
 // impact q(tf) at the index's scale and its tf (4095 = "4095 or more"), so the
 // window pass loads one word per posting and does no arithmetic on it.  One
 // wave per term; terms with a heavy row are skipped (the window pass reads rows).
+#ifndef SME_SPK_LANES
+#define SME_SPK_LANES 1
+#endif
+__device__ __forceinline__ uint32_t sparse_word(int32_t dn, int32_t f, const double *lut, double wi, double alpha,
+                                                int64_t dmin) {
+  return (uint32_t)(((int64_t)dn - dmin) & (kWin - 1)) | (impact(lut[f], wi, alpha) << 12) |
+         ((uint32_t)min(f, 0xFFF) << 20);
+}
+#if SME_SPK_LANES
+// 64 terms per wave step, one per lane: a term of <= kSpkSmall postings is packed
+// by its own lane (most terms: the Zipf tail and the df-1 docid terms), longer
+// ones by the whole wave in turn -- a wave per term spent a wave step and four
+// dependent loads on every one-posting term
+constexpr int kSpkSmall = 16;
+__global__ __launch_bounds__(256) void k_sparse_pack(const int64_t *off, int64_t V, const int32_t *hrow_of,
+                                                     const int32_t *docno, const int32_t *tf, const double *lut,
+                                                     const double *idf, double alpha, int64_t dmin, uint32_t *spk) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwv = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t t0 = (blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; t0 < V; t0 += nwv * 64) {
+    const int64_t t = t0 + lane;
+    int64_t b = 0, e = 0;
+    double wi = 0.0;
+    if (t < V && !(hrow_of && hrow_of[t] >= 0)) {
+      b = off[t];
+      e = off[t + 1];
+      wi = idf[t];
+    }
+    if (e - b <= kSpkSmall) {
+      for (int64_t i = b; i < e; i++) spk[i] = sparse_word(docno[i], tf[i], lut, wi, alpha, dmin);
+    }
+    for (uint64_t big = (uint64_t)__ballot(e - b > kSpkSmall); big; big &= big - 1) {  // (wave-uniform)
+      const int j = (int)__builtin_ctzll(big);
+      const int64_t bj = __shfl(b, j, 64), ej = __shfl(e, j, 64);
+      const double wj = __shfl(wi, j, 64);
+      for (int64_t i = bj + lane; i < ej; i += 64) spk[i] = sparse_word(docno[i], tf[i], lut, wj, alpha, dmin);
+    }
+  }
+}
+#else
 __global__ __launch_bounds__(256) void k_sparse_pack(const int64_t *off, int64_t V, const int32_t *hrow_of,
                                                      const int32_t *docno, const int32_t *tf, const double *lut,
                                                      const double *idf, double alpha, int64_t dmin, uint32_t *spk) {
@@ -2101,13 +2141,10 @@ __global__ __launch_bounds__(256) void k_sparse_pack(const int64_t *off, int64_t
     if (hrow_of && hrow_of[t] >= 0) continue;  // (wave-uniform)
     const int64_t b = off[t], e = off[t + 1];
     const double wi = idf[t];
-    for (int64_t i = b + lane; i < e; i += 64) {
-      const int32_t f = tf[i];
-      spk[i] = (uint32_t)(((int64_t)docno[i] - dmin) & (kWin - 1)) | (impact(lut[f], wi, alpha) << 12) |
-               ((uint32_t)min(f, 0xFFF) << 20);
-    }
+    for (int64_t i = b + lane; i < e; i += 64) spk[i] = sparse_word(docno[i], tf[i], lut, wi, alpha, dmin);
   }
 }
+#endif
 
 // largest weight of any term (its max tf is the first posting of the
 // reduce-order CSR): the index's impact scale alpha = 253.5 / wmax
@@ -2227,7 +2264,8 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     if (ix->d_spk.cap >= need || need <= (fr + cx->pool.idle()) / 4) {
       uint32_t *spk = ix->d_spk.as<uint32_t>((size_t)ix->P);
       const int32_t *hro = ix->q_H > 0 ? (const int32_t *)ix->d_hrow_of.p : nullptr;
-      hipLaunchKernelGGL(k_sparse_pack, dim3((unsigned)std::min<int64_t>((V + 3) / 4, 65536)), dim3(256), 0, st,
+      hipLaunchKernelGGL(k_sparse_pack, dim3((unsigned)std::min<int64_t>(SME_SPK_LANES ? (V + 255) / 256 : (V + 3) / 4, 65536)),
+                         dim3(256), 0, st,
                          (const int64_t *)ix->d_off.p, V, hro, (const int32_t *)ix->d_docno_d.p,
                          (const int32_t *)ix->d_tf_d.p, (const double *)ix->d_lut.p, (const double *)ix->d_idf.p,
                          ix->q_alpha, ix->dmin, spk);
