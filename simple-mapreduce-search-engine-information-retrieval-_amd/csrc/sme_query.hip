@@ -2102,13 +2102,16 @@ __device__ __forceinline__ uint32_t sparse_word(int32_t dn, int32_t f, const dou
 }
 #if SME_SPK_LANES
 // 64 terms per wave step, one per lane: a term of <= kSpkSmall postings is packed
-// by its own lane (most terms: the Zipf tail and the df-1 docid terms), longer
-// ones by the whole wave in turn -- a wave per term spent a wave step and four
-// dependent loads on every one-posting term
+// by its own lane (most terms: the Zipf tail and the df-1 docid terms); longer
+// ones are listed (one atomic per wave) for k_sparse_pack_big, a wave per term
+// over the whole grid (a wave per term for every term spent a wave step and four
+// dependent loads on each one-posting term; the listed terms packed by the wave
+// that met them clustered c5's word terms on a few waves)
 constexpr int kSpkSmall = 16;
 __global__ __launch_bounds__(256) void k_sparse_pack(const int64_t *off, int64_t V, const int32_t *hrow_of,
                                                      const int32_t *docno, const int32_t *tf, const double *lut,
-                                                     const double *idf, double alpha, int64_t dmin, uint32_t *spk) {
+                                                     const double *idf, double alpha, int64_t dmin, uint32_t *spk,
+                                                     int32_t *big_list, unsigned int *nbig) {
   const int lane = threadIdx.x & 63;
   const int64_t nwv = (int64_t)gridDim.x * (blockDim.x >> 6);
   for (int64_t t0 = (blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; t0 < V; t0 += nwv * 64) {
@@ -2123,12 +2126,26 @@ __global__ __launch_bounds__(256) void k_sparse_pack(const int64_t *off, int64_t
     if (e - b <= kSpkSmall) {
       for (int64_t i = b; i < e; i++) spk[i] = sparse_word(docno[i], tf[i], lut, wi, alpha, dmin);
     }
-    for (uint64_t big = (uint64_t)__ballot(e - b > kSpkSmall); big; big &= big - 1) {  // (wave-uniform)
-      const int j = (int)__builtin_ctzll(big);
-      const int64_t bj = __shfl(b, j, 64), ej = __shfl(e, j, 64);
-      const double wj = __shfl(wi, j, 64);
-      for (int64_t i = bj + lane; i < ej; i += 64) spk[i] = sparse_word(docno[i], tf[i], lut, wj, alpha, dmin);
+    const uint64_t bm = (uint64_t)__ballot(e - b > kSpkSmall);
+    if (bm) {
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(nbig, (unsigned int)__popcll(bm));
+      base = (unsigned int)__shfl((int)base, 0, 64);
+      if ((bm >> lane) & 1ull) big_list[base + __popcll(bm & ((1ull << lane) - 1ull))] = (int32_t)t;
     }
+  }
+}
+__global__ __launch_bounds__(256) void k_sparse_pack_big(const int64_t *off, const int32_t *docno, const int32_t *tf,
+                                                         const double *lut, const double *idf, double alpha,
+                                                         int64_t dmin, uint32_t *spk, const int32_t *big_list,
+                                                         const unsigned int *nbig) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwv = (int64_t)gridDim.x * (blockDim.x >> 6), n = (int64_t)*nbig;
+  for (int64_t w = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); w < n; w += nwv) {
+    const int64_t t = big_list[w];
+    const int64_t b = off[t], e = off[t + 1];
+    const double wi = idf[t];
+    for (int64_t i = b + lane; i < e; i += 64) spk[i] = sparse_word(docno[i], tf[i], lut, wi, alpha, dmin);
   }
 }
 #else
@@ -2264,11 +2281,25 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
     if (ix->d_spk.cap >= need || need <= (fr + cx->pool.idle()) / 4) {
       uint32_t *spk = ix->d_spk.as<uint32_t>((size_t)ix->P);
       const int32_t *hro = ix->q_H > 0 ? (const int32_t *)ix->d_hrow_of.p : nullptr;
-      hipLaunchKernelGGL(k_sparse_pack, dim3((unsigned)std::min<int64_t>(SME_SPK_LANES ? (V + 255) / 256 : (V + 3) / 4, 65536)),
-                         dim3(256), 0, st,
+#if SME_SPK_LANES
+      // (stream-ordered after the heavy-row kernels: their flag / scan slots are free)
+      int32_t *big_list = cx->ws[37].as<int32_t>(V + 1);
+      unsigned int *nbig = reinterpret_cast<unsigned int *>(cx->ws[35].as<uint64_t>(1));
+      SME_HIP(hipMemsetAsync(nbig, 0, sizeof(unsigned int), st));
+      hipLaunchKernelGGL(k_sparse_pack, dim3((unsigned)std::min<int64_t>((V + 255) / 256, 65536)), dim3(256), 0, st,
+                         (const int64_t *)ix->d_off.p, V, hro, (const int32_t *)ix->d_docno_d.p,
+                         (const int32_t *)ix->d_tf_d.p, (const double *)ix->d_lut.p, (const double *)ix->d_idf.p,
+                         ix->q_alpha, ix->dmin, spk, big_list, nbig);
+      hipLaunchKernelGGL(k_sparse_pack_big, dim3(16384), dim3(256), 0, st, (const int64_t *)ix->d_off.p,
+                         (const int32_t *)ix->d_docno_d.p, (const int32_t *)ix->d_tf_d.p, (const double *)ix->d_lut.p,
+                         (const double *)ix->d_idf.p, ix->q_alpha, ix->dmin, spk, (const int32_t *)big_list,
+                         (const unsigned int *)nbig);
+#else
+      hipLaunchKernelGGL(k_sparse_pack, dim3((unsigned)std::min<int64_t>((V + 3) / 4, 65536)), dim3(256), 0, st,
                          (const int64_t *)ix->d_off.p, V, hro, (const int32_t *)ix->d_docno_d.p,
                          (const int32_t *)ix->d_tf_d.p, (const double *)ix->d_lut.p, (const double *)ix->d_idf.p,
                          ix->q_alpha, ix->dmin, spk);
+#endif
       SME_CHECK_LAUNCH();
       ix->q_spk = spk;
     }
