@@ -2087,6 +2087,81 @@ __global__ __launch_bounds__(256) void k_heavy_imp3(const uint8_t *tfrow, const 
     sbq[i] = max_u8x4(o[0]) | (max_u8x4(o[1]) << 8) | (max_u8x4(o[2]) << 16) | (max_u8x4(o[3]) << 24);
   }
 }
+// SME_HEAVY_FUSED (default 1): the heavy rows in one pass -- a block per (row,
+// run of kHvWpb 4096-document windows) scatters the term's postings of each window
+// into a zeroed 4 KB LDS row and writes the window's tf bytes, impact bytes, 16-
+// document tf maxima and 4-document impact maxima densely from it (no row memset,
+// no byte-scatter into HBM, no second pass reading the tf rows back)
+#ifndef SME_HEAVY_FUSED
+#define SME_HEAVY_FUSED 1
+#endif
+constexpr int kHvWpb = 16;
+__global__ __launch_bounds__(256) void k_heavy_build(const int32_t *hterm, int64_t H, const int64_t *off,
+                                                     const int32_t *docno, const int32_t *tf, int64_t dmin,
+                                                     int64_t stride, const double *lut, int max_tf, const double *idf,
+                                                     double alpha, uint8_t *tfrow, uint8_t *imp, uint8_t *bm16,
+                                                     uint32_t *sbq) {
+  __shared__ uint8_t ql[256];
+  __shared__ alignas(16) uint8_t buf[kWin];
+  __shared__ int64_t s_cur;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t chunks = stride >> kWinB, nbr = (chunks + kHvWpb - 1) / kHvWpb;
+  for (int64_t bi = blockIdx.x; bi < H * nbr; bi += gridDim.x) {
+    const int64_t row = bi / nbr, c0 = (bi % nbr) * kHvWpb, c1 = min(chunks, c0 + kHvWpb);
+    const int64_t t = hterm[row], b = off[t], e = off[t + 1];
+    const double wi = idf[t];
+    __syncthreads();  // the previous run's LDS reads are done
+    ql[tid] = (uint8_t)(tid == 0 ? 0u : tid <= max_tf ? impact(lut[tid], wi, alpha) : 255u);
+    if (tid < 64) {
+      // first posting of the run: 64-ary lower bound of docno >= dmin + c0 * 4096
+      const int64_t target = dmin + (c0 << kWinB);
+      int64_t lo = b, hi = e;
+      while (lo < hi) {
+        const int64_t step = (hi - lo + 63) / 64, pos = lo + lane * step;
+        const uint64_t m = (uint64_t)__ballot(pos < hi && (int64_t)docno[pos] < target);
+        const int k = __popcll(m);
+        if (k == 0) {
+          hi = lo;
+        } else {
+          const int64_t nhi = min(hi, lo + k * step);
+          lo = lo + (k - 1) * step + 1;
+          hi = nhi;
+        }
+      }
+      if (tid == 0) s_cur = lo;
+    }
+    __syncthreads();
+    int64_t cur = s_cur;
+    for (int64_t c = c0; c < c1; c++) {
+      const int64_t wend = dmin + ((c + 1) << kWinB), wbase = wend - kWin;
+      reinterpret_cast<uint4 *>(buf)[tid] = make_uint4(0, 0, 0, 0);
+      __syncthreads();
+      // the window's postings are the next ones from the cursor (docno order)
+      for (;;) {
+        const int64_t i = cur + tid;
+        const bool in = i < e && (int64_t)docno[i] < wend;
+        if (in) buf[(int64_t)docno[i] - wbase] = (uint8_t)tf[i];
+        const int n = __syncthreads_count(in);
+        cur += n;
+        if (n < 256) break;
+      }
+      const uint4 v = reinterpret_cast<const uint4 *>(buf)[tid];
+      const int64_t fi = row * (stride >> 4) + (c << 8) + tid;  // flat 16-document block
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        o[u] = (uint32_t)ql[w4[u] & 0xFF] | ((uint32_t)ql[(w4[u] >> 8) & 0xFF] << 8) |
+               ((uint32_t)ql[(w4[u] >> 16) & 0xFF] << 16) | ((uint32_t)ql[w4[u] >> 24] << 24);
+      reinterpret_cast<uint4 *>(tfrow)[fi] = v;
+      reinterpret_cast<uint4 *>(imp)[fi] = make_uint4(o[0], o[1], o[2], o[3]);
+      bm16[fi] = (uint8_t)max(max(max_u8x4(v.x), max_u8x4(v.y)), max(max_u8x4(v.z), max_u8x4(v.w)));
+      sbq[fi] = max_u8x4(o[0]) | (max_u8x4(o[1]) << 8) | (max_u8x4(o[2]) << 16) | (max_u8x4(o[3]) << 24);
+      __syncthreads();  // buf is zeroed for the next window
+    }
+  }
+}
+
 // k_query_win's sparse posting words (index-resident, like the impact rows):
 // (docno - dmin) mod 4096 = the posting's place in its 4096-document window, its
 // impact q(tf) at the index's scale and its tf (4095 = "4095 or more"), so the
@@ -2253,13 +2328,20 @@ void prepare_queries(sme_index *ix, hipStream_t st) {
       uint8_t *buf = ix->d_heavy.as<uint8_t>((size_t)H * (size_t)per_row + 128);
       uint8_t *tfrow = buf, *imp = buf + H * stride, *bm16 = imp + H * stride, *bm1k = bm16 + H * (T << 6);
       uint8_t *sbq = bm1k + H * T + 64 - ((H * T) & 15);  // 16-byte aligned
+      const int64_t n16 = H * (T << 6), n1k = H * T;
+#if SME_HEAVY_FUSED
+      hipLaunchKernelGGL(k_heavy_build, dim3((unsigned)std::min<int64_t>(H * (((stride >> kWinB) + kHvWpb - 1) / kHvWpb), 1 << 16)),
+                         dim3(256), 0, st, hterm, H, off, (const int32_t *)ix->d_docno_d.p,
+                         (const int32_t *)ix->d_tf_d.p, ix->dmin, stride, (const double *)ix->d_lut.p, ix->max_tf,
+                         (const double *)ix->d_idf.p, ix->q_alpha, tfrow, imp, bm16, reinterpret_cast<uint32_t *>(sbq));
+#else
       SME_HIP(hipMemsetAsync(tfrow, 0, (size_t)(H * stride), st));
       hipLaunchKernelGGL(k_heavy_fill, dim3(16384), dim3(256), 0, st, hpre, H, hterm, off,
                          (const int32_t *)ix->d_docno_d.p, (const int32_t *)ix->d_tf_d.p, ix->dmin, stride, tfrow);
-      const int64_t n16 = H * (T << 6), n1k = H * T;
       hipLaunchKernelGGL(k_heavy_imp3, dim3((unsigned)std::min<int64_t>(H * (stride >> 12), 1 << 16)), dim3(256), 0, st,
                          tfrow, hterm, H, stride, (const double *)ix->d_lut.p, ix->max_tf,
                          (const double *)ix->d_idf.p, ix->q_alpha, imp, bm16, reinterpret_cast<uint32_t *>(sbq));
+#endif
       hipLaunchKernelGGL(k_heavy_bm1k, dim3((unsigned)std::min<int64_t>((n1k + 255) / 256, 1 << 16)), dim3(256), 0,
                          st, (const uint4 *)bm16, n1k, bm1k);
       SME_CHECK_LAUNCH();
