@@ -3286,10 +3286,12 @@ __global__ __launch_bounds__(NW * 64) void k_tfsort_block(const int64_t *__restr
     __syncthreads();
     const int64_t nch = (n + 63) >> 6, cpw = (nch + NW - 1) / NW;
     const int64_t c0 = (int64_t)w * cpw, c1 = c0 + cpw < nch ? c0 + cpw : nch;
+    int32_t tn = c0 < c1 && (c0 << 6) + lane < n ? tf_d[b + (c0 << 6) + lane] : -1;  // one chunk ahead
     for (int64_t c = c0; c < c1; c++) {
       const int64_t i = (c << 6) + lane;
       const bool v = i < n;
-      const int32_t t = v ? tf_d[b + i] : -1;
+      const int32_t t = tn;
+      tn = c + 1 < c1 && i + 64 < n ? tf_d[b + i + 64] : -1;
       uint64_t pend = __ballot(v);
       while (pend) {
         const int32_t tv = __shfl(t, __ffsll((unsigned long long)pend) - 1, 64);
@@ -3319,10 +3321,21 @@ __global__ __launch_bounds__(NW * 64) void k_tfsort_block(const int64_t *__restr
       base += c;
     }
     __syncthreads();
+    int32_t tn2 = -1, dn2 = 0;  // one chunk ahead
+    if (c0 < c1 && (c0 << 6) + lane < n) {
+      tn2 = tf_d[b + (c0 << 6) + lane];
+      dn2 = docno_d[b + (c0 << 6) + lane];
+    }
     for (int64_t c = c0; c < c1; c++) {
       const int64_t i = (c << 6) + lane;
       const bool v = i < n;
-      const int32_t t = v ? tf_d[b + i] : -1, d = v ? docno_d[b + i] : 0;
+      const int32_t t = tn2, d = dn2;
+      if (c + 1 < c1 && i + 64 < n) {
+        tn2 = tf_d[b + i + 64];
+        dn2 = docno_d[b + i + 64];
+      } else {
+        tn2 = -1;
+      }
       uint64_t pend = __ballot(v);
       while (pend) {
         const int32_t tv = __shfl(t, __ffsll((unsigned long long)pend) - 1, 64);
@@ -3415,9 +3428,11 @@ __global__ __launch_bounds__(256) void k_tf_tile_count(const int64_t *__restrict
     __builtin_amdgcn_wave_barrier();
     // per 64-posting chunk: one LDS add per distinct tf (ballot groups) -- most
     // postings have tf 1, and per-lane atomics on that one counter serialise
+    int32_t tn = b + lane < e ? tf_d[b + lane] : -1;  // the next chunk loads before this one is counted
     for (int64_t c = b; c < e; c += 64) {
       const bool v = c + lane < e;
-      const int32_t t = v ? tf_d[c + lane] : -1;
+      const int32_t t = tn;
+      tn = c + 64 + lane < e ? tf_d[c + 64 + lane] : -1;
       uint64_t pend = __ballot(v);
       while (pend) {
         const int32_t tv = __shfl(t, __ffsll((unsigned long long)pend) - 1, 64);
