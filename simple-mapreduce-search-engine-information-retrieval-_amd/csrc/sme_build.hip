@@ -29,6 +29,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <memory>
@@ -816,6 +817,9 @@ constexpr int kTokMiss = SME_TOKMISS;  // deferred raw-vocabulary inserts per ro
 #endif
 // SME_TOK_V3: one-barrier block scans and per-wave deferred inserts (no block
 // barrier between the probe pass and the inserts): c2 k_tok_fast 7.12 -> 6.88 ms
+#ifndef SME_D2H_PINNED
+#define SME_D2H_PINNED 1
+#endif
 #ifndef SME_TOK_V3
 #define SME_TOK_V3 1
 #endif
@@ -3543,8 +3547,20 @@ static int grid_for(int64_t n, int nt = 256, int cap = 8192) {
 template <typename T>
 static T d2h(const T *d, hipStream_t st) {
   T h;
+#if SME_D2H_PINNED
+  // through a small pinned buffer of the calling thread (a pageable destination
+  // takes the runtime's staged path: a longer stall per read-back, and the build
+  // reads back ~30 sizes)
+  static thread_local void *pin = nullptr;
+  if (!pin) SME_HIP(hipHostMalloc(&pin, 64, hipHostMallocDefault));
+  static_assert(sizeof(T) <= 64, "d2h");
+  SME_HIP(hipMemcpyAsync(pin, d, sizeof(T), hipMemcpyDeviceToHost, st));
+  SME_HIP(hipStreamSynchronize(st));
+  memcpy(&h, pin, sizeof(T));
+#else
   SME_HIP(hipMemcpyAsync(&h, d, sizeof(T), hipMemcpyDeviceToHost, st));
   SME_HIP(hipStreamSynchronize(st));
+#endif
   return h;
 }
 
