@@ -2088,64 +2088,73 @@ __global__ __launch_bounds__(256) void k_heavy_imp3(const uint8_t *tfrow, const 
   }
 }
 // SME_HEAVY_FUSED (default 1): the heavy rows in one pass -- a block per (row,
-// run of kHvWpb 4096-document windows) scatters the term's postings of each window
-// into a zeroed 4 KB LDS row and writes the window's tf bytes, impact bytes, 16-
-// document tf maxima and 4-document impact maxima densely from it (no row memset,
-// no byte-scatter into HBM, no second pass reading the tf rows back)
+// run of kHvWpb 4096-document windows) finds the run's postings (two 64-ary lower
+// bounds), scatters them into zeroed LDS rows (four loads per thread in flight)
+// and writes each window's tf bytes, impact bytes, 16-document tf maxima and
+// 4-document impact maxima densely from them (no row memset, no byte-scatter into
+// HBM, no second pass reading the tf rows back)
 #ifndef SME_HEAVY_FUSED
 #define SME_HEAVY_FUSED 1
 #endif
-constexpr int kHvWpb = 16;
+constexpr int kHvWpb = 8;  // windows per block: 32 KB of LDS rows
+// 64-ary lower bound (one wave): first p in [lo, hi) with docno[p] >= target
+__device__ __forceinline__ int64_t wave_lower_bound(const int32_t *docno, int64_t lo, int64_t hi, int64_t target,
+                                                    int lane) {
+  while (lo < hi) {
+    const int64_t step = (hi - lo + 63) / 64, pos = lo + lane * step;
+    const uint64_t m = (uint64_t)__ballot(pos < hi && (int64_t)docno[pos] < target);
+    const int k = __popcll(m);
+    if (k == 0) {
+      hi = lo;
+    } else {
+      const int64_t nhi = min(hi, lo + k * step);
+      lo = lo + (k - 1) * step + 1;
+      hi = nhi;
+    }
+  }
+  return lo;
+}
 __global__ __launch_bounds__(256) void k_heavy_build(const int32_t *hterm, int64_t H, const int64_t *off,
                                                      const int32_t *docno, const int32_t *tf, int64_t dmin,
                                                      int64_t stride, const double *lut, int max_tf, const double *idf,
                                                      double alpha, uint8_t *tfrow, uint8_t *imp, uint8_t *bm16,
                                                      uint32_t *sbq) {
   __shared__ uint8_t ql[256];
-  __shared__ alignas(16) uint8_t buf[kWin];
-  __shared__ int64_t s_cur;
-  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ alignas(16) uint8_t buf[kHvWpb * kWin];
+  __shared__ int64_t s_cur[2];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t chunks = stride >> kWinB, nbr = (chunks + kHvWpb - 1) / kHvWpb;
   for (int64_t bi = blockIdx.x; bi < H * nbr; bi += gridDim.x) {
     const int64_t row = bi / nbr, c0 = (bi % nbr) * kHvWpb, c1 = min(chunks, c0 + kHvWpb);
     const int64_t t = hterm[row], b = off[t], e = off[t + 1];
+    const int64_t wbase = dmin + (c0 << kWinB);
     const double wi = idf[t];
     __syncthreads();  // the previous run's LDS reads are done
     ql[tid] = (uint8_t)(tid == 0 ? 0u : tid <= max_tf ? impact(lut[tid], wi, alpha) : 255u);
-    if (tid < 64) {
-      // first posting of the run: 64-ary lower bound of docno >= dmin + c0 * 4096
-      const int64_t target = dmin + (c0 << kWinB);
-      int64_t lo = b, hi = e;
-      while (lo < hi) {
-        const int64_t step = (hi - lo + 63) / 64, pos = lo + lane * step;
-        const uint64_t m = (uint64_t)__ballot(pos < hi && (int64_t)docno[pos] < target);
-        const int k = __popcll(m);
-        if (k == 0) {
-          hi = lo;
-        } else {
-          const int64_t nhi = min(hi, lo + k * step);
-          lo = lo + (k - 1) * step + 1;
-          hi = nhi;
-        }
-      }
-      if (tid == 0) s_cur = lo;
+    for (int64_t c = c0; c < c1; c++) reinterpret_cast<uint4 *>(buf)[((c - c0) << 8) + tid] = make_uint4(0, 0, 0, 0);
+    // the run's postings: [lower bound of its first docno, lower bound past its last window)
+    if (wv < 2) {
+      const int64_t p = wave_lower_bound(docno, b, e, wv == 0 ? wbase : dmin + (c1 << kWinB), lane);
+      if (lane == 0) s_cur[wv] = p;
     }
     __syncthreads();
-    int64_t cur = s_cur;
-    for (int64_t c = c0; c < c1; c++) {
-      const int64_t wend = dmin + ((c + 1) << kWinB), wbase = wend - kWin;
-      reinterpret_cast<uint4 *>(buf)[tid] = make_uint4(0, 0, 0, 0);
-      __syncthreads();
-      // the window's postings are the next ones from the cursor (docno order)
-      for (;;) {
-        const int64_t i = cur + tid;
-        const bool in = i < e && (int64_t)docno[i] < wend;
-        if (in) buf[(int64_t)docno[i] - wbase] = (uint8_t)tf[i];
-        const int n = __syncthreads_count(in);
-        cur += n;
-        if (n < 256) break;
+    const int64_t p0 = s_cur[0], p1 = s_cur[1];
+    // scatter into the LDS rows, four postings per thread in flight
+    for (int64_t i0 = p0 + tid; i0 < p1; i0 += 4 * 256) {
+      int32_t d[4], f[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int64_t i = i0 + u * 256;
+        d[u] = i < p1 ? docno[i] : 0;
+        f[u] = i < p1 ? tf[i] : -1;
       }
-      const uint4 v = reinterpret_cast<const uint4 *>(buf)[tid];
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (f[u] >= 0) buf[(int64_t)d[u] - wbase] = (uint8_t)f[u];
+    }
+    __syncthreads();
+    for (int64_t c = c0; c < c1; c++) {
+      const uint4 v = reinterpret_cast<const uint4 *>(buf)[((c - c0) << 8) + tid];
       const int64_t fi = row * (stride >> 4) + (c << 8) + tid;  // flat 16-document block
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
       uint32_t o[4];
@@ -2157,7 +2166,6 @@ __global__ __launch_bounds__(256) void k_heavy_build(const int32_t *hterm, int64
       reinterpret_cast<uint4 *>(imp)[fi] = make_uint4(o[0], o[1], o[2], o[3]);
       bm16[fi] = (uint8_t)max(max(max_u8x4(v.x), max_u8x4(v.y)), max(max_u8x4(v.z), max_u8x4(v.w)));
       sbq[fi] = max_u8x4(o[0]) | (max_u8x4(o[1]) << 8) | (max_u8x4(o[2]) << 16) | (max_u8x4(o[3]) << 24);
-      __syncthreads();  // buf is zeroed for the next window
     }
   }
 }
