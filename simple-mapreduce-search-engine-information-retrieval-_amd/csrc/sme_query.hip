@@ -608,7 +608,15 @@ __global__ void k_row_wmax(const int32_t *term_of_row, const int64_t *rdf, int64
     const unsigned long long u = __shfl_xor(wm, o, 64);
     wm = u > wm ? u : wm;
   }
-  if ((threadIdx.x & 63) == 0 && wm) atomicMax(wmax_bits, wm);
+  // one atomic per block, and only when it can raise the maximum (single-address
+  // atomics serialise: one per wave took ~0.2 ms on c2's 2 M terms)
+  __shared__ unsigned long long s_wm[4];
+  if ((threadIdx.x & 63) == 0) s_wm[threadIdx.x >> 6] = wm;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); i++) wm = s_wm[i] > wm ? s_wm[i] : wm;
+    if (wm && wm > __hip_atomic_load(wmax_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(wmax_bits, wm);
+  }
 }
 // impact table of every batch row: q(tf) for tf < 256 (0 for tf = 0; tf above
 // the index's largest tf never occurs)
@@ -2248,7 +2256,7 @@ __global__ __launch_bounds__(256) void k_sparse_pack(const int64_t *off, int64_t
 
 // largest weight of any term (its max tf is the first posting of the
 // reduce-order CSR): the index's impact scale alpha = 253.5 / wmax
-__global__ void k_index_wmax(const int64_t *off, int64_t V, const int32_t *tf_o, const double *lut,
+__global__ __launch_bounds__(256) void k_index_wmax(const int64_t *off, int64_t V, const int32_t *tf_o, const double *lut,
                              const double *idf, unsigned long long *wmax_bits) {
   unsigned long long wm = 0;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < V; t += (int64_t)gridDim.x * blockDim.x) {
@@ -2262,7 +2270,15 @@ __global__ void k_index_wmax(const int64_t *off, int64_t V, const int32_t *tf_o,
     const unsigned long long u = __shfl_xor(wm, o, 64);
     wm = u > wm ? u : wm;
   }
-  if ((threadIdx.x & 63) == 0 && wm) atomicMax(wmax_bits, wm);
+  // one atomic per block, and only when it can raise the maximum (single-address
+  // atomics serialise: one per wave took ~0.2 ms on c2's 2 M terms)
+  __shared__ unsigned long long s_wm[4];
+  if ((threadIdx.x & 63) == 0) s_wm[threadIdx.x >> 6] = wm;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); i++) wm = s_wm[i] > wm ? s_wm[i] : wm;
+    if (wm && wm > __hip_atomic_load(wmax_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(wmax_bits, wm);
+  }
 }
 
 // Index-resident query structures, built once per index and heavy threshold:
